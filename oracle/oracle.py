@@ -1,0 +1,229 @@
+"""ctypes front-end of the C restatement (``oracle/liboracle.so``).
+
+TEST INFRASTRUCTURE ONLY: imported by ``tests/``, ``__graft_entry__.smoke()`` and
+``bench.py``'s cpu_baseline leg, never by the product package.  Every array is numpy;
+states are ``uint64[n, 8]`` packed words (``oracle/spec.py``).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+from . import spec
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboracle.so")
+ASIZE = spec.ACTION_SIZE
+
+_lib = None
+
+
+def build(force: bool = False) -> str:
+    if force or not os.path.exists(LIB_PATH) or \
+            os.path.getmtime(LIB_PATH) < os.path.getmtime(os.path.join(HERE, "yk_oracle.c")):
+        subprocess.run(["make", "-C", HERE, "-B" if force else "all"], check=True,
+                       stdout=subprocess.DEVNULL)
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        _lib = C.CDLL(LIB_PATH)
+        _lib.or_net_create.restype = C.c_void_p
+        _lib.or_net_create.argtypes = [C.c_int, C.c_int, C.POINTER(C.c_void_p)]
+        _lib.or_net_destroy.argtypes = [C.c_void_p]
+        _lib.or_net_predict.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+        _lib.or_net_forward_x.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+        _lib.or_draw64.restype = C.c_uint64
+        _lib.or_draw64.argtypes = [C.c_uint64, C.c_uint32, C.c_uint64]
+        _lib.or_pairwise_sum.restype = C.c_float
+        _lib.or_pairwise_sum.argtypes = [C.c_void_p, C.c_long]
+        _lib.or_selfplay.restype = C.c_int
+        _lib.or_selfplay.argtypes = [C.c_int, C.c_void_p, C.c_uint64, C.c_int, C.c_double, C.c_int, C.c_int,
+                                     C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                     C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                     C.c_void_p, C.c_void_p, C.c_int]
+        for name in ("or_step", "or_valid", "or_ended", "or_canonical", "or_featurize", "or_score_table",
+                     "or_score_dice", "or_key_hash_batch", "or_hash_prior", "or_init_board", "or_draws"):
+            getattr(_lib, name).restype = None
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def _w(states):
+    return np.ascontiguousarray(np.asarray(states, dtype=np.uint64).reshape(-1, 8))
+
+
+def _i32(x, n):
+    return np.ascontiguousarray(np.broadcast_to(np.asarray(x, dtype=np.int32), (n,)))
+
+
+def step(states, players, actions, seed, envs, ctr):
+    w = _w(states)
+    n = len(w)
+    out = np.zeros_like(w)
+    npl = np.zeros(n, dtype=np.int32)
+    st = np.zeros(n, dtype=np.int8)
+    c = np.ascontiguousarray(np.broadcast_to(np.asarray(ctr, dtype=np.uint64), (n,))).copy()
+    e = np.ascontiguousarray(np.broadcast_to(np.asarray(envs, dtype=np.uint32), (n,)))
+    lib().or_step(_p(w), _p(_i32(players, n)), _p(_i32(actions, n)), C.c_uint64(seed), _p(e), _p(c),
+                  _p(out), _p(npl), _p(st), C.c_int(n))
+    return out, npl, st, c
+
+
+def valid(states, players):
+    w = _w(states)
+    n = len(w)
+    out = np.zeros((n, ASIZE), dtype=np.uint8)
+    cnt = np.zeros(n, dtype=np.int32)
+    lib().or_valid(_p(w), _p(_i32(players, n)), _p(out), _p(cnt), C.c_int(n))
+    return out, cnt
+
+
+def ended(states, players):
+    w = _w(states)
+    n = len(w)
+    r = np.zeros(n, dtype=np.float64)
+    tot = np.zeros((n, 2), dtype=np.int32)
+    lib().or_ended(_p(w), _p(_i32(players, n)), _p(r), _p(tot), C.c_int(n))
+    return r, tot
+
+
+def canonical(states, players):
+    w = _w(states)
+    out = np.zeros_like(w)
+    lib().or_canonical(_p(w), _p(_i32(players, len(w))), _p(out), C.c_int(len(w)))
+    return out
+
+
+def featurize(states):
+    w = _w(states)
+    x = np.zeros((len(w), 59), dtype=np.float32)
+    lib().or_featurize(_p(w), _p(x), C.c_int(len(w)))
+    return x
+
+
+def score_table(states, players):
+    w = _w(states)
+    out = np.zeros((len(w), 12, 252), dtype=np.int32)
+    lib().or_score_table(_p(w), _p(_i32(players, len(w))), _p(out), C.c_int(len(w)))
+    return out
+
+
+def score_dice(dice):
+    d = np.ascontiguousarray(np.asarray(dice, dtype=np.int8).reshape(-1, 5))
+    out = np.zeros((len(d), 12), dtype=np.int32)
+    lib().or_score_dice(_p(d), _p(out), C.c_int(len(d)))
+    return out
+
+
+def key_hash(states):
+    w = _w(states)
+    out = np.zeros(len(w), dtype=np.uint64)
+    lib().or_key_hash_batch(_p(w), _p(out), C.c_int(len(w)))
+    return out
+
+
+def hash_prior(states):
+    w = _w(states)
+    pi = np.zeros((len(w), ASIZE), dtype=np.float32)
+    v = np.zeros(len(w), dtype=np.float32)
+    lib().or_hash_prior(_p(w), _p(pi), _p(v), C.c_int(len(w)))
+    return pi, v
+
+
+def init_board(seed, envs, ctr=0):
+    e = np.ascontiguousarray(np.asarray(envs, dtype=np.uint32).reshape(-1))
+    c = np.ascontiguousarray(np.broadcast_to(np.asarray(ctr, dtype=np.uint64), e.shape)).copy()
+    out = np.zeros((len(e), 8), dtype=np.uint64)
+    lib().or_init_board(C.c_uint64(seed), _p(e), _p(c), _p(out), C.c_int(len(e)))
+    return out, c
+
+
+def draws(seed, env, ctr0, n):
+    out = np.zeros(n, dtype=np.uint64)
+    lib().or_draws(C.c_uint64(seed), C.c_uint32(env), C.c_uint64(ctr0), _p(out), C.c_int(n))
+    return out
+
+
+def pairwise_sum(a):
+    a = np.ascontiguousarray(a, dtype=np.float32)
+    return np.float32(lib().or_pairwise_sum(_p(a), C.c_long(len(a))))
+
+
+class Net:
+    """C restatement of YachtNNet.forward + exp(log_softmax) (NNet.py:177-195)."""
+
+    def __init__(self, state_dict, hidden, nblocks):
+        self._keep = [np.ascontiguousarray(np.asarray(v, dtype=np.float32)) for v in state_dict.values()]
+        arr = (C.c_void_p * len(self._keep))(*[a.ctypes.data for a in self._keep])
+        self.h = lib().or_net_create(hidden, nblocks, arr)
+        self.hidden, self.nblocks = hidden, nblocks
+
+    def predict_states(self, states):
+        w = _w(states)
+        pi = np.zeros((len(w), ASIZE), dtype=np.float32)
+        v = np.zeros(len(w), dtype=np.float32)
+        lib().or_net_predict(C.c_void_p(self.h), _p(w), _p(pi), _p(v), C.c_int(len(w)))
+        return pi, v
+
+    def forward_x(self, x):
+        x = np.ascontiguousarray(x, dtype=np.float32).reshape(-1, 59)
+        pi = np.zeros((len(x), ASIZE), dtype=np.float32)
+        v = np.zeros(len(x), dtype=np.float32)
+        lib().or_net_forward_x(C.c_void_p(self.h), _p(x), _p(pi), _p(v), C.c_int(len(x)))
+        return pi, v
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib().or_net_destroy(C.c_void_p(self.h))
+                self.h = None
+        except Exception:
+            pass
+
+
+MODE_HASH, MODE_MLP, MODE_REPLAY = 0, 1, 2
+
+
+def selfplay(envs, seed, sims, cpuct=1.5, temp_threshold=15, mode=MODE_HASH, net=None, replay=None,
+             max_moves=64, want_counts=True, threads=1):
+    """Coach.executeEpisode for each env id (fresh MCTS per game, Coach.py:93).
+
+    replay: list (per env) of (pi f32[k,3226], v f32[k]) predictions consumed in call order.
+    Returns a dict of numpy arrays (see ep_out_t in yk_oracle.c)."""
+    e = np.ascontiguousarray(np.asarray(envs, dtype=np.uint32).reshape(-1))
+    n = len(e)
+    M = max_moves
+    canon = np.zeros((n, M, 8), dtype=np.uint64)
+    mv = np.zeros((n, M, 8), dtype=np.int32)
+    ctr = np.zeros((n, M, 2), dtype=np.uint64)
+    counts = np.zeros((n, M, ASIZE), dtype=np.int32) if want_counts else None
+    values = np.zeros((n, M), dtype=np.float64)
+    stats = np.zeros((n, 8), dtype=np.int64)
+    final = np.zeros((n, 8), dtype=np.uint64)
+    rpi = rv = rn = None
+    keep = []
+    if mode == MODE_REPLAY:
+        pis = [np.ascontiguousarray(p, dtype=np.float32) for p, _ in replay]
+        vs = [np.ascontiguousarray(v, dtype=np.float32) for _, v in replay]
+        keep += pis + vs
+        rpi = (C.c_void_p * n)(*[p.ctypes.data for p in pis])
+        rv = (C.c_void_p * n)(*[v.ctypes.data for v in vs])
+        rn_arr = np.array([len(v) for v in vs], dtype=np.int64)
+        keep.append(rn_arr)
+        rn = _p(rn_arr)
+    nerr = lib().or_selfplay(n, _p(e), C.c_uint64(seed), sims, C.c_double(cpuct), temp_threshold, M, mode,
+                             C.c_void_p(net.h if net is not None else None), rpi, rv, rn,
+                             _p(canon), _p(mv), _p(ctr), _p(counts) if counts is not None else None,
+                             _p(values), _p(stats), _p(final), threads)
+    return dict(canon=canon, mv=mv, ctr=ctr, counts=counts, values=values, stats=stats, final=final,
+                nerr=nerr)

@@ -1,0 +1,364 @@
+"""Generate the golden fixtures under tests/golden/ by running the REFERENCE itself.
+
+Run only in the build container (the reference does not exist on the GPU box):
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+
+The reference (``/root/reference``) is imported read-only and driven through its own
+public surface - ``YachtGame``, ``score_category``, ``state_to_vec``,
+``NNetWrapper.predict``, ``MCTS``, ``Coach.executeEpisode`` - with exactly four
+process-global RNG entry points replaced by the per-game stream of
+``oracle/spec.py`` (``yacht.YachtGame.roll_five``, ``yacht.YachtGame.tiebreak_uniform``,
+``numpy.random.choice``; ``YachtGame.py:154-159``, ``MCTS.py:46``, ``Coach.py:65``).
+``np.random.choice(n, p=...)`` is re-stated exactly as numpy's legacy
+``RandomState.choice`` computes it (cumsum / normalise / searchsorted right) with the
+uniform draw taken from the stream.  Only data (inputs and outputs) is written.
+"""
+from __future__ import annotations
+
+import os
+import random as pyrandom
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = os.environ.get("YK_REFERENCE", "/root/reference")
+sys.path.insert(0, REPO)
+sys.path.insert(0, REF)
+sys.dont_write_bytecode = True
+
+from oracle import spec  # noqa: E402
+
+import yacht.YachtGame as YG  # noqa: E402
+from yacht.YachtGame import YachtGame, YachtState, PlayerState, score_category  # noqa: E402
+
+# ------------------------------------------------------------------ RNG patching
+_STREAM = [spec.Stream(0, 0)]
+_orig_choice = np.random.choice
+
+
+def _roll_five():
+    s = _STREAM[0]
+    return [s.die() for _ in range(5)]
+
+
+def _tiebreak():
+    return _STREAM[0].below(2)
+
+
+def _choice(a, size=None, replace=True, p=None):
+    assert size is None and replace
+    s = _STREAM[0]
+    arr = None if isinstance(a, (int, np.integer)) else np.asarray(a)
+    n = int(a) if arr is None else len(arr)
+    if p is None:
+        idx = s.below(n)
+    else:
+        # numpy/random/mtrand.pyx RandomState.choice, p-branch, size=None
+        pp = np.asarray(p, dtype=np.float64)
+        cdf = pp.cumsum()
+        cdf /= cdf[-1]
+        idx = int(cdf.searchsorted(s.uniform53(), side="right"))
+    return idx if arr is None else arr[idx]
+
+
+YG.roll_five = _roll_five
+YG.tiebreak_uniform = _tiebreak
+np.random.choice = _choice
+
+
+def set_stream(seed, env, ctr=0):
+    _STREAM[0] = spec.Stream(seed, env, ctr)
+
+
+def words(s):
+    return spec.pack_state(s)
+
+
+# ------------------------------------------------------------------ 1. score table
+def make_score_table():
+    import itertools
+    dice = np.array(list(itertools.product(range(1, 7), repeat=5)), dtype=np.int8)
+    out = np.zeros((len(dice), 12), dtype=np.int32)
+    for i, d in enumerate(dice):
+        dl = [int(x) for x in d]
+        for c in range(12):
+            out[i, c] = score_category(c, dl)
+    return dice, out
+
+
+# ------------------------------------------------------------------ 2. env transitions
+STATUS = {None: 0, "ValueError-bid": 1, "ValueError-score": 2, "RuntimeError": 3, "AssertionError": 4}
+
+
+def _apply(game, s, player, action):
+    try:
+        ns, npl = game.getNextState(s, player, action)
+        return ns, npl, 0
+    except ValueError as e:
+        return None, 0, (1 if "BID" in str(e) else 2)
+    except RuntimeError:
+        return None, 0, 3
+    except AssertionError:
+        return None, 0, 4
+
+
+def make_transitions(seed=7, n_games=60):
+    """Real-play walks, MCTS-style (player=1 + canonical) walks and error cases."""
+    game = YachtGame()
+    rnd = pyrandom.Random(seed)
+    rec = dict(state=[], player=[], action=[], ctr=[], env=[], next_state=[], next_player=[],
+               status=[], ctr_after=[])
+    states = {}  # words tuple -> YachtState (for per-state fixtures)
+
+    def record(s, player, action, env):
+        ctr = _STREAM[0].ctr
+        ns, npl, st = _apply(game, s, player, action)
+        rec["state"].append(words(s))
+        rec["player"].append(player)
+        rec["action"].append(action)
+        rec["ctr"].append(ctr)
+        rec["env"].append(env)
+        rec["next_state"].append(words(ns) if ns is not None else [0] * 8)
+        rec["next_player"].append(npl)
+        rec["status"].append(st)
+        rec["ctr_after"].append(_STREAM[0].ctr)
+        states.setdefault(tuple(words(s)), s)
+        if ns is not None:
+            states.setdefault(tuple(words(ns)), ns)
+        return ns, npl, st
+
+    def valid_list(s, player):
+        return [int(a) for a in np.nonzero(game.getValidMoves(s, player))[0]]
+
+    for g in range(n_games):
+        env = 1000 + g
+        set_stream(seed, env)
+        s = game.getInitBoard()
+        player = 1
+        step = 0
+        while game.getGameEnded(s, player) == 0:
+            step += 1
+            va = valid_list(s, player)
+            # occasionally exercise an illegal / out-of-phase action first (no state change)
+            r = rnd.random()
+            if r < 0.04:
+                record(s, player, rnd.randrange(202, 3226) if va[0] < 202 else rnd.randrange(0, 202), env)
+            elif r < 0.08 and va and va[0] >= 202:
+                record(s, player, rnd.randrange(202, 3226), env)  # often used-cat / bad combo
+            # MCTS-style side walk: player 1 + canonical until dead or terminal
+            if rnd.random() < 0.35:
+                saved = _STREAM[0].ctr
+                t = game.getCanonicalForm(s, player)
+                for _ in range(12):
+                    vt = valid_list(t, 1)
+                    if not vt or game.getGameEnded(t, 1) != 0:
+                        break
+                    t2, p2, st = record(t, 1, rnd.choice(vt), env)
+                    t = game.getCanonicalForm(t2, p2)
+                _STREAM[0].ctr = saved + 1000003  # keep side-walk draws disjoint
+            if va and va[0] < 202 and rnd.random() < 0.3:
+                # equal-target, equal-amount bids to force tiebreak draws
+                a = rnd.choice(va) if s.p1_bid is None and s.p2_bid is None else None
+                if a is None:
+                    pend = s.p1_bid if s.p1_bid is not None else s.p2_bid
+                    a = (0 if pend[0] == "A" else 1) * 101 + pend[1] // 500
+            else:
+                a = rnd.choice(va)
+            s, player, st = record(s, player, a, env)
+            assert st == 0
+        states.setdefault(tuple(words(s)), s)
+
+    # hand-made error cases
+    set_stream(seed, 99)
+    s = YachtState(round_no=13, phase=0, rollA=[1, 2, 3, 4, 5], rollB=[6, 6, 6, 6, 6],
+                   p1=PlayerState(carry=[1, 2, 3, 4, 5]), p2=PlayerState(carry=[2, 2, 2, 2, 2]))
+    record(s, 1, 5, 99)      # RuntimeError: BID phase in round 13
+    s = YachtState(round_no=3, phase=0, rollA=[1, 2, 3, 4, 5], rollB=[6, 6, 6, 6, 6],
+                   p1_bid=("A", 1000), p1=PlayerState(carry=[1, 2, 3, 4, 5]),
+                   p2=PlayerState(carry=[2, 2, 2, 2, 2]))
+    record(s, 1, 7, 99)      # AssertionError: same bidder twice
+    s = YachtState(round_no=1, phase=0, rollA=[1, 1, 1, 1, 1], rollB=[2, 2, 2, 2, 2])
+    s1, p1, _ = record(s, 1, 101 + 40, 99)
+    record(s1, p1, 101 + 40, 99)  # tie on B with equal amounts -> tiebreak draw
+    s = YachtState(round_no=12, phase=1, rollA=[1, 2, 3, 4, 5], rollB=[6, 6, 6, 6, 6],
+                   p1=PlayerState(carry=[6, 6, 6, 6, 6], used_mask=0x7FF),
+                   p2=PlayerState(carry=[1, 2, 3, 4, 5, 6, 6, 6, 6, 6], used_mask=0x7FF))
+    record(s, -1, 202 + 11 * 252 + 251, 99)  # round 12 -> 13: no re-roll, phase SCORE
+
+    return ({k: np.array(v, dtype=np.uint64 if "state" in k or k.startswith("ctr") else np.int64)
+             for k, v in rec.items()}, states)
+
+
+def make_state_fixtures(game, states):
+    from yacht.NNet import state_to_vec
+    keys = sorted(states.keys())
+    W = np.array(keys, dtype=np.uint64)
+    n = len(keys)
+    valid = np.zeros((n, 2, 3226), dtype=np.uint8)
+    ended = np.zeros((n, 2), dtype=np.float64)
+    canon = np.zeros((n, 8), dtype=np.uint64)
+    feat = np.zeros((n, 59), dtype=np.float32)
+    totals = np.zeros((n, 2), dtype=np.int64)
+    strs = []
+    for i, k in enumerate(keys):
+        s = states[k]
+        for j, p in enumerate((1, -1)):
+            valid[i, j] = game.getValidMoves(s, p)
+            ended[i, j] = game.getGameEnded(s, p)
+        canon[i] = words(game.getCanonicalForm(s, -1))
+        feat[i] = state_to_vec(game, s)
+        totals[i] = (s.p1.total_with_bonus(), s.p2.total_with_bonus())
+        strs.append(game.stringRepresentation(s))
+    assert len(set(strs)) == n, "packing is not injective w.r.t. stringRepresentation"
+    return dict(states=W, valid=np.packbits(valid, axis=-1, bitorder="little"), ended=ended,
+                canon=canon, feat=feat, totals=totals)
+
+
+# ------------------------------------------------------------------ 3. predict
+def make_predict(game, states, hidden, nblocks, n_states=32):
+    import torch
+    from utils import dotdict
+    from yacht.NNet import NNetWrapper, state_to_vec
+    torch.set_num_threads(4)
+    args = dotdict(dict(lr=2e-3, weight_decay=1e-4, epochs=1, batch_size=64, vloss_weight=1.5,
+                        cuda=False, hidden=hidden, nblocks=nblocks, dropout=0.3))
+    w = NNetWrapper(game, args)
+    sd = spec.closed_form_weights(hidden, nblocks)
+    w.nnet.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    keys = sorted(states.keys())
+    rnd = pyrandom.Random(hidden * 31 + nblocks)
+    pick = sorted(rnd.sample(range(len(keys)), n_states))
+    W = np.array([keys[i] for i in pick], dtype=np.uint64)
+    X = np.stack([state_to_vec(game, states[keys[i]]) for i in pick])
+    PI = np.zeros((n_states, 3226), dtype=np.float32)
+    V = np.zeros((n_states,), dtype=np.float32)
+    for j, i in enumerate(pick):
+        pi, v = w.predict(states[keys[i]])
+        PI[j], V[j] = pi, v
+    return dict(states=W, x=X, pi=PI, v=V, hidden=np.int64(hidden), nblocks=np.int64(nblocks))
+
+
+# ------------------------------------------------------------------ 4. self-play episodes
+class HashNet:
+    """``NeuralNet`` stand-in (NeuralNet.py:14-50) returning ``spec.hash_prior``."""
+
+    def __init__(self, game, args=None):
+        self.game = game
+        self.calls = 0
+
+    def predict(self, board):
+        self.calls += 1
+        return spec.hash_prior(words(board))
+
+
+def run_episode(seed, env, sims, cpuct=1.5, temp_threshold=15):
+    from utils import dotdict
+    from Coach import Coach
+    from MCTS import MCTS
+    game = YachtGame()
+    args = dotdict(dict(numMCTSSims=sims, cpuct=cpuct, tempThreshold=temp_threshold))
+    set_stream(seed, env)
+    nnet = HashNet(game)
+    coach = Coach(game, nnet, args)
+    coach.mcts = MCTS(game, nnet, args)
+    mcts = coach.mcts
+    moves = []
+    in_search = [False]
+    orig_gap = mcts.getActionProb
+    orig_next = game.getNextState
+
+    def gap(canonical, temp=1):
+        in_search[0] = True
+        ctr0 = _STREAM[0].ctr
+        pi = orig_gap(canonical, temp=temp)
+        in_search[0] = False
+        key = game.stringRepresentation(canonical)
+        counts = [(a, mcts.Nsa[(key, a)]) for a in range(3226) if (key, a) in mcts.Nsa]
+        moves.append(dict(canon=words(canonical), temp=temp, counts=counts, ctr_search=ctr0,
+                          n_ps=len(mcts.Ps), n_es=len(mcts.Es), n_sa=len(mcts.Nsa),
+                          root_ns=mcts.Ns.get(key, -1),
+                          pi_nz=[(a, float(p)) for a, p in enumerate(pi) if p != 0]))
+        return pi
+
+    def nxt(board, player, action):
+        if not in_search[0]:
+            moves[-1].update(player=player, action=int(action), ctr_step=_STREAM[0].ctr)
+        return orig_next(board, player, action)
+
+    mcts.getActionProb = gap
+    game.getNextState = nxt
+    t0 = time.time()
+    examples = coach.executeEpisode()
+    dt = time.time() - t0
+    assert len(examples) == len(moves)
+    return dict(seed=seed, env=env, sims=sims, cpuct=cpuct, temp_threshold=temp_threshold,
+                moves=moves, values=[float(e[2]) for e in examples], ctr_end=_STREAM[0].ctr,
+                expansions=nnet.calls, nodes=len(mcts.Es), seconds=dt)
+
+
+def pack_episodes(eps):
+    """Flatten episode dicts into fixed arrays (npz-friendly)."""
+    out = {}
+    nm = max(len(e["moves"]) for e in eps)
+    E = len(eps)
+    out["meta"] = np.array([[e["seed"], e["env"], e["sims"], e["temp_threshold"], len(e["moves"]),
+                             e["ctr_end"], e["expansions"], e["nodes"]] for e in eps], dtype=np.int64)
+    out["cpuct"] = np.array([e["cpuct"] for e in eps], dtype=np.float64)
+    canon = np.zeros((E, nm, 8), dtype=np.uint64)
+    mv = np.zeros((E, nm, 8), dtype=np.int64)  # temp, player, action, ctr_search, ctr_step, n_ps, root_ns, ncounts
+    vals = np.zeros((E, nm), dtype=np.float64)
+    cnt_a, cnt_n, cnt_off = [], [], np.zeros((E, nm + 1), dtype=np.int64)
+    k = 0
+    for i, e in enumerate(eps):
+        for j, m in enumerate(e["moves"]):
+            canon[i, j] = m["canon"]
+            mv[i, j] = [m["temp"], m["player"], m["action"], m["ctr_search"], m["ctr_step"], m["n_ps"],
+                        m["root_ns"], len(m["counts"])]
+            cnt_off[i, j] = k
+            for a, n in m["counts"]:
+                cnt_a.append(a)
+                cnt_n.append(n)
+                k += 1
+            vals[i, j] = e["values"][j]
+        cnt_off[i, len(e["moves"]):] = k
+    out.update(canon=canon, moves=mv, values=vals, count_action=np.array(cnt_a, dtype=np.int32),
+               count_n=np.array(cnt_n, dtype=np.int32), count_off=cnt_off)
+    return out
+
+
+def main():
+    t0 = time.time()
+    dice, table = make_score_table()
+    np.savez_compressed(os.path.join(HERE, "score_table.npz"), dice=dice, score=table)
+    print("score table", table.shape, f"{time.time() - t0:.1f}s")
+
+    tr, states = make_transitions()
+    np.savez_compressed(os.path.join(HERE, "transitions.npz"), seed=np.uint64(7), **tr)
+    print("transitions", len(tr["action"]), "states", len(states), f"{time.time() - t0:.1f}s")
+    game = YachtGame()
+    sf = make_state_fixtures(game, states)
+    np.savez_compressed(os.path.join(HERE, "states.npz"), **sf)
+    print("state fixtures", len(sf["states"]), f"{time.time() - t0:.1f}s")
+
+    for hidden, nblocks in ((256, 6), (64, 1)):
+        pf = make_predict(game, states, hidden, nblocks)
+        np.savez_compressed(os.path.join(HERE, f"predict_h{hidden}_b{nblocks}.npz"), **pf)
+        print("predict", hidden, nblocks, f"{time.time() - t0:.1f}s")
+
+    eps = []
+    for env, sims, cpuct, tt in ((0, 25, 1.5, 15), (1, 25, 1.5, 15), (2, 25, 1.5, 15), (3, 8, 1.5, 15),
+                                 (4, 2, 1.5, 15), (5, 25, 1.0, 49), (6, 100, 1.5, 15)):
+        ep = run_episode(20251015, env, sims, cpuct, tt)
+        eps.append(ep)
+        print(f"episode env={env} sims={sims}: {len(ep['moves'])} moves, {ep['expansions']} expansions, "
+              f"{ep['nodes']} nodes, {ep['seconds']:.1f}s")
+    np.savez_compressed(os.path.join(HERE, "episodes_hash.npz"), **pack_episodes(eps))
+    print(f"done in {time.time() - t0:.1f}s")
+
+
+if __name__ == "__main__":
+    main()
