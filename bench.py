@@ -1,0 +1,189 @@
+#!/usr/bin/env python3
+"""Benchmark: batched Yacht Auction self-play on MI355X.
+
+One step = one complete self-play episode batch: ``--envs`` games (default 4096) per GPU,
+each running ``--sims`` (default 100) MCTS simulations per real move over all 48 moves
+(Coach.executeEpisode -> MCTS.getActionProb -> MCTS.search, all on the GPU), followed by
+the RCCL all-gather of the trajectory records when N > 1.
+
+Metric (BASELINE.json): MCTS node-expansions/sec (one expansion = one NNetWrapper.predict
+of the reference = one new MCTS.Ps entry), whole job, plus episodes/s.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+Prints ONE JSON line on rank 0.  Data: synthetic (games from seeded streams), random-init
+YachtNNet (kaiming-uniform per YachtNNet._init, seed 0, hidden 256, 6 blocks).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "nypc-yacht-auction_amd"))
+sys.path.insert(0, REPO)
+
+METRIC = "MCTS node-expansions/sec/GPU @4096 envs x100 sims; episodes/sec 1-8 GPU"
+F32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense f32 matrix peak
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E spec peak
+H, NB, A = 256, 6, 3226
+# algorithmic FLOPs per expansion (per predicted row), YachtNNet.py:24-70 at hidden 256, 6 blocks
+TRUNK_FLOP = 2 * (59 * H + 2 * NB * H * H + H * 128 + 128)
+PIHEAD_FLOP = 2 * H * A
+
+
+def cpu_baseline(state_dict, sims, seconds_target=15.0, threads=None):
+    """The oracle restatement (C, OpenMP over games) on this host's cores: bounded sample."""
+    from oracle import oracle as O
+    threads = threads or min(16, os.cpu_count() or 1)
+    net = O.Net(state_dict, H, NB)
+    # calibrate: one game per thread, then scale the sample to ~seconds_target
+    t0 = time.time()
+    r = O.selfplay(list(range(threads)), 1, sims, mode=O.MODE_MLP, net=net, want_counts=False, threads=threads)
+    dt = time.time() - t0
+    exps = int(r["stats"][:, 1].sum())
+    games = threads
+    if dt < seconds_target / 2:
+        k = max(1, int(seconds_target / max(dt, 1e-3)) - 1)
+        t1 = time.time()
+        r = O.selfplay(list(range(threads, threads * (k + 1))), 1, sims, mode=O.MODE_MLP, net=net,
+                       want_counts=False, threads=threads)
+        dt += time.time() - t1
+        exps += int(r["stats"][:, 1].sum())
+        games += threads * k
+    return {"value": exps / dt, "unit": "expansions/s", "cores": threads, "kind": "port",
+            "sample": f"{games} full self-play games x {sims} sims (C restatement, oracle/yk_oracle.c, "
+                      f"same net), {exps} expansions in {dt:.1f}s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--envs", type=int, default=4096, help="games per GPU")
+    ap.add_argument("--sims", type=int, default=100)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel event timing")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    from yacht_amd import dist as D
+    from yacht_amd.engine import SelfPlayEngine
+    from yacht_amd.nnet import YachtNNet, YkNet
+
+    rank, world, local = D.setup()
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    torch.manual_seed(args.seed)
+    model = YachtNNet(hidden=H, nblocks=NB)  # random init of the reference architecture
+    sd = model.state_dict()
+    net = YkNet(sd, H, NB)
+    eng = SelfPlayEngine(args.envs, args.sims, 1.5, 15, net=net, max_moves=64)
+    stream = torch.cuda.current_stream()
+    env_base = D.env_base(rank, args.envs)
+    gathered_bytes = 0
+
+    def step(i):
+        nonlocal gathered_bytes
+        eng.run(args.seed + i, env_base, stream)
+        if world > 1:
+            buf = eng.pack_records(stream=stream)
+            g = D.allgather_records(buf)
+            gathered_bytes = g.numel()
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    exp0 = 0
+    if not args.no_profile:
+        eng.profile(True)
+    t0 = time.perf_counter()
+    exps = 0
+    games = 0
+    for i in range(args.steps):
+        step(args.warmup + i)
+        st = eng.stats()
+        exps += st["expansions"]
+        games += args.envs
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kt = eng.kernel_times() if not args.no_profile else {}
+    st = eng.stats()
+    if st["errors"]:
+        raise SystemExit(f"engine error flags {st['errors']}")
+
+    tot = torch.tensor([elapsed, float(exps), float(games)], dtype=torch.float64,
+                       device="cuda" if world > 1 else "cpu")
+    if world > 1:
+        t_max = tot[:1].clone()
+        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+        sums = tot[1:].clone()
+        dist.all_reduce(sums, op=dist.ReduceOp.SUM)
+        elapsed, exps, games = float(t_max[0]), float(sums[0]), float(sums[1])
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    value = exps / elapsed
+    out = {
+        "metric": METRIC, "value": value, "unit": "expansions/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": 1000.0 * elapsed / args.steps, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": f"{args.envs} games/GPU x {args.sims} sims, full 48-move self-play episodes, "
+                               f"YachtNNet hidden {H} x {NB} blocks (random init)",
+                   "envs_per_gpu": args.envs, "sims": args.sims, "cpuct": 1.5, "temp_threshold": 15,
+                   "parallelism": f"games sharded over {world} GPU(s), RCCL all-gather of trajectories"},
+        "episodes_per_s": games / elapsed,
+        "expansions_per_s_per_gpu": value / world,
+        "expansions_per_episode_batch": exps / args.steps,
+    }
+    if world > 1:
+        out["allgather_bytes"] = gathered_bytes
+    if kt:
+        # dominant kernel and its roofline (algorithmic work per launch / average launch time)
+        per = {k: (ms / n if n else 0.0, n, ms) for k, (ms, n) in kt.items()}
+        out["kernel_ms"] = {k: {"avg_ms": round(a, 5), "launches": n, "total_ms": round(t, 2)}
+                            for k, (a, n, t) in per.items()}
+        dom = max(per, key=lambda k: per[k][2])
+        exp_per_launch = exps / world / max(per["trunk"][1], 1) if per["trunk"][1] else 0.0
+        if dom in ("trunk", "pihead"):
+            flop = (TRUNK_FLOP if dom == "trunk" else PIHEAD_FLOP) * exp_per_launch
+            ach = flop / (per[dom][0] * 1e-3) / 1e12
+            out["roofline"] = {"kernel": dom, "bound": "mfma", "achieved": ach, "peak": F32_MFMA_PEAK_TFLOPS,
+                               "unit": "TFLOP/s", "frac": ach / F32_MFMA_PEAK_TFLOPS, "traffic": None,
+                               "work_per_launch": f"{exp_per_launch:.0f} expansions x "
+                                                  f"{TRUNK_FLOP if dom == 'trunk' else PIHEAD_FLOP} FLOP"}
+        else:
+            # env/MCTS kernels: algorithmic bytes = 4*S_scan + 16*D + 4*V_new + 364 per expansion
+            scan_b = 4 * st["scanned"] + 16 * st["path_edges"] + 4 * st["vnew"] + 364 * st["expansions"]
+            launches = max(per[dom][1], 1)
+            b = scan_b / max(st["sims"], 1)
+            ach = b / (per[dom][0] * 1e-3) / 1e9
+            out["roofline"] = {"kernel": dom, "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                               "frac": ach / HBM_PEAK_GBS, "traffic": None,
+                               "work_per_launch": f"{b:.0f} algorithmic bytes"}
+    if world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(sd, args.sims)
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

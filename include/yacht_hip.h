@@ -1,0 +1,187 @@
+/*
+ * yacht_hip.h - C ABI of libyacht_hip.so, the MI355X (gfx950) self-play engine for
+ * Yacht Auction.  This is the drop-in boundary for the reference's hot path
+ *   Coach.executeEpisode -> MCTS.getActionProb -> MCTS.search
+ *     -> YachtGame.{getNextState,getValidMoves,getGameEnded,getCanonicalForm,...}
+ *     -> NNetWrapper.predict
+ * (paths relative to the reference repository iyioon/NYPC-Yacht-Auction).
+ *
+ * Conventions
+ *  - Every array argument is a DEVICE pointer owned by the caller (hipMalloc /
+ *    torch), unless the comment says "host".  `stream` is a hipStream_t (NULL = the
+ *    default stream).  Calls are asynchronous on `stream` unless they say otherwise.
+ *  - Return value: YK_OK (0) or a negative YK_ERR_* code (API / HIP / capacity error).
+ *    The reference's per-call Python exceptions are reported per element in a
+ *    `status` array (YK_ST_*), because a batch can contain both good and bad inputs.
+ *  - A game state is the 64-byte packed yk_state_t (layout: DESIGN.md section 3; it is
+ *    injective on exactly the fields of YachtGame.stringRepresentation, so two states
+ *    are the same MCTS node iff their 8 words are equal).
+ *  - Randomness: the reference draws from process-global numpy / `random` RNGs
+ *    (YachtGame.py:154-159, MCTS.py:46, Coach.py:65).  Here every game owns a stream
+ *    (seed, env_id, counter) of Philox4x32-10 draws; each die, tie-break, tie pick and
+ *    sampling uniform consumes one counter value.  Given the same draws the results
+ *    are identical to the reference (tests/test_oracle_golden.py, tests/test_gpu_*.py).
+ *  - No torch types cross this boundary.
+ */
+#ifndef YACHT_HIP_H
+#define YACHT_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define YK_ACTION_SIZE 3226   /* YachtGame.py:42 */
+#define YK_NUM_BID_ACTIONS 202 /* YachtGame.py:32 */
+#define YK_FEATURES 59        /* YachtGame.getBoardSize, NNet.py:47 */
+#define YK_MASK_WORDS 101     /* ceil(3226 / 32) */
+
+typedef struct { uint64_t w[8]; } yk_state_t;
+
+/* return codes */
+#define YK_OK 0
+#define YK_ERR_ARG (-1)
+#define YK_ERR_HIP (-2)
+#define YK_ERR_NOMEM (-3)
+#define YK_ERR_CAPACITY (-4) /* a fixed-size engine pool overflowed; results invalid */
+#define YK_ERR_STATE (-5)    /* engine misuse (e.g. MCTS root round went backwards) */
+
+/* per-element status of yk_step: the reference's exceptions */
+#define YK_ST_OK 0
+#define YK_ST_VALUE_BID 1   /* ValueError("Invalid action in BID phase")   YachtGame.py:268-269 */
+#define YK_ST_VALUE_SCORE 2 /* ValueError("Invalid action in SCORE phase") YachtGame.py:306-307 */
+#define YK_ST_RUNTIME 3     /* RuntimeError("Invalid phase/state")          YachtGame.py:372 */
+#define YK_ST_ASSERT 4      /* AssertionError, _resolve_bids_and_assign     YachtGame.py:508 */
+#define YK_ST_CAPACITY 5    /* a carry would exceed 10 dice (unreachable from getInitBoard) */
+
+const char* yk_version(void);
+/* last HIP error code seen by the library (hipError_t as int), 0 if none */
+int yk_last_hip_error(void);
+/* HOST: draw `ctr` of game `env`'s stream (Philox4x32-10, key = seed, counter = (ctr, env, 0)):
+ * low 32 bits = word 0, high = word 1.  die = 1 + ((d >> 32) * 6 >> 32), below(n) likewise,
+ * uniform = (d >> 11) * 2^-53. */
+uint64_t yk_rng_draw64(uint64_t seed, uint32_t env, uint64_t ctr);
+
+/* ---------------------------------------------------------------- Game plugin (batched)
+ * Replaces YachtGame (yacht/YachtGame.py:210-467) behind Game.py:14-113.  Player values
+ * follow the reference: 1 = player 1, anything else = player 2 (-1). */
+
+/* getInitBoard (YachtGame.py:232-237): draws rollA then rollB (10 dice) from each game's
+ * stream; rng_ctr[i] is read and advanced. */
+int yk_init_board(yk_state_t* out, uint64_t* rng_ctr, const uint32_t* env_ids, uint64_t seed, int n,
+                  void* stream);
+/* getNextState (YachtGame.py:260-372, _resolve_bids_and_assign :502-542).  Pure: `in` is
+ * not modified (out may alias in).  rng_ctr advanced by the draws made (tie-break, re-rolls).
+ * status[i] != YK_ST_OK => out[i] / next_players[i] / rng_ctr[i] unspecified (the
+ * reference raised).  The silent no-op of an illegal SCORE action is YK_ST_OK with the
+ * state copied and the player flipped (YachtGame.py:312-314, 322-324). */
+int yk_step(const yk_state_t* in, const int32_t* players, const int32_t* actions, uint64_t seed,
+            const uint32_t* env_ids, uint64_t* rng_ctr, yk_state_t* out, int32_t* next_players, int8_t* status,
+            int n, void* stream);
+/* getValidMoves (YachtGame.py:374-406) as a bitmask: bit (a & 31) of mask[i*101 + a/32];
+ * counts[i] = number of valid actions (may be NULL). */
+int yk_valid_mask(const yk_state_t* in, const int32_t* players, uint32_t* mask, int32_t* counts, int n,
+                  void* stream);
+/* getGameEnded (YachtGame.py:408-428): result[i] in {0, 1e-4, 1, -1} (python float);
+ * totals[i*2+{0,1}] = total_with_bonus of p1/p2 (YachtGame.py:128-130), may be NULL. */
+int yk_ended(const yk_state_t* in, const int32_t* players, double* result, int32_t* totals, int n, void* stream);
+/* getCanonicalForm (YachtGame.py:430-442): player 1 -> copy; else p1<->p2 and bids swapped
+ * (the reference does NOT mask the pending bid, despite its docstring). */
+int yk_canonical(const yk_state_t* in, const int32_t* players, yk_state_t* out, int n, void* stream);
+/* score_category (YachtGame.py:57-108) of every (category, combo) on the mover's carry:
+ * out[(i*12 + cat)*252 + combo]; -1 where combo position >= len(carry). */
+int yk_score_table(const yk_state_t* in, const int32_t* players, int32_t* out, int n, void* stream);
+/* score_category on explicit dice: dice[i*5..+5] in 1..6 -> out[i*12 + cat]. */
+int yk_score_dice(const int8_t* dice, int32_t* out, int n, void* stream);
+/* state_to_vec (yacht/NNet.py:65-86), bit-exact float32: x[i*59 + f]. */
+int yk_featurize(const yk_state_t* in, float* x, int n, void* stream);
+/* 64-bit transposition-key hash (stands in for stringRepresentation, YachtGame.py:448-467). */
+int yk_key_hash(const yk_state_t* in, uint64_t* out, int n, void* stream);
+/* Deterministic test prior (oracle/spec.py hash_prior): pi[i*3226 + a], v[i]. */
+int yk_hash_prior(const yk_state_t* in, float* pi, float* v, int n, void* stream);
+
+/* ---------------------------------------------------------------- NeuralNet.predict
+ * Replaces NNetWrapper.predict (yacht/NNet.py:177-195) over YachtNNet
+ * (yacht/pytorch/YachtNNet.py:8-70), eval mode, batched, float32 (MFMA f32). */
+typedef struct yk_net yk_net_t;
+/* params: HOST float32 arrays in YachtNNet.state_dict() order (inp.0.weight, inp.0.bias,
+ * inp.1.weight, inp.1.bias, blocks.{b}.{fc1,ln1,fc2,ln2}.{weight,bias}, pi_head.0.*,
+ * pi_head.2.*, v_head.0.*, v_head.2.*, v_head.4.*).  hidden in {64,128,256,512}. */
+int yk_net_create(yk_net_t** net, int hidden, int nblocks, const float* const* params, int nparams);
+/* pi[i*3226 + a] = exp(log_softmax(logits)), v[i] = tanh(v_head). */
+int yk_net_predict(yk_net_t* net, const yk_state_t* states, float* pi, float* v, int n, void* stream);
+/* same from explicit feature rows x[i*59 + f] */
+int yk_net_predict_features(yk_net_t* net, const float* x, float* pi, float* v, int n, void* stream);
+int yk_net_destroy(yk_net_t* net);
+
+/* ---------------------------------------------------------------- self-play engine
+ * Batched Coach.executeEpisode (Coach.py:34-72) over n_envs games in lock-step; every game
+ * runs MCTS.getActionProb (MCTS.py:28-54) / MCTS.search (MCTS.py:56-164) with its own
+ * tree (reset per episode, Coach.py:93). */
+typedef struct {
+    int n_envs;             /* games per batch (per GPU) */
+    int sims;               /* numMCTSSims */
+    double cpuct;           /* cpuct */
+    int temp_threshold;     /* tempThreshold */
+    int max_moves;          /* record capacity per game (every real game has 48 moves) */
+    int prior;              /* 0 = yk_net (MLP), 1 = hash prior (test) */
+    int record_predictions; /* test: keep every expansion's (pi, v) per game */
+    int max_expansions;     /* capacity of that record per game (record_predictions only) */
+    int64_t arena_entries;  /* per game per generation P/edge-slot entries; 0 = default */
+} yk_engine_config_t;
+
+typedef struct yk_engine yk_engine_t;
+int yk_engine_create(yk_engine_t** eng, const yk_engine_config_t* cfg, yk_net_t* net);
+int yk_engine_destroy(yk_engine_t* eng);
+/* Plays one complete episode for each of the n_envs games (game i uses stream env_base+i).
+ * Synchronises `stream` once per real move to test termination.  Returns YK_OK, or
+ * YK_ERR_CAPACITY / YK_ERR_STATE if a device-side check failed (see yk_engine_stats). */
+int yk_selfplay(yk_engine_t* eng, uint64_t seed, uint32_t env_base, void* stream);
+/* Per-kernel timing with HIP events on the engine's stream (adds an event pair around each
+ * launch while enabled; resets the accumulators).  yk_engine_kernel_times: HOST ms[8],
+ * launches[8] for classes 0 select, 1 trunk (predict layers), 2 policy head, 3 expand+backup,
+ * 4 move begin (root / tree compaction), 5 move end (policy, sampling, real step). */
+int yk_engine_profile(yk_engine_t* eng, int enable);
+int yk_engine_kernel_times(yk_engine_t* eng, double* ms, int64_t* launches);
+/* HOST out[16]: 0 expansions, 1 valid entries scanned by UCB, 2 real moves (max over games),
+ * 3 device error flags, 4 max live nodes, 5 max live edges, 6 max arena entries used (per shard),
+ * 7 new-node valid entries written, 8 search path edges backed up, 9 lock-step sims run */
+int yk_engine_stats(yk_engine_t* eng, int64_t* out);
+/* Copies the last episode batch to HOST arrays (any may be NULL):
+ *   states[n][max_moves][8]  canonical board of each example (Coach.py:57,61)
+ *   info[n][max_moves][8]    temp, player, action, expansions-so-far, root Ns, n visited, status, 0
+ *   ctr[n][max_moves][2]     stream counter before the search / before the real step
+ *   values[n][max_moves]     example value r*(-1)**(player != curPlayer) (Coach.py:72)
+ *   final_states[n][8], n_moves[n]
+ *   visits_off[n*max_moves+1], visits[...][2] (action, N): root visit counts, ascending
+ *   action (size: yk_engine_records(...) with visits=NULL returns the total in *n_visits). */
+int yk_engine_records(yk_engine_t* eng, uint64_t* states, int32_t* info, uint64_t* ctr, double* values,
+                      uint64_t* final_states, int32_t* n_moves, int64_t* visits_off, int32_t* visits,
+                      int64_t* n_visits);
+/* record_predictions: HOST pi[n][max_expansions][3226], v[n][max_expansions], count[n] */
+int yk_engine_predictions(yk_engine_t* eng, float* pi, float* v, int32_t* count);
+/* Fixed-size trajectory records of the last batch for the multi-GPU all-gather:
+ * yk_engine_record_bytes = size of the packed image; yk_engine_pack_records copies it
+ * (device to device, async on `stream`) into dst (device, >= that many bytes).  Image:
+ * states[n][M][8] u64 | info[n][M][8] i32 | ctr[n][M][2] u64 | values[n][M] f64 |
+ * visits[n][VCAP] u32 (action << 16 | N) | visits_off[n][M+1] i32 | n_moves[n] i32 |
+ * final_states[n][8] u64 (M = max_moves, VCAP = 2 * M * max(sims, 32)). */
+int64_t yk_engine_record_bytes(yk_engine_t* eng);
+int yk_engine_pack_records(yk_engine_t* eng, void* dst, int64_t capacity, void* stream);
+
+/* ---------------------------------------------------------------- MCTS plugin
+ * MCTS(game, nnet, args).getActionProb (MCTS.py:28-54) for n_envs independent searches
+ * sharing nothing: runs `sims` searches from roots[i] (device, canonical boards) with
+ * persistent trees, drawing from game i's stream (rng_ctr[i], advanced), and writes the
+ * root visit counts counts[i*3226 + a] (device).  Roots must not go back in round
+ * (trees keep only nodes of rounds >= the root's, which is parity-safe because a game's
+ * round never decreases).  yk_mcts_reset clears all trees. */
+int yk_mcts_search(yk_engine_t* eng, const yk_state_t* roots, uint64_t seed, const uint32_t* env_ids,
+                   uint64_t* rng_ctr, int sims, int32_t* counts, void* stream);
+int yk_mcts_reset(yk_engine_t* eng);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* YACHT_HIP_H */

@@ -1,0 +1,1232 @@
+// yk_engine.hip - batched self-play: Coach.executeEpisode (Coach.py:34-72) driving
+// MCTS.getActionProb / MCTS.search (MCTS.py:28-164) for thousands of games in lock-step.
+//
+// Lock-step semantics.  Every game runs simulation k of move m at the same time:
+//   k_select         one wavefront per game walks its own tree from the root (UCB argmax
+//                    over the compact valid set, transitions with the game's own RNG
+//                    stream) to the first unexpanded state, a terminal, or a dead node;
+//   k_trunk/k_pihead one batched f32-MFMA forward over all pending leaves (yk_net.hip);
+//   k_expand_backup  one wavefront per game: exp(log_softmax), mask, numpy-pairwise
+//                    renormalise, insert the node, back the value up the path.
+// Within a game the simulations stay strictly sequential, so each game reproduces the
+// reference's recursive search exactly (no virtual loss); only different games overlap.
+//
+// Data layout (per game): open-addressing index of node ids keyed by the
+// 64-byte packed state; 96-byte node records; one arena holding, per expanded node, its
+// prior P over the compact valid set (f32) and a u16 edge slot per valid action; 16-byte
+// edges {Q (f64 value + python-type tag), N}.  Node/edge pools are double-buffered; at a
+// real round change the survivors (round >= the root's round - the only nodes a game can
+// ever reach again, since round_no never decreases) are compacted into the other buffer.
+#include <math.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "yk_api.h"
+#include "yk_common.h"
+#include "yk_net.h"
+
+using namespace yk;
+
+namespace {
+
+constexpr int MAXD = 64;          // max search depth (path entries)
+constexpr int LUT_N = 1 << 16;    // f32(sqrt(Ns)), f32(sqrt(Ns + 1e-8)) table size
+constexpr int GAMES_PER_BLOCK = 4;
+
+// python value kinds on the search path (MCTS.py:82, 115, 147)
+enum : uint32_t { T_INT = 0, T_F64 = 1, T_F32 = 2 };
+
+struct NodeRec {          // 96 bytes
+    uint64_t key[8];      // packed canonical state
+    uint64_t hash;
+    uint64_t vinfo;       // cats nibbles [0:48] | k [48:52] | n [52:56] | W [56:64]
+    uint32_t p_off;       // arena offset (entries) of P / slots
+    uint32_t nvalid;
+    uint32_t Ns;
+    uint32_t pad;
+};
+struct Edge {             // 16 bytes
+    double Q;
+    uint32_t N;
+    uint32_t tag;
+};
+
+struct EngDev {
+    int E, NCAP, HCAP, ECAP, M, VCAP;
+    int64_t AE;
+    int sims, temp_threshold;
+    float c32;
+    int prior;  // 0 net, 1 hash
+    int rec_pred, max_exp;
+    uint64_t seed;
+    NodeRec* nodes[2];
+    uint32_t* hidx[2];
+    Edge* edges[2];
+    uint32_t* node_count;  // [2][E]
+    uint32_t* edge_count;  // [2][E]
+    float* arenaP;
+    uint16_t* arenaS;
+    uint32_t* arena_top;   // [E]
+    uint8_t* gen;          // [E]
+    uint8_t* cur_round;    // [E]
+    // game state
+    yk_state_t* board;
+    int32_t* cur;
+    uint64_t* ctr;
+    uint32_t* env_id;
+    uint8_t* done;
+    int32_t* nmoves;
+    yk_state_t* root;
+    // per-sim
+    yk_state_t* leaf_state;
+    uint64_t* leaf_hash;
+    uint8_t* leaf_flag;
+    uint32_t* path;        // [E][MAXD]: j << 20 | node id
+    uint8_t* path_len;
+    double* res_v;
+    uint32_t* res_t;
+    const float* logits;   // [E][PI_LD]
+    const float* vpred;    // [E]
+    const float* lut_sq;
+    const float* lut_sqe;
+    // records
+    yk_state_t* rec_state; // [E][M]
+    int32_t* rec_info;     // [E][M][8]
+    uint64_t* rec_ctr;     // [E][M][2]
+    double* rec_val;       // [E][M]
+    uint32_t* rec_visits;  // [E][VCAP]: action << 16 | N
+    int32_t* rec_voff;     // [E][M+1]
+    double* final_r;       // [E]
+    int32_t* final_cur;    // [E]
+    float* rec_pi;         // [E][max_exp][3226]  (record_predictions)
+    float* rec_v;          // [E][max_exp]
+    // stats
+    uint64_t* gstats;      // [E][8]: expansions, scanned, path edges, vnew, max nodes, max edges, max arena, sims
+    uint32_t* err;         // [1] error bits
+};
+
+enum : uint32_t {
+    ERR_NODES = 1u, ERR_EDGES = 2u, ERR_ARENA = 4u, ERR_DEPTH = 8u, ERR_STEP = 16u, ERR_ROUND = 32u,
+    ERR_VISITS = 64u, ERR_MOVES = 128u, ERR_ZERO_COUNTS = 256u, ERR_ROOT = 512u, ERR_HASH = 1024u
+};
+
+// numpy float32 pairwise-sum plan for n = 3226 (loops_utils.h.src @TYPE@_pairwise_sum)
+struct PwPlan {
+    int nleaf, nop, root;
+    uint16_t start[64], len[64];
+    uint8_t a[64], b[64];
+};
+constexpr int pw_build(PwPlan& p, int start, int n) {
+    if (n <= 128) {
+        p.start[p.nleaf] = (uint16_t)start;
+        p.len[p.nleaf] = (uint16_t)n;
+        return p.nleaf++;
+    }
+    int n2 = n / 2;
+    n2 -= n2 % 8;
+    const int l = pw_build(p, start, n2);
+    const int r = pw_build(p, start + n2, n - n2);
+    p.a[p.nop] = (uint8_t)l;
+    p.b[p.nop] = (uint8_t)r;
+    return 64 + p.nop++;
+}
+constexpr PwPlan make_plan() {
+    PwPlan p{};
+    p.root = pw_build(p, 0, ASIZE);
+    return p;
+}
+static __constant__ PwPlan c_pw = make_plan();
+static_assert(make_plan().nleaf <= 64 && make_plan().nop <= 64, "pairwise plan too large");
+
+__device__ __forceinline__ YkS ld_state(const yk_state_t* p) {
+    const uint4* q = reinterpret_cast<const uint4*>(p);
+    YkS s;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        uint4 v = q[k];
+        s.w[2 * k] = (uint64_t)v.x | ((uint64_t)v.y << 32);
+        s.w[2 * k + 1] = (uint64_t)v.z | ((uint64_t)v.w << 32);
+    }
+    return s;
+}
+__device__ __forceinline__ void st_state(yk_state_t* p, const YkS& s) {
+    uint4* q = reinterpret_cast<uint4*>(p);
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+        q[k] = make_uint4((uint32_t)s.w[2 * k], (uint32_t)(s.w[2 * k] >> 32), (uint32_t)s.w[2 * k + 1],
+                          (uint32_t)(s.w[2 * k + 1] >> 32));
+}
+__device__ __forceinline__ bool key_eq(const NodeRec& r, const YkS& s) {
+    bool eq = true;
+#pragma unroll
+    for (int i = 0; i < 8; i++) eq &= r.key[i] == s.w[i];
+    return eq;
+}
+__device__ __forceinline__ uint64_t pack_vinfo(const VInfo& v) {
+    return (v.cats & 0xFFFFFFFFFFFFull) | ((uint64_t)v.k << 48) | ((uint64_t)v.n << 52) | ((uint64_t)v.W << 56);
+}
+__device__ __forceinline__ VInfo unpack_vinfo(uint64_t x, uint32_t V) {
+    VInfo v;
+    v.cats = x & 0xFFFFFFFFFFFFull;
+    v.k = (int)((x >> 48) & 0xF);
+    v.n = (int)((x >> 52) & 0xF);
+    v.W = (int)(x >> 56);
+    v.V = (int)V;
+    return v;
+}
+__device__ __forceinline__ int pad4(int v) { return (v + 3) & ~3; }
+
+// open-addressing lookup; returns node id or -1.  Uniform across the wave.
+__device__ __forceinline__ int lookup(const EngDev& d, int g, int e, const YkS& s, uint64_t h) {
+    const uint32_t* hx = d.hidx[g] + (long)e * d.HCAP;
+    const NodeRec* nodes = d.nodes[g] + (long)e * d.NCAP;
+    const uint32_t mask = (uint32_t)d.HCAP - 1;
+    uint32_t slot = (uint32_t)h & mask;
+    for (int probe = 0; probe < d.HCAP; probe++) {
+        const uint32_t v = hx[slot];
+        if (v == 0) return -1;
+        const NodeRec& r = nodes[v - 1];
+        if (r.hash == h && key_eq(r, s)) return (int)(v - 1);
+        slot = (slot + 1) & mask;
+    }
+    return -1;
+}
+__device__ __forceinline__ bool insert_index(const EngDev& d, int g, int e, uint64_t h, uint32_t id) {
+    uint32_t* hx = d.hidx[g] + (long)e * d.HCAP;
+    const uint32_t mask = (uint32_t)d.HCAP - 1;
+    uint32_t slot = (uint32_t)h & mask;
+    for (int probe = 0; probe < d.HCAP; probe++) {
+        if (hx[slot] == 0) {
+            hx[slot] = id + 1;
+            return true;
+        }
+        slot = (slot + 1) & mask;
+    }
+    return false;
+}
+
+// orders this wave's LDS / global accesses across lanes (waves of a block diverge, so no
+// __syncthreads in per-game code)
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ float wave_sumf(float v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// ------------------------------------------------------------------ python-typed arithmetic
+// NEP 50 weak-scalar rules of numpy 2 (verified bitwise): any float32
+// operand makes the result float32 (python ints/floats are cast to f32 first); python
+// float with int -> float64; int / int -> float64 (true division).
+struct PyV {
+    double v;
+    uint32_t t;
+};
+__device__ __forceinline__ PyV pv_update(PyV q, uint32_t n, PyV v) {  // (n*q + v) / (n+1)  MCTS.py:155-156
+    PyV prod, sum, out;
+    if (q.t == T_F32) prod = PyV{(double)((float)n * (float)q.v), T_F32};
+    else prod = PyV{(double)n * q.v, q.t};
+    if (prod.t == T_F32 || v.t == T_F32) sum = PyV{(double)((float)prod.v + (float)v.v), T_F32};
+    else if (prod.t == T_F64 || v.t == T_F64) sum = PyV{prod.v + v.v, T_F64};
+    else sum = PyV{prod.v + v.v, T_INT};
+    if (sum.t == T_F32) out = PyV{(double)((float)sum.v / (float)(n + 1)), T_F32};
+    else out = PyV{sum.v / (double)(n + 1), T_F64};
+    return out;
+}
+
+// ------------------------------------------------------------------ kernels
+__global__ void k_lut(float* sq, float* sqe) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= LUT_N) return;
+    sq[i] = (float)sqrt((double)i);
+    sqe[i] = (float)sqrt((double)i + 1e-8);
+}
+
+// reset every tree (MCTS() per episode, Coach.py:93) and, for self-play, start the games
+__global__ void k_reset(EngDev d, int start_games, uint32_t env_base) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= d.E) return;
+    d.node_count[e] = d.node_count[d.E + e] = 0;
+    d.edge_count[e] = d.edge_count[d.E + e] = 0;
+    d.arena_top[e] = 0;
+    d.gen[e] = 0;
+    d.cur_round[e] = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) d.gstats[(long)e * 8 + k] = 0;
+    if (!start_games) return;
+    d.env_id[e] = env_base + (uint32_t)e;
+    Stream rs{d.seed, d.env_id[e], 0};
+    YkS s;
+#pragma unroll
+    for (int k = 0; k < 8; k++) s.w[k] = 0;
+    s.w[0] = 1ull | NO_BIDS;  // getInitBoard  YachtGame.py:232-237
+    new_round_rolls(s, rs);
+    st_state(d.board + e, s);
+    d.cur[e] = 1;
+    d.ctr[e] = rs.ctr;
+    d.done[e] = 0;
+    d.nmoves[e] = 0;
+    d.rec_voff[(long)e * (d.M + 1)] = 0;
+}
+
+// Per move: root = canonical(board, cur)  (Coach.py:57); on a real round change compact the
+// game's tree into the other buffer, keeping nodes whose round >= the root's.  One wave per game.
+__global__ __launch_bounds__(256) void k_move_begin(EngDev d, int move, int external_root) {
+    const int lane = threadIdx.x & 63;
+    const int e = blockIdx.x * GAMES_PER_BLOCK + (threadIdx.x >> 6);
+    if (e >= d.E) return;
+    if (!external_root) {
+        if (d.done[e]) return;
+        const YkS b = ld_state(d.board + e);
+        const YkS r = canonical(b, d.cur[e]);
+        if (lane == 0) {
+            st_state(d.root + e, r);
+            d.rec_ctr[((long)e * d.M + move) * 2] = d.ctr[e];
+        }
+    }
+    const YkS r = ld_state(d.root + e);
+    const int rr = s_round(r);
+    const int cr = d.cur_round[e];
+    if (rr == cr) return;
+    if (rr < cr) {
+        if (lane == 0) atomicOr(d.err, ERR_ROUND);
+        return;
+    }
+    // ---- compaction g -> g ^ 1 (in-place for the arena: survivors only move down)
+    const int g = d.gen[e], h = g ^ 1;
+    uint32_t* hx = d.hidx[h] + (long)e * d.HCAP;
+    for (int i = lane; i < d.HCAP; i += 64) hx[i] = 0;
+    const NodeRec* src = d.nodes[g] + (long)e * d.NCAP;
+    NodeRec* dst = d.nodes[h] + (long)e * d.NCAP;
+    const Edge* esrc = d.edges[g] + (long)e * d.ECAP;
+    Edge* edst = d.edges[h] + (long)e * d.ECAP;
+    float* P = d.arenaP + (long)e * d.AE;
+    uint16_t* S = d.arenaS + (long)e * d.AE;
+    const uint32_t cnt = d.node_count[g * d.E + e];
+    uint32_t nn = 0, ne = 0, top = 0;
+    wave_sync();
+    for (uint32_t id = 0; id < cnt; id++) {
+        NodeRec rec = src[id];
+        if ((int)(rec.key[0] & 0xF) < rr) continue;
+        const int V = (int)rec.nvalid, VP = pad4(V);
+        const uint32_t so = rec.p_off;
+        for (int j0 = 0; j0 < VP; j0 += 64) {
+            const int j = j0 + lane;
+            float p = 0.f;
+            uint16_t sl = 0;
+            if (j < VP) {
+                p = P[so + j];
+                sl = S[so + j];
+            }
+            const bool vis = j < V && sl != 0;
+            const uint64_t bal = __ballot(vis);
+            const uint32_t before = __popcll(bal & ((1ull << lane) - 1));
+            uint16_t nsl = 0;
+            if (vis) {
+                edst[ne + before] = esrc[sl - 1];
+                nsl = (uint16_t)(ne + before + 1);
+            }
+            ne += (uint32_t)__popcll(bal);
+            if (j < VP) {
+                P[top + j] = p;
+                S[top + j] = nsl;
+            }
+        }
+        rec.p_off = top;
+        top += (uint32_t)VP;
+        if (lane == 0) {
+            dst[nn] = rec;
+            insert_index(d, h, e, rec.hash, nn);
+        }
+        nn++;
+    }
+    if (lane == 0) {
+        d.node_count[h * d.E + e] = nn;
+        d.edge_count[h * d.E + e] = ne;
+        d.arena_top[e] = top;
+        d.gen[e] = (uint8_t)h;
+        d.cur_round[e] = (uint8_t)rr;
+    }
+}
+
+// One simulation's descent (MCTS.search, MCTS.py:56-152 up to the recursion).
+__global__ __launch_bounds__(256) void k_select(EngDev d, const uint32_t* env_ids, uint64_t* ctr_arr) {
+    const int lane = threadIdx.x & 63;
+    const int e = blockIdx.x * GAMES_PER_BLOCK + (threadIdx.x >> 6);
+    if (e >= d.E) return;
+    if (d.done[e]) {
+        if (lane == 0) {
+            d.leaf_flag[e] = 0;
+            d.path_len[e] = 0;
+        }
+        return;
+    }
+    const int g = d.gen[e];
+    YkS s = ld_state(d.root + e);
+    Stream rs{d.seed, env_ids[e], ctr_arr[e]};
+    const NodeRec* nodes = d.nodes[g] + (long)e * d.NCAP;
+    const Edge* edges = d.edges[g] + (long)e * d.ECAP;
+    const float* Pbase = d.arenaP + (long)e * d.AE;
+    const uint16_t* Sbase = d.arenaS + (long)e * d.AE;
+    uint32_t* path = d.path + (long)e * MAXD;
+    int depth = 0;
+    uint64_t scanned = 0;
+    int leaf = 0;
+    PyV res{0.0, T_INT};
+    while (true) {
+        const double es = game_ended(s, 1);  // Es (MCTS.py:78-82)
+        if (es != 0.0) {
+            res = PyV{-es, T_F64};
+            break;
+        }
+        const uint64_t hsh = key_hash(s);
+        const int nid = lookup(d, g, e, s, hsh);
+        if (nid < 0) {  // leaf: predict (MCTS.py:84-115)
+            leaf = 1;
+            if (lane == 0) {
+                st_state(d.leaf_state + e, s);
+                d.leaf_hash[e] = hsh;
+            }
+            break;
+        }
+        const NodeRec& nd = nodes[nid];
+        const int V = (int)nd.nvalid;
+        if (V == 0) {  // no valid action: MCTS.py:141-147 returns 0 (python int)
+            res = PyV{0.0, T_INT};
+            break;
+        }
+        // UCB argmax, MCTS.py:117-135: float32 arithmetic, strict '>' => lowest action wins
+        const uint32_t Ns = nd.Ns;
+        float sq, sqe;
+        if (Ns < (uint32_t)LUT_N) {
+            sq = d.lut_sq[Ns];
+            sqe = d.lut_sqe[Ns];
+        } else {
+            sq = (float)sqrt((double)Ns);
+            sqe = (float)sqrt((double)Ns + 1e-8);
+        }
+        const float* P = Pbase + nd.p_off;
+        const uint16_t* S = Sbase + nd.p_off;
+        float best = -INFINITY;
+        int bj = 0x7FFFFFFF;
+        for (int j0 = lane * 4; j0 < V; j0 += 256) {
+            const float4 p4 = *reinterpret_cast<const float4*>(P + j0);
+            const ushort4 s4 = *reinterpret_cast<const ushort4*>(S + j0);
+            const float pv[4] = {p4.x, p4.y, p4.z, p4.w};
+            const uint16_t sv[4] = {s4.x, s4.y, s4.z, s4.w};
+#pragma unroll
+            for (int t = 0; t < 4; t++) {
+                const int j = j0 + t;
+                if (j < V) {
+                    float u;
+                    const float cp = d.c32 * pv[t];
+                    if (sv[t]) {
+                        const Edge ed = edges[sv[t] - 1];
+                        u = (float)ed.Q + (cp * sq) / (float)(ed.N + 1);
+                    } else {
+                        u = cp * sqe;
+                    }
+                    if (u > best) {
+                        best = u;
+                        bj = j;
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            const float ob = __shfl_xor(best, o, 64);
+            const int oj = __shfl_xor(bj, o, 64);
+            if (ob > best || (ob == best && oj < bj)) {
+                best = ob;
+                bj = oj;
+            }
+        }
+        scanned += (uint64_t)V;
+        int j = bj;
+        if (j == 0x7FFFFFFF) j = 0;  // MCTS.py:138-143: first valid action
+        if (depth >= MAXD) {
+            if (lane == 0) atomicOr(d.err, ERR_DEPTH);
+            res = PyV{0.0, T_INT};
+            break;
+        }
+        if (lane == 0) path[depth] = ((uint32_t)j << 20) | (uint32_t)nid;
+        depth++;
+        const VInfo vi = unpack_vinfo(nd.vinfo, nd.nvalid);
+        const int a = compact_to_action(vi, j);
+        int np = 1;
+        const int st = step_state(s, 1, a, rs, np);  // MCTS.py:149
+        if (st != YK_ST_OK) {
+            if (lane == 0) atomicOr(d.err, ERR_STEP);
+            res = PyV{0.0, T_INT};
+            break;
+        }
+        s = canonical(s, np);  // MCTS.py:150
+    }
+    if (lane == 0) {
+        d.leaf_flag[e] = (uint8_t)leaf;
+        d.path_len[e] = (uint8_t)depth;
+        d.res_v[e] = res.v;
+        d.res_t[e] = res.t;
+        ctr_arr[e] = rs.ctr;
+        d.gstats[(long)e * 8 + 1] += scanned;
+        d.gstats[(long)e * 8 + 2] += (uint64_t)depth;
+        d.gstats[(long)e * 8 + 7] += 1;
+    }
+}
+
+// Leaf expansion (MCTS.py:84-115) and backup (MCTS.py:154-164).  One wave per game.
+__global__ __launch_bounds__(256) void k_expand_backup(EngDev d) {
+    __shared__ float buf_all[GAMES_PER_BLOCK][ASIZE + 2];
+    __shared__ float vals_all[GAMES_PER_BLOCK][128];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int e = blockIdx.x * GAMES_PER_BLOCK + w;
+    if (e >= d.E) return;
+    if (d.done[e]) return;
+    const int g = d.gen[e];
+    PyV res{d.res_v[e], d.res_t[e]};
+    if (d.leaf_flag[e]) {
+        float* buf = buf_all[w];
+        float* vals = vals_all[w];
+        const YkS s = ld_state(d.leaf_state + e);
+        const uint64_t hsh = d.leaf_hash[e];
+        const VInfo vi = valid_info(s, 1);
+        const int V = vi.V;
+        // ---- predict row -> pi = exp(log_softmax(logits))  (NNet.py:193)
+        float v;
+        const int pidx = (int)d.gstats[(long)e * 8 + 0];
+        const bool rec = d.rec_pred && pidx < d.max_exp;
+        float* rpi = rec ? d.rec_pi + ((long)e * d.max_exp + pidx) * ASIZE : nullptr;
+        if (d.prior == 0) {
+            const float* x = d.logits + (long)e * PI_LD;
+            float m = -INFINITY;
+            for (int a = lane; a < ASIZE; a += 64) m = fmaxf(m, x[a]);
+            m = wave_max(m);
+            float se = 0.f;
+            for (int a = lane; a < ASIZE; a += 64) se += expf(x[a] - m);
+            const float lse = logf(wave_sumf(se));
+            for (int a = lane; a < ASIZE; a += 64) {
+                const float p = expf(x[a] - m - lse);
+                if (rec) rpi[a] = p;
+                buf[a] = action_valid(s, 1, a) ? p : 0.0f;  // Ps * valids (MCTS.py:88)
+            }
+            v = d.vpred[e];
+        } else {
+            for (int a = lane; a < ASIZE; a += 64) {
+                const float p = hash_prior_pi(hsh, a);
+                if (rec) rpi[a] = p;
+                buf[a] = action_valid(s, 1, a) ? p : 0.0f;
+            }
+            v = hash_prior_v(hsh);
+        }
+        if (rec && lane == 0) d.rec_v[(long)e * d.max_exp + pidx] = v;
+        wave_sync();
+        // ---- np.sum(Ps) with numpy's float32 pairwise summation (MCTS.py:89)
+        if (lane < c_pw.nleaf) {
+            const int st = c_pw.start[lane], n = c_pw.len[lane];
+            const float* a = buf + st;
+            float res_s;
+            if (n < 8) {
+                res_s = 0.0f;
+                for (int i = 0; i < n; i++) res_s += a[i];
+            } else {
+                float r0 = a[0], r1 = a[1], r2 = a[2], r3 = a[3], r4 = a[4], r5 = a[5], r6 = a[6], r7 = a[7];
+                int i;
+                for (i = 8; i < n - (n % 8); i += 8) {
+                    r0 += a[i]; r1 += a[i + 1]; r2 += a[i + 2]; r3 += a[i + 3];
+                    r4 += a[i + 4]; r5 += a[i + 5]; r6 += a[i + 6]; r7 += a[i + 7];
+                }
+                res_s = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+                for (; i < n; i++) res_s += a[i];
+            }
+            vals[lane] = res_s;
+        }
+        wave_sync();
+        if (lane == 0) {
+            for (int o = 0; o < c_pw.nop; o++) vals[64 + o] = vals[c_pw.a[o]] + vals[c_pw.b[o]];
+        }
+        wave_sync();
+        const float sum = vals[c_pw.root];
+        // ---- allocate + write P over the compact valid set, zero edge slots
+        const int VP = pad4(V);
+        const uint32_t off = d.arena_top[e];
+        const uint32_t nid = d.node_count[g * d.E + e];
+        bool ok = true;
+        if ((int64_t)off + VP > d.AE) {
+            if (lane == 0) atomicOr(d.err, ERR_ARENA);
+            ok = false;
+        }
+        if (nid >= (uint32_t)d.NCAP) {
+            if (lane == 0) atomicOr(d.err, ERR_NODES);
+            ok = false;
+        }
+        if (ok) {
+            float* P = d.arenaP + (long)e * d.AE + off;
+            uint16_t* S = d.arenaS + (long)e * d.AE + off;
+            const float inv_fallback = V > 0 ? 1.0f / (float)V : 0.0f;
+            for (int j = lane; j < VP; j += 64) {
+                float p = 0.0f;
+                if (j < V) p = sum > 0.0f ? buf[compact_to_action(vi, j)] / sum : inv_fallback;  // MCTS.py:90-107
+                P[j] = p;
+                S[j] = 0;
+            }
+            if (lane == 0) {
+                NodeRec r;
+#pragma unroll
+                for (int i = 0; i < 8; i++) r.key[i] = s.w[i];
+                r.hash = hsh;
+                r.vinfo = pack_vinfo(vi);
+                r.p_off = off;
+                r.nvalid = (uint32_t)V;
+                r.Ns = 0;
+                r.pad = 0;
+                d.nodes[g][(long)e * d.NCAP + nid] = r;
+                if (!insert_index(d, g, e, hsh, nid)) atomicOr(d.err, ERR_HASH);
+                d.node_count[g * d.E + e] = nid + 1;
+                d.arena_top[e] = off + (uint32_t)VP;
+                uint64_t* gs = d.gstats + (long)e * 8;
+                gs[0] += 1;
+                gs[3] += (uint64_t)V;
+                if (nid + 1 > gs[4]) gs[4] = nid + 1;
+                if (off + VP > gs[6]) gs[6] = off + VP;
+            }
+        }
+        res = PyV{-(double)v, T_F32};  // return -v  (MCTS.py:115)
+    }
+    // ---- backup along the path (serial: one game's updates depend on nothing else)
+    if (lane == 0) {
+        const int depth = d.path_len[e];
+        const uint32_t* path = d.path + (long)e * MAXD;
+        NodeRec* nodes = d.nodes[g] + (long)e * d.NCAP;
+        Edge* edges = d.edges[g] + (long)e * d.ECAP;
+        uint16_t* Sb = d.arenaS + (long)e * d.AE;
+        uint32_t ne = d.edge_count[g * d.E + e];
+        PyV v = res;
+        for (int k = depth - 1; k >= 0; k--) {
+            const uint32_t pe = path[k];
+            const uint32_t nid = pe & 0xFFFFF, j = pe >> 20;
+            NodeRec& nd = nodes[nid];
+            uint16_t* slot = Sb + nd.p_off + j;
+            const uint16_t sl = *slot;
+            if (sl) {
+                Edge& ed = edges[sl - 1];
+                const PyV q = pv_update(PyV{ed.Q, ed.tag}, ed.N, v);
+                ed.Q = q.v;
+                ed.tag = q.t;
+                ed.N += 1;
+            } else if (ne < (uint32_t)d.ECAP && ne < 65535u) {
+                edges[ne] = Edge{v.v, 1u, v.t};
+                *slot = (uint16_t)(ne + 1);
+                ne++;
+            } else {
+                atomicOr(d.err, ERR_EDGES);
+            }
+            nd.Ns += 1;
+            v.v = -v.v;  // return -v
+        }
+        d.edge_count[g * d.E + e] = ne;
+        uint64_t* gs = d.gstats + (long)e * 8;
+        if (ne > gs[5]) gs[5] = ne;
+    }
+}
+
+// getActionProb tail (MCTS.py:40-54) + Coach sampling/step (Coach.py:59-72).  One wave per game.
+__global__ __launch_bounds__(256) void k_move_end(EngDev d, int move) {
+    __shared__ uint32_t vis_all[GAMES_PER_BLOCK][ASIZE];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int e = blockIdx.x * GAMES_PER_BLOCK + w;
+    if (e >= d.E) return;
+    if (d.done[e]) return;
+    uint32_t* vis = vis_all[w];
+    const int g = d.gen[e];
+    const YkS r = ld_state(d.root + e);
+    const int nid = lookup(d, g, e, r, key_hash(r));
+    int nvis = 0;
+    uint32_t root_ns = 0xFFFFFFFFu;
+    if (nid >= 0) {
+        const NodeRec& nd = d.nodes[g][(long)e * d.NCAP + nid];
+        root_ns = nd.Ns;
+        const VInfo vi = unpack_vinfo(nd.vinfo, nd.nvalid);
+        const uint16_t* S = d.arenaS + (long)e * d.AE + nd.p_off;
+        const Edge* edges = d.edges[g] + (long)e * d.ECAP;
+        for (int j0 = 0; j0 < (int)nd.nvalid; j0 += 64) {
+            const int j = j0 + lane;
+            const uint16_t sl = j < (int)nd.nvalid ? S[j] : 0;
+            const uint64_t bal = __ballot(sl != 0);
+            if (sl) {
+                const int pos = nvis + __popcll(bal & ((1ull << lane) - 1));
+                vis[pos] = ((uint32_t)compact_to_action(vi, j) << 16) | (edges[sl - 1].N & 0xFFFF);
+            }
+            nvis += __popcll(bal);
+        }
+    } else if (lane == 0) {
+        atomicOr(d.err, ERR_ROOT);
+    }
+    wave_sync();
+    // record the visit counts (sparse, ascending action)
+    const long vbase = (long)e * d.VCAP;
+    const int voff = d.rec_voff[(long)e * (d.M + 1) + move];
+    const bool room = voff + nvis <= d.VCAP;
+    if (room)
+        for (int i = lane; i < nvis; i += 64) d.rec_visits[vbase + voff + i] = vis[i];
+    if (lane != 0) return;
+    if (!room) atomicOr(d.err, ERR_VISITS);
+    d.rec_voff[(long)e * (d.M + 1) + move + 1] = room ? voff + nvis : voff;
+    const int stepi = move + 1;
+    const int temp = stepi < d.temp_threshold ? 1 : 0;  // Coach.py:58
+    Stream rs{d.seed, d.env_id[e], d.ctr[e]};
+    int action = 0;
+    if (temp == 0) {
+        // bestAs = argwhere(counts == max(counts)); np.random.choice(bestAs)  (MCTS.py:44-49)
+        uint32_t mx = 0;
+        for (int i = 0; i < nvis; i++) mx = max(mx, vis[i] & 0xFFFF);
+        if (mx == 0) {
+            action = rs.below(ASIZE);  // every count is 0: all 3226 actions tie
+        } else {
+            int nb = 0;
+            for (int i = 0; i < nvis; i++) nb += (vis[i] & 0xFFFF) == mx;
+            int pick = rs.below(nb);
+            for (int i = 0; i < nvis; i++)
+                if ((vis[i] & 0xFFFF) == mx && pick-- == 0) {
+                    action = (int)(vis[i] >> 16);
+                    break;
+                }
+        }
+        (void)rs.uniform53();  // np.random.choice(len(pi), p=one-hot) still draws (Coach.py:65)
+    } else {
+        // probs = counts / sum; np.random.choice(len(pi), p=probs): cumsum, /= cdf[-1],
+        // searchsorted(u, 'right')
+        double total = 0.0;
+        for (int i = 0; i < nvis; i++) total += (double)(vis[i] & 0xFFFF);
+        if (total == 0.0) {
+            atomicOr(d.err, ERR_ZERO_COUNTS);
+        } else {
+            double c = 0.0;
+            for (int i = 0; i < nvis; i++) c += (double)(vis[i] & 0xFFFF) / total;
+            const double last = c;
+            const double u = rs.uniform53();
+            c = 0.0;
+            action = ASIZE;
+            for (int i = 0; i < nvis; i++) {
+                c += (double)(vis[i] & 0xFFFF) / total;
+                if (c / last > u) {
+                    action = (int)(vis[i] >> 16);
+                    break;
+                }
+            }
+        }
+    }
+    // record + real step (Coach.py:61-67)
+    const long ri = (long)e * d.M + move;
+    st_state(d.rec_state + ri, r);
+    d.rec_ctr[ri * 2 + 1] = rs.ctr;
+    const int player = d.cur[e];
+    YkS b = ld_state(d.board + e);
+    int np = 0;
+    const int st = step_state(b, player, action, rs, np);
+    int32_t* info = d.rec_info + ri * 8;
+    info[0] = temp;
+    info[1] = player;
+    info[2] = action;
+    info[3] = (int32_t)d.gstats[(long)e * 8 + 0];
+    info[4] = (int32_t)root_ns;
+    info[5] = nvis;
+    info[6] = st;
+    info[7] = 0;
+    d.nmoves[e] = stepi;
+    if (st != YK_ST_OK) {
+        atomicOr(d.err, ERR_STEP);
+        d.done[e] = 1;
+        return;
+    }
+    st_state(d.board + e, b);
+    d.cur[e] = np;
+    d.ctr[e] = rs.ctr;
+    const double rgame = game_ended(b, np);  // Coach.py:69
+    if (rgame != 0.0) {
+        d.done[e] = 1;
+        d.final_r[e] = rgame;
+        d.final_cur[e] = np;
+    } else if (stepi >= d.M) {
+        atomicOr(d.err, ERR_MOVES);
+        d.done[e] = 1;
+        d.final_r[e] = 0.0;
+        d.final_cur[e] = np;
+    }
+}
+
+// example values r * (-1)**(player != curPlayer)  (Coach.py:71-72)
+__global__ void k_finalize(EngDev d) {
+    const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (long)d.E * d.M) return;
+    const int e = (int)(t / d.M), m = (int)(t % d.M);
+    if (m >= d.nmoves[e]) {
+        d.rec_val[t] = 0.0;
+        return;
+    }
+    const int pl = d.rec_info[t * 8 + 1];
+    d.rec_val[t] = d.final_r[e] * ((pl != d.final_cur[e]) ? -1.0 : 1.0);
+}
+
+// dense root visit counts for the MCTS plugin (MCTS.py:41-42)
+__global__ void k_root_counts(EngDev d, int32_t* counts) {
+    const int lane = threadIdx.x & 63;
+    const int e = blockIdx.x * GAMES_PER_BLOCK + (threadIdx.x >> 6);
+    if (e >= d.E) return;
+    int32_t* c = counts + (long)e * ASIZE;
+    for (int a = lane; a < ASIZE; a += 64) c[a] = 0;
+    wave_sync();
+    const int g = d.gen[e];
+    const YkS r = ld_state(d.root + e);
+    const int nid = lookup(d, g, e, r, key_hash(r));
+    if (nid < 0) return;
+    const NodeRec& nd = d.nodes[g][(long)e * d.NCAP + nid];
+    const VInfo vi = unpack_vinfo(nd.vinfo, nd.nvalid);
+    const uint16_t* S = d.arenaS + (long)e * d.AE + nd.p_off;
+    const Edge* edges = d.edges[g] + (long)e * d.ECAP;
+    for (int j = lane; j < (int)nd.nvalid; j += 64)
+        if (S[j]) c[compact_to_action(vi, j)] = (int32_t)edges[S[j] - 1].N;
+}
+
+__global__ void k_count_done(const uint8_t* done, int E, int32_t* out) {
+    __shared__ int s;
+    if (threadIdx.x == 0) s = 0;
+    __syncthreads();
+    int c = 0;
+    for (int e = threadIdx.x; e < E; e += blockDim.x) c += done[e] ? 1 : 0;
+    atomicAdd(&s, c);
+    __syncthreads();
+    if (threadIdx.x == 0) *out = s;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ host object
+struct yk_engine {
+    yk_engine_config_t cfg;
+    yk_net_t* net = nullptr;
+    EngDev d{};
+    std::vector<void*> allocs;
+    float* a_pi = nullptr;
+    float* logits = nullptr;
+    float* vpred = nullptr;
+    float *lut_sq = nullptr, *lut_sqe = nullptr;
+    int32_t* done_count = nullptr;
+    int32_t* host_done = nullptr;
+    uint32_t* mcts_env = nullptr;
+    bool have_records = false;
+    // profiling (yk_engine_profile): per-kernel-class HIP events, accumulated per move
+    bool prof = false;
+    std::vector<hipEvent_t> ev;
+    std::vector<int> ev_cls;
+    int ev_used = 0;
+    double kms[8] = {0};
+    int64_t klaunch[8] = {0};
+};
+
+namespace {
+// kernel classes for yk_engine_kernel_times
+enum { KC_SELECT = 0, KC_TRUNK = 1, KC_PIHEAD = 2, KC_EXPAND = 3, KC_MOVE_BEGIN = 4, KC_MOVE_END = 5, KC_N = 8 };
+
+void prof_mark(yk_engine* eng, int cls, hipStream_t s) {  // records an event pair boundary
+    if (!eng->prof) return;
+    if (eng->ev_used + 1 >= (int)eng->ev.size()) {
+        const size_t old = eng->ev.size();
+        eng->ev.resize(old + 4096);
+        eng->ev_cls.resize(old + 4096);
+        for (size_t i = old; i < eng->ev.size(); i++) (void)hipEventCreate(&eng->ev[i]);
+    }
+    eng->ev_cls[eng->ev_used] = cls;
+    (void)hipEventRecord(eng->ev[eng->ev_used++], s);
+}
+void prof_collect(yk_engine* eng) {  // call after a stream sync
+    if (!eng->prof) return;
+    for (int i = 0; i + 1 < eng->ev_used; i++) {
+        const int cls = eng->ev_cls[i];
+        if (cls < 0) continue;
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, eng->ev[i], eng->ev[i + 1]) == hipSuccess) {
+            eng->kms[cls] += ms;
+            eng->klaunch[cls] += 1;
+        }
+    }
+    eng->ev_used = 0;
+}
+
+template <class T>
+int dalloc(yk_engine* eng, T** p, size_t count) {
+    void* q = nullptr;
+    if (hipMalloc(&q, sizeof(T) * (count ? count : 1)) != hipSuccess) {
+        (void)hipGetLastError();
+        return YK_ERR_NOMEM;
+    }
+    eng->allocs.push_back(q);
+    *p = static_cast<T*>(q);
+    return YK_OK;
+}
+int check_errors(yk_engine* eng, hipStream_t s) {
+    uint32_t err = 0;
+    YK_HIP(hipMemcpyAsync(&err, eng->d.err, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    YK_HIP(hipStreamSynchronize(s));
+    if (err & (ERR_NODES | ERR_EDGES | ERR_ARENA | ERR_DEPTH | ERR_VISITS | ERR_HASH)) return YK_ERR_CAPACITY;
+    if (err) return YK_ERR_STATE;
+    return YK_OK;
+}
+int run_sims(yk_engine* eng, int sims, const uint32_t* env_ids, uint64_t* ctr, hipStream_t s) {
+    EngDev& d = eng->d;
+    const dim3 gb((d.E + GAMES_PER_BLOCK - 1) / GAMES_PER_BLOCK), bb(256);
+    for (int k = 0; k < sims; k++) {
+        prof_mark(eng, KC_SELECT, s);
+        hipLaunchKernelGGL(k_select, gb, bb, 0, s, d, env_ids, ctr);
+        YK_LAUNCHED();
+        if (d.prior == 0) {
+            prof_mark(eng, KC_TRUNK, s);
+            int rc = launch_trunk(eng->net->dev, d.leaf_state, nullptr, nullptr, nullptr, d.E, eng->a_pi, eng->vpred, s);
+            if (rc) return rc;
+            prof_mark(eng, KC_PIHEAD, s);
+            rc = launch_pihead(eng->net->dev, eng->a_pi, nullptr, d.E, eng->logits, s);
+            if (rc) return rc;
+        }
+        prof_mark(eng, KC_EXPAND, s);
+        hipLaunchKernelGGL(k_expand_backup, gb, bb, 0, s, d);
+        YK_LAUNCHED();
+    }
+    prof_mark(eng, -1, s);
+    return YK_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int yk_engine_create(yk_engine_t** out, const yk_engine_config_t* cfg, yk_net_t* net) {
+    if (!out || !cfg) return YK_ERR_ARG;
+    if (cfg->n_envs <= 0 || cfg->sims < 1 || cfg->max_moves < 1 || cfg->max_moves > 4096) return YK_ERR_ARG;
+    if (cfg->prior == 0 && !net) return YK_ERR_ARG;
+    if (cfg->prior != 0 && cfg->prior != 1) return YK_ERR_ARG;
+    yk_engine* eng = new yk_engine();
+    eng->cfg = *cfg;
+    eng->net = net;
+    EngDev& d = eng->d;
+    d.E = cfg->n_envs;
+    d.sims = cfg->sims;
+    d.c32 = (float)cfg->cpuct;
+    d.temp_threshold = cfg->temp_threshold;
+    d.prior = cfg->prior;
+    d.M = cfg->max_moves;
+    // capacities: one new node per simulation; a round holds <= 4 real moves
+    // and round 2 also keeps the round-2 nodes made while searching round 1 (<= 2 moves).
+    d.NCAP = 6 * cfg->sims + 64;
+    int hcap = 1;
+    while (hcap < 2 * d.NCAP) hcap <<= 1;
+    d.HCAP = hcap;
+    d.ECAP = std::min(2 * d.NCAP, 65535);
+    d.AE = cfg->arena_entries > 0 ? ((cfg->arena_entries + 3) & ~3LL) : (int64_t)cfg->sims * 7000 + 4096;
+    d.VCAP = 2 * cfg->max_moves * std::max(cfg->sims, 32);
+    d.rec_pred = cfg->record_predictions ? 1 : 0;
+    d.max_exp = cfg->record_predictions ? std::max(cfg->max_expansions, 1) : 0;
+    const size_t E = (size_t)d.E;
+    int rc = YK_OK;
+#define A(p, n) \
+    if (rc == YK_OK) rc = dalloc(eng, &(p), (n))
+    for (int g = 0; g < 2; g++) {
+        A(d.nodes[g], E * d.NCAP);
+        A(d.hidx[g], E * d.HCAP);
+        A(d.edges[g], E * d.ECAP);
+    }
+    A(d.node_count, 2 * E);
+    A(d.edge_count, 2 * E);
+    A(d.arenaP, E * (size_t)d.AE);
+    A(d.arenaS, E * (size_t)d.AE);
+    A(d.arena_top, E);
+    A(d.gen, E);
+    A(d.cur_round, E);
+    A(d.board, E);
+    A(d.cur, E);
+    A(d.ctr, E);
+    A(d.env_id, E);
+    A(d.done, E);
+    A(d.nmoves, E);
+    A(d.root, E);
+    A(d.leaf_state, E);
+    A(d.leaf_hash, E);
+    A(d.leaf_flag, E);
+    A(d.path, E * MAXD);
+    A(d.path_len, E);
+    A(d.res_v, E);
+    A(d.res_t, E);
+    A(eng->vpred, E);
+    A(eng->lut_sq, (size_t)LUT_N);
+    A(eng->lut_sqe, (size_t)LUT_N);
+    A(d.rec_state, E * d.M);
+    A(d.rec_info, E * d.M * 8);
+    A(d.rec_ctr, E * d.M * 2);
+    A(d.rec_val, E * d.M);
+    A(d.rec_visits, E * (size_t)d.VCAP);
+    A(d.rec_voff, E * (d.M + 1));
+    A(d.final_r, E);
+    A(d.final_cur, E);
+    A(d.gstats, E * 8);
+    A(d.err, 1);
+    A(eng->done_count, 1);
+    A(eng->mcts_env, E);
+    if (d.prior == 0) {
+        A(eng->a_pi, E * (size_t)net->dev.H);
+        A(eng->logits, E * (size_t)PI_LD);
+    }
+    if (d.rec_pred) {
+        A(d.rec_pi, E * (size_t)d.max_exp * ASIZE);
+        A(d.rec_v, E * (size_t)d.max_exp);
+    }
+#undef A
+    if (rc == YK_OK && hipHostMalloc((void**)&eng->host_done, sizeof(int32_t)) != hipSuccess) rc = YK_ERR_NOMEM;
+    if (rc != YK_OK) {
+        yk_engine_destroy(eng);
+        return rc;
+    }
+    d.logits = eng->logits;
+    d.vpred = eng->vpred;
+    d.lut_sq = eng->lut_sq;
+    d.lut_sqe = eng->lut_sqe;
+    hipLaunchKernelGGL(k_lut, dim3(LUT_N / 256), dim3(256), 0, 0, eng->lut_sq, eng->lut_sqe);
+    YK_LAUNCHED();
+    YK_HIP(hipMemset(d.err, 0, sizeof(uint32_t)));
+    YK_HIP(hipMemset(d.done, 0, E));
+    YK_HIP(hipMemset(d.leaf_state, 0, sizeof(yk_state_t) * E));
+    std::vector<uint32_t> ids(E);
+    for (size_t i = 0; i < E; i++) ids[i] = (uint32_t)i;
+    YK_HIP(hipMemcpy(eng->mcts_env, ids.data(), sizeof(uint32_t) * E, hipMemcpyHostToDevice));
+    YK_HIP(hipDeviceSynchronize());
+    *out = eng;
+    return YK_OK;
+}
+
+int yk_engine_destroy(yk_engine_t* eng) {
+    if (!eng) return YK_OK;
+    for (hipEvent_t e : eng->ev) (void)hipEventDestroy(e);
+    for (void* p : eng->allocs) (void)hipFree(p);
+    if (eng->host_done) (void)hipHostFree(eng->host_done);
+    delete eng;
+    return YK_OK;
+}
+
+int yk_selfplay(yk_engine_t* eng, uint64_t seed, uint32_t env_base, void* stream) {
+    if (!eng) return YK_ERR_ARG;
+    hipStream_t s = as_stream(stream);
+    EngDev& d = eng->d;
+    d.seed = seed;
+    const dim3 gb((d.E + GAMES_PER_BLOCK - 1) / GAMES_PER_BLOCK), bb(256);
+    YK_HIP(hipMemsetAsync(d.err, 0, sizeof(uint32_t), s));
+    YK_HIP(hipMemsetAsync(d.hidx[0], 0, sizeof(uint32_t) * (size_t)d.E * d.HCAP, s));
+    hipLaunchKernelGGL(k_reset, dim3((d.E + 255) / 256), dim3(256), 0, s, d, 1, env_base);
+    YK_LAUNCHED();
+    eng->have_records = false;
+    for (int move = 0; move < d.M; move++) {
+        prof_mark(eng, KC_MOVE_BEGIN, s);
+        hipLaunchKernelGGL(k_move_begin, gb, bb, 0, s, d, move, 0);
+        YK_LAUNCHED();
+        int rc = run_sims(eng, d.sims, d.env_id, d.ctr, s);
+        if (rc) return rc;
+        prof_mark(eng, KC_MOVE_END, s);
+        hipLaunchKernelGGL(k_move_end, gb, bb, 0, s, d, move);
+        YK_LAUNCHED();
+        prof_mark(eng, -1, s);
+        hipLaunchKernelGGL(k_count_done, dim3(1), dim3(1024), 0, s, d.done, d.E, eng->done_count);
+        YK_LAUNCHED();
+        YK_HIP(hipMemcpyAsync(eng->host_done, eng->done_count, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+        YK_HIP(hipStreamSynchronize(s));
+        prof_collect(eng);
+        if (*eng->host_done >= d.E) break;
+    }
+    hipLaunchKernelGGL(k_finalize, dim3((unsigned)(((long)d.E * d.M + 255) / 256)), dim3(256), 0, s, d);
+    YK_LAUNCHED();
+    eng->have_records = true;
+    return check_errors(eng, s);
+}
+
+int yk_engine_profile(yk_engine_t* eng, int enable) {
+    if (!eng) return YK_ERR_ARG;
+    eng->prof = enable != 0;
+    eng->ev_used = 0;
+    for (int i = 0; i < 8; i++) {
+        eng->kms[i] = 0;
+        eng->klaunch[i] = 0;
+    }
+    return YK_OK;
+}
+
+int yk_engine_kernel_times(yk_engine_t* eng, double* ms, int64_t* launches) {
+    if (!eng || !ms || !launches) return YK_ERR_ARG;
+    for (int i = 0; i < 8; i++) {
+        ms[i] = eng->kms[i];
+        launches[i] = eng->klaunch[i];
+    }
+    return YK_OK;
+}
+
+int yk_engine_stats(yk_engine_t* eng, int64_t* out) {
+    if (!eng || !out) return YK_ERR_ARG;
+    EngDev& d = eng->d;
+    std::vector<uint64_t> gs((size_t)d.E * 8);
+    std::vector<int32_t> nm(d.E);
+    uint32_t err = 0;
+    YK_HIP(hipDeviceSynchronize());
+    YK_HIP(hipMemcpy(gs.data(), d.gstats, sizeof(uint64_t) * gs.size(), hipMemcpyDeviceToHost));
+    YK_HIP(hipMemcpy(nm.data(), d.nmoves, sizeof(int32_t) * nm.size(), hipMemcpyDeviceToHost));
+    YK_HIP(hipMemcpy(&err, d.err, sizeof(uint32_t), hipMemcpyDeviceToHost));
+    for (int i = 0; i < 16; i++) out[i] = 0;
+    for (int e = 0; e < d.E; e++) {
+        const uint64_t* g = &gs[(size_t)e * 8];
+        out[0] += (int64_t)g[0];
+        out[1] += (int64_t)g[1];
+        out[2] = std::max<int64_t>(out[2], nm[e]);
+        out[4] = std::max<int64_t>(out[4], (int64_t)g[4]);
+        out[5] = std::max<int64_t>(out[5], (int64_t)g[5]);
+        out[6] = std::max<int64_t>(out[6], (int64_t)g[6]);
+        out[7] += (int64_t)g[3];
+        out[8] += (int64_t)g[2];
+        out[9] = std::max<int64_t>(out[9], (int64_t)g[7]);
+    }
+    out[3] = err;
+    out[10] = d.NCAP;
+    out[11] = d.ECAP;
+    out[12] = d.AE;
+    out[13] = d.VCAP;
+    return YK_OK;
+}
+
+int yk_engine_records(yk_engine_t* eng, uint64_t* states, int32_t* info, uint64_t* ctr, double* values,
+                      uint64_t* final_states, int32_t* n_moves, int64_t* visits_off, int32_t* visits,
+                      int64_t* n_visits) {
+    if (!eng) return YK_ERR_ARG;
+    if (!eng->have_records) return YK_ERR_STATE;
+    EngDev& d = eng->d;
+    const size_t E = d.E, M = d.M;
+    YK_HIP(hipDeviceSynchronize());
+    if (states) YK_HIP(hipMemcpy(states, d.rec_state, sizeof(yk_state_t) * E * M, hipMemcpyDeviceToHost));
+    if (info) YK_HIP(hipMemcpy(info, d.rec_info, sizeof(int32_t) * E * M * 8, hipMemcpyDeviceToHost));
+    if (ctr) YK_HIP(hipMemcpy(ctr, d.rec_ctr, sizeof(uint64_t) * E * M * 2, hipMemcpyDeviceToHost));
+    if (values) YK_HIP(hipMemcpy(values, d.rec_val, sizeof(double) * E * M, hipMemcpyDeviceToHost));
+    if (final_states) YK_HIP(hipMemcpy(final_states, d.board, sizeof(yk_state_t) * E, hipMemcpyDeviceToHost));
+    if (n_moves) YK_HIP(hipMemcpy(n_moves, d.nmoves, sizeof(int32_t) * E, hipMemcpyDeviceToHost));
+    if (visits_off || visits || n_visits) {
+        std::vector<int32_t> voff(E * (M + 1));
+        std::vector<int32_t> nm(E);
+        YK_HIP(hipMemcpy(voff.data(), d.rec_voff, sizeof(int32_t) * voff.size(), hipMemcpyDeviceToHost));
+        YK_HIP(hipMemcpy(nm.data(), d.nmoves, sizeof(int32_t) * E, hipMemcpyDeviceToHost));
+        int64_t total = 0;
+        for (size_t e = 0; e < E; e++) total += voff[e * (M + 1) + nm[e]];
+        if (n_visits) *n_visits = total;
+        if (visits_off || visits) {
+            std::vector<uint32_t> raw(E * (size_t)d.VCAP);
+            YK_HIP(hipMemcpy(raw.data(), d.rec_visits, sizeof(uint32_t) * raw.size(), hipMemcpyDeviceToHost));
+            int64_t k = 0;
+            for (size_t e = 0; e < E; e++) {
+                for (size_t m = 0; m < M; m++) {
+                    const int32_t a0 = voff[e * (M + 1) + m];
+                    const int32_t a1 = (int)m < nm[e] ? voff[e * (M + 1) + m + 1] : a0;
+                    if (visits_off) visits_off[e * M + m] = k;
+                    for (int32_t i = a0; i < a1; i++, k++)
+                        if (visits) {
+                            const uint32_t x = raw[e * d.VCAP + i];
+                            visits[2 * k] = (int32_t)(x >> 16);
+                            visits[2 * k + 1] = (int32_t)(x & 0xFFFF);
+                        }
+                }
+            }
+            if (visits_off) visits_off[E * M] = k;
+        }
+    }
+    return YK_OK;
+}
+
+int yk_engine_predictions(yk_engine_t* eng, float* pi, float* v, int32_t* count) {
+    if (!eng || !eng->d.rec_pred) return YK_ERR_ARG;
+    EngDev& d = eng->d;
+    YK_HIP(hipDeviceSynchronize());
+    if (pi) YK_HIP(hipMemcpy(pi, d.rec_pi, sizeof(float) * (size_t)d.E * d.max_exp * ASIZE, hipMemcpyDeviceToHost));
+    if (v) YK_HIP(hipMemcpy(v, d.rec_v, sizeof(float) * (size_t)d.E * d.max_exp, hipMemcpyDeviceToHost));
+    if (count) {
+        std::vector<uint64_t> gs((size_t)d.E * 8);
+        YK_HIP(hipMemcpy(gs.data(), d.gstats, sizeof(uint64_t) * gs.size(), hipMemcpyDeviceToHost));
+        for (int e = 0; e < d.E; e++) count[e] = (int32_t)gs[(size_t)e * 8];
+    }
+    return YK_OK;
+}
+
+static void record_parts(yk_engine* eng, void** p, int64_t* b) {
+    EngDev& d = eng->d;
+    const int64_t E = d.E, M = d.M;
+    void* pp[] = {d.rec_state, d.rec_info, d.rec_ctr, d.rec_val, d.rec_visits, d.rec_voff, d.nmoves, d.board};
+    int64_t bb[] = {E * M * 64, E * M * 8 * 4, E * M * 2 * 8, E * M * 8, E * d.VCAP * 4, E * (M + 1) * 4, E * 4,
+                    E * 64};
+    for (int i = 0; i < 8; i++) {
+        p[i] = pp[i];
+        b[i] = bb[i];
+    }
+}
+
+int64_t yk_engine_record_bytes(yk_engine_t* eng) {
+    if (!eng) return YK_ERR_ARG;
+    void* p[8];
+    int64_t b[8], t = 0;
+    record_parts(eng, p, b);
+    for (int i = 0; i < 8; i++) t += (b[i] + 15) & ~15LL;
+    return t;
+}
+
+int yk_engine_pack_records(yk_engine_t* eng, void* dst, int64_t capacity, void* stream) {
+    if (!eng || !dst) return YK_ERR_ARG;
+    if (!eng->have_records) return YK_ERR_STATE;
+    if (capacity < yk_engine_record_bytes(eng)) return YK_ERR_ARG;
+    void* p[8];
+    int64_t b[8], off = 0;
+    record_parts(eng, p, b);
+    for (int i = 0; i < 8; i++) {
+        YK_HIP(hipMemcpyAsync((char*)dst + off, p[i], (size_t)b[i], hipMemcpyDeviceToDevice, as_stream(stream)));
+        off += (b[i] + 15) & ~15LL;
+    }
+    return YK_OK;
+}
+
+int yk_mcts_reset(yk_engine_t* eng) {
+    if (!eng) return YK_ERR_ARG;
+    EngDev& d = eng->d;
+    YK_HIP(hipMemset(d.err, 0, sizeof(uint32_t)));
+    YK_HIP(hipMemset(d.hidx[0], 0, sizeof(uint32_t) * (size_t)d.E * d.HCAP));
+    YK_HIP(hipMemset(d.done, 0, (size_t)d.E));
+    hipLaunchKernelGGL(k_reset, dim3((d.E + 255) / 256), dim3(256), 0, 0, d, 0, 0u);
+    YK_LAUNCHED();
+    YK_HIP(hipDeviceSynchronize());
+    return YK_OK;
+}
+
+int yk_mcts_search(yk_engine_t* eng, const yk_state_t* roots, uint64_t seed, const uint32_t* env_ids,
+                   uint64_t* rng_ctr, int sims, int32_t* counts, void* stream) {
+    if (!eng || !roots || !env_ids || !rng_ctr || !counts || sims < 0) return YK_ERR_ARG;
+    hipStream_t s = as_stream(stream);
+    EngDev& d = eng->d;
+    d.seed = seed;
+    const dim3 gb((d.E + GAMES_PER_BLOCK - 1) / GAMES_PER_BLOCK), bb(256);
+    YK_HIP(hipMemcpyAsync(d.root, roots, sizeof(yk_state_t) * (size_t)d.E, hipMemcpyDeviceToDevice, s));
+    YK_HIP(hipMemsetAsync(d.done, 0, (size_t)d.E, s));
+    YK_HIP(hipMemsetAsync(d.err, 0, sizeof(uint32_t), s));
+    hipLaunchKernelGGL(k_move_begin, gb, bb, 0, s, d, 0, 1);
+    YK_LAUNCHED();
+    int rc = run_sims(eng, sims, env_ids, rng_ctr, s);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_root_counts, gb, bb, 0, s, d, counts);
+    YK_LAUNCHED();
+    return check_errors(eng, s);
+}
+
+}  // extern "C"

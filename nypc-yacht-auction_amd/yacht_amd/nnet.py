@@ -1,0 +1,163 @@
+"""YachtNNet weights (torch) + NNetWrapper.predict on the MI355X f32-MFMA kernels.
+
+``YachtNNet`` repeats the reference architecture (yacht/pytorch/YachtNNet.py:8-70) so its
+``state_dict`` names and initialisation match; torch only holds the weights.  Inference
+(``NNetWrapper.predict``, NNet.py:177-195) runs through ``yk_net_predict`` - featurize,
+13 dense layers, both heads and exp(log_softmax) on the GPU.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from collections import OrderedDict
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import kernels as K
+from ._lib import call, lib, ptr, stream_ptr
+from .state import ACTION_SIZE, pack
+from .utils import dotdict
+
+DEFAULT_ARGS = dotdict(dict(lr=2e-3, weight_decay=1e-4, epochs=15, batch_size=512, vloss_weight=1.5,
+                            cuda=True, hidden=256, nblocks=6, dropout=0.3))
+
+
+class ResidualBlock(nn.Module):  # YachtNNet.py:8-21
+    def __init__(self, dim, dropout=0.2):
+        super().__init__()
+        self.fc1 = nn.Linear(dim, dim)
+        self.ln1 = nn.LayerNorm(dim)
+        self.fc2 = nn.Linear(dim, dim)
+        self.ln2 = nn.LayerNorm(dim)
+        self.dropout = nn.Dropout(dropout)
+
+    def forward(self, x):
+        h = self.ln1(F.silu(self.fc1(x)))
+        h = self.dropout(h)
+        h = self.ln2(F.silu(self.fc2(h)))
+        return x + h
+
+
+class YachtNNet(nn.Module):  # YachtNNet.py:24-70
+    def __init__(self, input_len=59, action_size=ACTION_SIZE, hidden=256, nblocks=6, dropout=0.3):
+        super().__init__()
+        self.input_len, self.action_size = input_len, action_size
+        self.inp = nn.Sequential(nn.Linear(input_len, hidden), nn.LayerNorm(hidden), nn.SiLU(), nn.Dropout(dropout))
+        self.blocks = nn.ModuleList([ResidualBlock(hidden, dropout) for _ in range(nblocks)])
+        self.pi_head = nn.Sequential(nn.LayerNorm(hidden), nn.SiLU(), nn.Linear(hidden, action_size))
+        self.v_head = nn.Sequential(nn.LayerNorm(hidden), nn.SiLU(), nn.Linear(hidden, 128), nn.SiLU(),
+                                    nn.Linear(128, 1))
+        for m in self.modules():
+            if isinstance(m, nn.Linear):
+                nn.init.kaiming_uniform_(m.weight, nonlinearity="relu")
+                nn.init.zeros_(m.bias)
+
+    def forward(self, x):
+        if x.ndim == 3:
+            x = x.squeeze(1)
+        h = self.inp(x)
+        for blk in self.blocks:
+            h = blk(h)
+        return self.pi_head(h), torch.tanh(self.v_head(h))
+
+
+class YkNet:
+    """Owns a device copy of the weights in the kernels' layout (yk_net_create)."""
+
+    def __init__(self, state_dict, hidden: int, nblocks: int):
+        arrs = [np.ascontiguousarray(t.detach().to("cpu", torch.float32).numpy() if torch.is_tensor(t)
+                                     else np.asarray(t, dtype=np.float32)) for t in state_dict.values()]
+        if len(arrs) != 14 + 8 * nblocks:
+            raise ValueError(f"state_dict has {len(arrs)} tensors, expected {14 + 8 * nblocks}")
+        ptrs = (C.c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])
+        h = C.c_void_p()
+        call("yk_net_create", C.byref(h), hidden, nblocks, ptrs, len(arrs))
+        self.handle = h.value
+        self.hidden, self.nblocks = hidden, nblocks
+
+    def predict_states(self, states: torch.Tensor):
+        """states int64[n, 8] (device) -> pi f32[n, 3226], v f32[n]."""
+        n = states.shape[0]
+        pi = torch.empty((n, ACTION_SIZE), dtype=torch.float32, device="cuda")
+        v = torch.empty(n, dtype=torch.float32, device="cuda")
+        call("yk_net_predict", self.handle, ptr(states.contiguous()), ptr(pi), ptr(v), n, stream_ptr())
+        return pi, v
+
+    def predict_features(self, x: torch.Tensor):
+        x = x.to("cuda", torch.float32).contiguous()
+        n = x.shape[0]
+        pi = torch.empty((n, ACTION_SIZE), dtype=torch.float32, device="cuda")
+        v = torch.empty(n, dtype=torch.float32, device="cuda")
+        call("yk_net_predict_features", self.handle, ptr(x), ptr(pi), ptr(v), n, stream_ptr())
+        return pi, v
+
+    def __del__(self):
+        try:
+            if getattr(self, "handle", None):
+                lib().yk_net_destroy(self.handle)
+                self.handle = None
+        except Exception:
+            pass
+
+
+class NNetWrapper:
+    """NeuralNet plugin (NeuralNet.py:14-50, NNet.py:91-213) with GPU inference."""
+
+    def __init__(self, game, args=None):
+        self.game = game
+        self.args = args or DEFAULT_ARGS
+        self.input_len = 59
+        self.action_size = game.getActionSize()
+        self.nnet = YachtNNet(self.input_len, self.action_size, self.args.hidden, self.args.nblocks,
+                              self.args.dropout)
+        self._yk = None
+        self._yk_version = None
+
+    def _weights_version(self):
+        return tuple(p._version for p in self.nnet.parameters())
+
+    def yk_net(self) -> YkNet:
+        """Device weights for the kernels; rebuilt when the torch parameters change."""
+        v = self._weights_version()
+        if self._yk is None or v != self._yk_version:
+            self._yk = YkNet(self.nnet.state_dict(), self.args.hidden, self.args.nblocks)
+            self._yk_version = v
+        return self._yk
+
+    def predict(self, board):  # NNet.py:177-195
+        pi, v = self.yk_net().predict_states(K.states_to_device(pack(board)))
+        return pi[0].cpu().numpy(), np.float32(v[0].item())
+
+    def predict_batch(self, states: torch.Tensor):
+        return self.yk_net().predict_states(states)
+
+    def train(self, examples):
+        raise NotImplementedError("NNetWrapper.train (NNet.py:118-174) is the next row of the build (SURVEY 8f f1)")
+
+    def save_checkpoint(self, folder="checkpoint", filename="checkpoint.pth.tar"):  # NNet.py:198-205
+        os.makedirs(folder, exist_ok=True)
+        torch.save({"state_dict": self.nnet.state_dict(), "args": dict(self.args)}, os.path.join(folder, filename))
+
+    def load_checkpoint(self, folder="checkpoint", filename="checkpoint.pth.tar"):  # NNet.py:207-213
+        ck = torch.load(os.path.join(folder, filename), map_location="cpu", weights_only=True)
+        sd = ck["state_dict"] if "state_dict" in ck else ck
+        self.nnet.load_state_dict(OrderedDict(sd))
+        self._yk = None
+
+
+class HashPriorNet:
+    """Deterministic stand-in for NNetWrapper (oracle/spec.py hash_prior, computed on the
+    GPU by the engine itself).  It exists so whole self-play episodes can be compared
+    bit-for-bit with the reference's own Coach/MCTS code; it is not a model."""
+
+    yk_prior = "hash"
+
+    def __init__(self, game=None, args=None):
+        self.game = game
+
+    def predict(self, board):
+        pi, v = K.hash_prior(K.states_to_device(pack(board)))
+        return pi[0].cpu().numpy(), np.float32(v[0].item())

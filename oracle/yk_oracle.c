@@ -816,6 +816,21 @@ static int run_episode(const ep_cfg_t* cfg, pred_t* pr, uint64_t seed, uint32_t 
         out->stats[4] = (int64_t)rs.ctr; out->stats[5] = err;
     }
     if (out->final_state) pack(&board, out->final_state);
+    if (out->stats) { /* live-set footprint under round eviction (engine sizing): max over root rounds
+                         of live nodes / valid entries / edges */
+        long nv[16] = {0}, nn[16] = {0}, ne[16] = {0};
+        for (int i = 0; i < m.tree.n; i++) {
+            int rr = (int)(m.tree.nodes[i].key[0] & 0xF);
+            nn[rr]++; nv[rr] += m.tree.nodes[i].nvalid; ne[rr] += m.tree.nodes[i].ne;
+        }
+        long bv = nv[1] + nv[2], bn = nn[1] + nn[2], be = ne[1] + ne[2];
+        for (int rr = 2; rr < 14; rr++) {
+            if (nv[rr] > bv) bv = nv[rr];
+            if (nn[rr] > bn) bn = nn[rr];
+            if (ne[rr] > be) be = ne[rr];
+        }
+        out->stats[6] = bv; out->stats[7] = bn | (be << 32);
+    }
     free(counts); free(cdf); free(players);
     tree_free(&m.tree);
     return err;
