@@ -929,8 +929,18 @@ int yk_engine_create(yk_engine_t** out, const yk_engine_config_t* cfg, yk_net_t*
     int hcap = 1;
     while (hcap < 2 * d.NCAP) hcap <<= 1;
     d.HCAP = hcap;
-    d.ECAP = std::min(2 * d.NCAP, 65535);
-    d.AE = cfg->arena_entries > 0 ? ((cfg->arena_entries + 3) & ~3LL) : (int64_t)cfg->sims * 7000 + 4096;
+    d.ECAP = std::min(4 * d.NCAP, 65535);
+    // Arena: the worst case (every live node a 3024-action score node) cannot overflow; use it
+    // when it fits in 60% of free HBM, else a measured-footprint default (overflow is detected).
+    if (cfg->arena_entries > 0) {
+        d.AE = (cfg->arena_entries + 3) & ~3LL;
+    } else {
+        const int64_t worst = (int64_t)d.NCAP * 3024;
+        size_t free_b = 0, total_b = 0;
+        (void)hipMemGetInfo(&free_b, &total_b);
+        const double need = (double)worst * 6.0 * cfg->n_envs;
+        d.AE = (need < 0.6 * (double)free_b) ? worst : (int64_t)cfg->sims * 9000 + 65536;
+    }
     d.VCAP = 2 * cfg->max_moves * std::max(cfg->sims, 32);
     d.rec_pred = cfg->record_predictions ? 1 : 0;
     d.max_exp = cfg->record_predictions ? std::max(cfg->max_expansions, 1) : 0;

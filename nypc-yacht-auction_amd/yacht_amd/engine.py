@@ -37,8 +37,18 @@ class SelfPlayEngine:
         self.handle = h.value
         self.n_envs, self.sims, self.max_moves = n_envs, sims, max_moves
 
+    ERROR_BITS = {1: "node pool", 2: "edge pool", 4: "arena", 8: "search depth", 16: "transition status",
+                  32: "root round went backwards", 64: "visit records", 128: "move cap", 256: "zero visit counts",
+                  512: "root not in tree", 1024: "hash index full"}
+
     def run(self, seed: int, env_base: int = 0, stream=None):
-        call("yk_selfplay", self.handle, seed & (2**64 - 1), env_base & (2**32 - 1), stream_ptr(stream))
+        from ._lib import YkError
+        try:
+            call("yk_selfplay", self.handle, seed & (2**64 - 1), env_base & (2**32 - 1), stream_ptr(stream))
+        except YkError as e:
+            st = self.stats()
+            bits = [n for b, n in self.ERROR_BITS.items() if st["errors"] & b]
+            raise YkError(f"yk_selfplay [{', '.join(bits)}; stats {st}]", e.code) from None
 
     KERNEL_CLASSES = ("select", "trunk", "pihead", "expand_backup", "move_begin", "move_end")
 
