@@ -31,9 +31,8 @@ METRIC = "MCTS node-expansions/sec/GPU @4096 envs x100 sims; episodes/sec 1-8 GP
 F32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense f32 matrix peak
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E spec peak
 H, NB, A = 256, 6, 3226
-# algorithmic FLOPs per expansion (per predicted row), YachtNNet.py:24-70 at hidden 256, 6 blocks
-TRUNK_FLOP = 2 * (59 * H + 2 * NB * H * H + H * 128 + 128)
-PIHEAD_FLOP = 2 * H * A
+# algorithmic FLOPs per expansion (one predicted row), YachtNNet.py:24-70 at hidden 256, 6 blocks
+PREDICT_FLOP = 2 * (59 * H + 2 * NB * H * H + H * 128 + 128 + H * A)  # = 3,320,576
 
 
 def cpu_baseline(state_dict, sims, seconds_target=15.0, threads=None):
@@ -161,22 +160,22 @@ def main():
         out["kernel_ms"] = {k: {"avg_ms": round(a, 5), "launches": n, "total_ms": round(t, 2)}
                             for k, (a, n, t) in per.items()}
         dom = max(per, key=lambda k: per[k][2])
-        exp_per_launch = exps / world / max(per["trunk"][1], 1) if per["trunk"][1] else 0.0
-        if dom in ("trunk", "pihead"):
-            flop = (TRUNK_FLOP if dom == "trunk" else PIHEAD_FLOP) * exp_per_launch
+        if dom == "forward":
+            # algorithmic FLOP per launch = expansions predicted per launch x 3,320,576
+            exp_per_launch = exps / world / max(per["forward"][1], 1)
+            flop = PREDICT_FLOP * exp_per_launch
             ach = flop / (per[dom][0] * 1e-3) / 1e12
-            out["roofline"] = {"kernel": dom, "bound": "mfma", "achieved": ach, "peak": F32_MFMA_PEAK_TFLOPS,
-                               "unit": "TFLOP/s", "frac": ach / F32_MFMA_PEAK_TFLOPS, "traffic": None,
-                               "work_per_launch": f"{exp_per_launch:.0f} expansions x "
-                                                  f"{TRUNK_FLOP if dom == 'trunk' else PIHEAD_FLOP} FLOP"}
+            out["roofline"] = {"kernel": "k_forward", "bound": "mfma", "achieved": ach,
+                               "peak": F32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": ach / F32_MFMA_PEAK_TFLOPS,
+                               "traffic": None,
+                               "work_per_launch": f"{exp_per_launch:.0f} expansions x {PREDICT_FLOP} FLOP (f32)"}
         else:
             # env/MCTS kernels: algorithmic bytes = 4*S_scan + 16*D + 4*V_new + 364 per expansion
             scan_b = 4 * st["scanned"] + 16 * st["path_edges"] + 4 * st["vnew"] + 364 * st["expansions"]
-            launches = max(per[dom][1], 1)
             b = scan_b / max(st["sims"], 1)
             ach = b / (per[dom][0] * 1e-3) / 1e9
-            out["roofline"] = {"kernel": dom, "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                               "frac": ach / HBM_PEAK_GBS, "traffic": None,
+            out["roofline"] = {"kernel": "k_" + dom, "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS,
+                               "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "traffic": None,
                                "work_per_launch": f"{b:.0f} algorithmic bytes"}
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(sd, args.sims)

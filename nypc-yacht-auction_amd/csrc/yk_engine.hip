@@ -5,7 +5,7 @@
 //   k_select         one wavefront per game walks its own tree from the root (UCB argmax
 //                    over the compact valid set, transitions with the game's own RNG
 //                    stream) to the first unexpanded state, a terminal, or a dead node;
-//   k_trunk/k_pihead one batched f32-MFMA forward over all pending leaves (yk_net.hip);
+//   k_forward        one batched f32-MFMA forward over all pending leaves (yk_net.hip);
 //   k_expand_backup  one wavefront per game: exp(log_softmax), mask, numpy-pairwise
 //                    renormalise, insert the node, back the value up the path.
 // Within a game the simulations stay strictly sequential, so each game reproduces the
@@ -82,7 +82,10 @@ struct EngDev {
     yk_state_t* leaf_state;
     uint64_t* leaf_hash;
     uint8_t* leaf_flag;
-    uint32_t* path;        // [E][MAXD]: j << 20 | node id
+    uint64_t* path;        // [E][MAXD]: (p_off + j) << 32 | node id
+    int32_t* leaf_row;     // [E]: compact predict row of this game's leaf (-1: none)
+    int32_t* rows;         // [E]: leaf rows -> game
+    int32_t* nrows;        // [1]
     uint8_t* path_len;
     double* res_v;
     uint32_t* res_t;
@@ -378,7 +381,7 @@ __global__ __launch_bounds__(256) void k_select(EngDev d, const uint32_t* env_id
     const Edge* edges = d.edges[g] + (long)e * d.ECAP;
     const float* Pbase = d.arenaP + (long)e * d.AE;
     const uint16_t* Sbase = d.arenaS + (long)e * d.AE;
-    uint32_t* path = d.path + (long)e * MAXD;
+    uint64_t* path = d.path + (long)e * MAXD;
     int depth = 0;
     uint64_t scanned = 0;
     int leaf = 0;
@@ -460,7 +463,7 @@ __global__ __launch_bounds__(256) void k_select(EngDev d, const uint32_t* env_id
             res = PyV{0.0, T_INT};
             break;
         }
-        if (lane == 0) path[depth] = ((uint32_t)j << 20) | (uint32_t)nid;
+        if (lane == 0) path[depth] = ((uint64_t)(nd.p_off + (uint32_t)j) << 32) | (uint32_t)nid;
         depth++;
         const VInfo vi = unpack_vinfo(nd.vinfo, nd.nvalid);
         const int a = compact_to_action(vi, j);
@@ -483,6 +486,40 @@ __global__ __launch_bounds__(256) void k_select(EngDev d, const uint32_t* env_id
         d.gstats[(long)e * 8 + 2] += (uint64_t)depth;
         d.gstats[(long)e * 8 + 7] += 1;
     }
+}
+
+// Compact the games that reached a leaf into predict rows (order-preserving block scan).
+__global__ __launch_bounds__(1024) void k_leaf_scan(EngDev d) {
+    __shared__ int part[1024];
+    const int t = threadIdx.x;
+    const int per = (d.E + 1023) / 1024;
+    const int b0 = t * per;
+    int c = 0;
+    for (int i = 0; i < per; i++) {
+        const int e = b0 + i;
+        if (e < d.E && !d.done[e] && d.leaf_flag[e]) c++;
+    }
+    part[t] = c;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {  // Hillis-Steele inclusive scan
+        const int v = t >= o ? part[t - o] : 0;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    int r = part[t] - c;
+    for (int i = 0; i < per; i++) {
+        const int e = b0 + i;
+        if (e >= d.E) break;
+        if (!d.done[e] && d.leaf_flag[e]) {
+            d.leaf_row[e] = r;
+            d.rows[r] = e;
+            r++;
+        } else {
+            d.leaf_row[e] = -1;
+        }
+    }
+    if (t == 1023) *d.nrows = part[1023];
 }
 
 // Leaf expansion (MCTS.py:84-115) and backup (MCTS.py:154-164).  One wave per game.
@@ -508,19 +545,51 @@ __global__ __launch_bounds__(256) void k_expand_backup(EngDev d) {
         const bool rec = d.rec_pred && pidx < d.max_exp;
         float* rpi = rec ? d.rec_pi + ((long)e * d.max_exp + pidx) * ASIZE : nullptr;
         if (d.prior == 0) {
-            const float* x = d.logits + (long)e * PI_LD;
+            // the whole logits row in registers: 13 float4 per lane, one latency
+            const int row = d.leaf_row[e];
+            const float4* x4 = reinterpret_cast<const float4*>(d.logits + (long)row * PI_LD);
+            constexpr int NV = (PI_LD / 4 + 63) / 64;  // 13
+            float4 xv[NV];
+#pragma unroll
+            for (int i = 0; i < NV; i++) {
+                const int k = lane + 64 * i;
+                xv[i] = k < PI_LD / 4 ? x4[k] : make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+            }
             float m = -INFINITY;
-            for (int a = lane; a < ASIZE; a += 64) m = fmaxf(m, x[a]);
+#pragma unroll
+            for (int i = 0; i < NV; i++) {
+                const int a = 4 * (lane + 64 * i);
+                if (a + 0 < ASIZE) m = fmaxf(m, xv[i].x);
+                if (a + 1 < ASIZE) m = fmaxf(m, xv[i].y);
+                if (a + 2 < ASIZE) m = fmaxf(m, xv[i].z);
+                if (a + 3 < ASIZE) m = fmaxf(m, xv[i].w);
+            }
             m = wave_max(m);
             float se = 0.f;
-            for (int a = lane; a < ASIZE; a += 64) se += expf(x[a] - m);
-            const float lse = logf(wave_sumf(se));
-            for (int a = lane; a < ASIZE; a += 64) {
-                const float p = expf(x[a] - m - lse);
-                if (rec) rpi[a] = p;
-                buf[a] = action_valid(s, 1, a) ? p : 0.0f;  // Ps * valids (MCTS.py:88)
+#pragma unroll
+            for (int i = 0; i < NV; i++) {
+                const int a = 4 * (lane + 64 * i);
+                if (a + 0 < ASIZE) se += expf(xv[i].x - m);
+                if (a + 1 < ASIZE) se += expf(xv[i].y - m);
+                if (a + 2 < ASIZE) se += expf(xv[i].z - m);
+                if (a + 3 < ASIZE) se += expf(xv[i].w - m);
             }
-            v = d.vpred[e];
+            const float lse = logf(wave_sumf(se));
+#pragma unroll
+            for (int i = 0; i < NV; i++) {
+                const int a0 = 4 * (lane + 64 * i);
+                const float xs[4] = {xv[i].x, xv[i].y, xv[i].z, xv[i].w};
+#pragma unroll
+                for (int t = 0; t < 4; t++) {
+                    const int a = a0 + t;
+                    if (a < ASIZE) {
+                        const float p = expf(xs[t] - m - lse);
+                        if (rec) rpi[a] = p;
+                        buf[a] = action_valid(s, 1, a) ? p : 0.0f;  // Ps * valids (MCTS.py:88)
+                    }
+                }
+            }
+            v = d.vpred[row];
         } else {
             for (int a = lane; a < ASIZE; a += 64) {
                 const float p = hash_prior_pi(hsh, a);
@@ -603,40 +672,47 @@ __global__ __launch_bounds__(256) void k_expand_backup(EngDev d) {
         }
         res = PyV{-(double)v, T_F32};  // return -v  (MCTS.py:115)
     }
-    // ---- backup along the path (serial: one game's updates depend on nothing else)
-    if (lane == 0) {
-        const int depth = d.path_len[e];
-        const uint32_t* path = d.path + (long)e * MAXD;
+    // ---- backup (MCTS.py:154-164): the path's nodes are distinct, so every level updates in
+    // parallel; level k receives v * (-1)^(depth-1-k) ("return -v" per level).
+    const int depth = d.path_len[e];
+    if (depth > 0) {
+        const uint64_t* path = d.path + (long)e * MAXD;
         NodeRec* nodes = d.nodes[g] + (long)e * d.NCAP;
         Edge* edges = d.edges[g] + (long)e * d.ECAP;
         uint16_t* Sb = d.arenaS + (long)e * d.AE;
-        uint32_t ne = d.edge_count[g * d.E + e];
-        PyV v = res;
-        for (int k = depth - 1; k >= 0; k--) {
-            const uint32_t pe = path[k];
-            const uint32_t nid = pe & 0xFFFFF, j = pe >> 20;
-            NodeRec& nd = nodes[nid];
-            uint16_t* slot = Sb + nd.p_off + j;
-            const uint16_t sl = *slot;
+        const uint32_t ne0 = d.edge_count[g * d.E + e];
+        uint64_t pe = 0;
+        uint16_t sl = 0;
+        if (lane < depth) {
+            pe = path[lane];
+            sl = Sb[pe >> 32];
+        }
+        const bool is_new = lane < depth && sl == 0;
+        const uint64_t bal = __ballot(is_new);
+        const uint32_t eid = ne0 + (uint32_t)__popcll(bal & ((1ull << lane) - 1));
+        const uint32_t ne1 = ne0 + (uint32_t)__popcll(bal);
+        if (lane < depth) {
+            PyV v = res;
+            if ((depth - 1 - lane) & 1) v.v = -v.v;
             if (sl) {
                 Edge& ed = edges[sl - 1];
                 const PyV q = pv_update(PyV{ed.Q, ed.tag}, ed.N, v);
                 ed.Q = q.v;
                 ed.tag = q.t;
                 ed.N += 1;
-            } else if (ne < (uint32_t)d.ECAP && ne < 65535u) {
-                edges[ne] = Edge{v.v, 1u, v.t};
-                *slot = (uint16_t)(ne + 1);
-                ne++;
+            } else if (eid < (uint32_t)d.ECAP && eid < 65535u) {
+                edges[eid] = Edge{v.v, 1u, v.t};
+                Sb[pe >> 32] = (uint16_t)(eid + 1);
             } else {
                 atomicOr(d.err, ERR_EDGES);
             }
-            nd.Ns += 1;
-            v.v = -v.v;  // return -v
+            nodes[(uint32_t)pe].Ns += 1;
         }
-        d.edge_count[g * d.E + e] = ne;
-        uint64_t* gs = d.gstats + (long)e * 8;
-        if (ne > gs[5]) gs[5] = ne;
+        if (lane == 0) {
+            d.edge_count[g * d.E + e] = ne1;
+            uint64_t* gs = d.gstats + (long)e * 8;
+            if (ne1 > gs[5]) gs[5] = ne1;
+        }
     }
 }
 
@@ -817,7 +893,6 @@ struct yk_engine {
     yk_net_t* net = nullptr;
     EngDev d{};
     std::vector<void*> allocs;
-    float* a_pi = nullptr;
     float* logits = nullptr;
     float* vpred = nullptr;
     float *lut_sq = nullptr, *lut_sqe = nullptr;
@@ -836,7 +911,7 @@ struct yk_engine {
 
 namespace {
 // kernel classes for yk_engine_kernel_times
-enum { KC_SELECT = 0, KC_TRUNK = 1, KC_PIHEAD = 2, KC_EXPAND = 3, KC_MOVE_BEGIN = 4, KC_MOVE_END = 5, KC_N = 8 };
+enum { KC_SELECT = 0, KC_FORWARD = 1, KC_SCAN = 2, KC_EXPAND = 3, KC_MOVE_BEGIN = 4, KC_MOVE_END = 5, KC_N = 8 };
 
 void prof_mark(yk_engine* eng, int cls, hipStream_t s) {  // records an event pair boundary
     if (!eng->prof) return;
@@ -890,11 +965,11 @@ int run_sims(yk_engine* eng, int sims, const uint32_t* env_ids, uint64_t* ctr, h
         hipLaunchKernelGGL(k_select, gb, bb, 0, s, d, env_ids, ctr);
         YK_LAUNCHED();
         if (d.prior == 0) {
-            prof_mark(eng, KC_TRUNK, s);
-            int rc = launch_trunk(eng->net->dev, d.leaf_state, nullptr, nullptr, nullptr, d.E, eng->a_pi, eng->vpred, s);
-            if (rc) return rc;
-            prof_mark(eng, KC_PIHEAD, s);
-            rc = launch_pihead(eng->net->dev, eng->a_pi, nullptr, d.E, eng->logits, s);
+            prof_mark(eng, KC_SCAN, s);
+            hipLaunchKernelGGL(k_leaf_scan, dim3(1), dim3(1024), 0, s, d);
+            YK_LAUNCHED();
+            prof_mark(eng, KC_FORWARD, s);
+            int rc = launch_forward(eng->net->dev, d.leaf_state, nullptr, d.rows, d.nrows, d.E, eng->logits, eng->vpred, s);
             if (rc) return rc;
         }
         prof_mark(eng, KC_EXPAND, s);
@@ -972,6 +1047,9 @@ int yk_engine_create(yk_engine_t** out, const yk_engine_config_t* cfg, yk_net_t*
     A(d.leaf_flag, E);
     A(d.path, E * MAXD);
     A(d.path_len, E);
+    A(d.leaf_row, E);
+    A(d.rows, E);
+    A(d.nrows, 1);
     A(d.res_v, E);
     A(d.res_t, E);
     A(eng->vpred, E);
@@ -990,7 +1068,6 @@ int yk_engine_create(yk_engine_t** out, const yk_engine_config_t* cfg, yk_net_t*
     A(eng->done_count, 1);
     A(eng->mcts_env, E);
     if (d.prior == 0) {
-        A(eng->a_pi, E * (size_t)net->dev.H);
         A(eng->logits, E * (size_t)PI_LD);
     }
     if (d.rec_pred) {

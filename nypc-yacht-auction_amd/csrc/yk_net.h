@@ -7,25 +7,26 @@
 
 namespace yk {
 
-constexpr int PI_LD = 3264;  // logits row stride: 3226 padded to 51 tiles of 64 columns
+constexpr int PI_LD = 3264;         // logits row stride: 3226 padded to 204 tiles of 16 columns
+constexpr int PI_TILES = PI_LD / 16;
 
+// Dense weights are stored in MFMA fragment order ("packed"): for a [N][K] matrix,
+//   P[nt][kb][lane][i] = W[16 nt + (lane & 15)][16 kb + 4 (lane >> 4) + i]
+// so one wave loads a 16-column x 16-deep slice as one contiguous 1 KB float4 access.
 struct NetDev {
     int H, NB;
-    const float *w_in, *b_in, *g_in, *be_in;  // w_in [H][64] (59 used)
-    const float *w1, *b1, *g1, *be1;          // [NB][H][H], [NB][H] ...
+    const float *w_in, *b_in, *g_in, *be_in;  // w_in packed [H/16][4][64][4] (K 59 padded to 64)
+    const float *w1, *b1, *g1, *be1;          // per block: packed [H/16][H/16][64][4], vectors [H]
     const float *w2, *b2, *g2, *be2;
-    const float *g_pi, *be_pi, *w_pi, *b_pi;  // w_pi [PI_LD][H] (rows >= 3226 zero)
-    const float *g_v, *be_v, *w_v1, *b_v1, *w_v2, *b_v2;  // w_v1 [128][H], w_v2 [128], b_v2 [1]
+    const float *g_pi, *be_pi, *w_pi, *b_pi;  // w_pi packed [204][H/16][64][4] (rows >= 3226 zero), b_pi [3264]
+    const float *g_v, *be_v, *w_v1, *b_v1, *w_v2, *b_v2;  // w_v1 packed [8][H/16][64][4], w_v2 [128], b_v2 [1]
 };
 
-// Trunk: features (from packed states, or explicit rows x[n][59]) -> a_pi[n][H] =
-// SiLU(LN_pi(h)) and v[n] = tanh(v_head(h)).  `rows` (optional) maps output row i to
-// input state index rows[i]; `count` (optional, device) overrides n.
-int launch_trunk(const NetDev& net, const yk_state_t* states, const float* x, const int32_t* rows,
-                 const int32_t* count, int n, float* a_pi, float* v, hipStream_t stream);
-// logits[n][PI_LD] = a_pi @ w_pi^T + b_pi  (f32 MFMA)
-int launch_pihead(const NetDev& net, const float* a_pi, const int32_t* count, int n, float* logits,
-                  hipStream_t stream);
+// Full forward: features (from packed states, or explicit rows x[n][59]) ->
+// logits[n][PI_LD] (pi_head before softmax) and v[n] = tanh(v_head).  `rows` (optional) maps
+// output row i to input index rows[i]; `count` (optional, device) overrides n.
+int launch_forward(const NetDev& net, const yk_state_t* states, const float* x, const int32_t* rows,
+                   const int32_t* count, int n, float* logits, float* v, hipStream_t stream);
 // pi[n][3226] = exp(log_softmax(logits[:, :3226]))
 int launch_softmax(const float* logits, float* pi, int n, hipStream_t stream);
 

@@ -1,14 +1,14 @@
 // yk_net.hip - NNetWrapper.predict (yacht/NNet.py:177-195) over YachtNNet
 // (yacht/pytorch/YachtNNet.py:8-70), batched over all pending leaves, float32.
 //
-// Two kernels carry the FLOPs (3,320,576 per row at H=256, 6 blocks):
-//  * k_trunk: one 256-thread workgroup per 16 rows keeps the whole activation tile in
-//    LDS across all 13 dense layers (featurize -> Linear/LN/SiLU -> 6 x ResidualBlock ->
-//    head LayerNorms -> value head).  Each dense layer is [16 x K] x [K x N] on
-//    v_mfma_f32_16x16x4_f32; the four waves split N; weights stream from L2.
-//  * k_pihead: logits = a_pi @ W_pi^T + b over 64 x 64 output tiles (f32 MFMA).
-// f32-in MFMA is exact f32 (fmaf chain), so results track torch's float32 CPU path
-// within the 1e-5 tolerance of the north star (tests/test_gpu_net.py).
+// One kernel, k_forward, carries all 3,320,576 FLOP per row (hidden 256, 6 blocks): a
+// 1024-thread workgroup (16 waves, 4 per SIMD) owns 16 rows and keeps their activations in
+// LDS through featurize -> Linear/LN/SiLU -> 6 x ResidualBlock -> head LayerNorms ->
+// policy logits (204 x 16 columns) and the value head.  Every dense layer runs on
+// v_mfma_f32_16x16x4_f32 (exact f32: fmaf chains), so results track torch's float32 CPU
+// path within the north star's 1e-5 (tests/test_gpu_net.py).  Weights are pre-packed in
+// MFMA fragment order (yk_net.h) so each wave streams them as contiguous 1 KB loads, and
+// the next layer's slice is issued before the LayerNorm phase so it flies under it.
 #include <vector>
 
 #include "yk_api.h"
@@ -19,10 +19,16 @@ using namespace yk;
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
+// Diagnostic builds only (tools/trunk_ablate.cpp): 2 = no MFMA, 3 = no weight loads.
+#ifndef YK_ABL
+#define YK_ABL 0
+#endif
+
 namespace {
 
-constexpr int ROWS = 16;  // rows per trunk workgroup
+constexpr int ROWS = 16;  // rows per workgroup
 constexpr int FPAD = 68;  // feature tile row stride (64 + 4)
+constexpr int PCH = 4;    // policy-head tiles per chunk (accumulators in flight per wave)
 
 __device__ __forceinline__ float silu(float x) { return x / (1.0f + expf(-x)); }
 
@@ -32,42 +38,72 @@ __device__ __forceinline__ float wave_sum(float v) {
     return v;
 }
 
-// acc[t] += A[16 x K] (LDS, row stride lda) x W[n0 + 16t .. +16][K]^T (global, row stride ldw)
-// Lane l supplies A[l&15][k0 + 4(l>>4) + i] and W[.][k0 + 4(l>>4) + i] to MFMA i of each
-// 16-deep k-block, so each lane's operands are one float4 from each source.
-template <int K, int NT>
-__device__ __forceinline__ void gemm16(const float* A, int lda, const float* __restrict__ W, int ldw, int n0,
-                                       floatx4 (&acc)[NT]) {
-    const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
-#pragma unroll
-    for (int t = 0; t < NT; t++) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
-    const float* wrow[NT];
-#pragma unroll
-    for (int t = 0; t < NT; t++) wrow[t] = W + (long)(n0 + 16 * t + r) * ldw + 4 * q;
-#pragma unroll 2
-    for (int k0 = 0; k0 < K; k0 += 16) {
-        const float4 a = *reinterpret_cast<const float4*>(A + r * lda + k0 + 4 * q);
-        float4 b[NT];
-#pragma unroll
-        for (int t = 0; t < NT; t++) b[t] = *reinterpret_cast<const float4*>(wrow[t] + k0);
-#pragma unroll
-        for (int t = 0; t < NT; t++) {
-            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b[t].x, acc[t], 0, 0, 0);
-            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b[t].y, acc[t], 0, 0, 0);
-            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b[t].z, acc[t], 0, 0, 0);
-            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b[t].w, acc[t], 0, 0, 0);
-        }
-    }
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops, NOT for its
+// outstanding global loads (a __syncthreads() would drain vmcnt and expose the weight
+// stream's latency at every layer).
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+__device__ __forceinline__ float4 ld_frag(const float* __restrict__ P, int KB, int nt, int kb, int lane) {
+#if YK_ABL == 3
+    return make_float4(1e-3f * kb, 1e-3f * nt, 2e-3f, 3e-3f + P[0] * 0.f);
+#else
+    return *reinterpret_cast<const float4*>(P + ((long)(nt * KB + kb) * 64 + lane) * 4);
+#endif
 }
 
-// D[16 x 16] tile t of the wave: lane holds rows 4(l>>4)+j, column n0 + 16t + (l&15)
+// A wave's weight slice for one dense layer: NT 16-column tiles starting at tile nt0, all K.
+template <int K, int NT>
+struct WSlice {
+    float4 b[K / 16][NT];
+};
+template <int K, int NT>
+__device__ __forceinline__ void load_w(WSlice<K, NT>& ws, const float* __restrict__ P, int nt0) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int kb = 0; kb < K / 16; kb++)
+#pragma unroll
+        for (int t = 0; t < NT; t++) ws.b[kb][t] = ld_frag(P, K / 16, nt0 + t, kb, lane);
+    __builtin_amdgcn_sched_barrier(0);  // issue them here, ahead of the work that hides them
+}
+
+// acc[t] = A[16 x K] (LDS, row stride lda) x slice^T.  Lane l supplies A[l&15][16kb + 4(l>>4) + i]
+// and W[.][16kb + 4(l>>4) + i] to MFMA i of each 16-deep k-block.  Two partial accumulators
+// keep consecutive MFMAs independent (40-cycle dependent latency vs 32-cycle issue).
+template <int K, int NT>
+__device__ __forceinline__ void mma16(const float* A, int lda, const WSlice<K, NT>& ws, floatx4 (&acc)[NT]) {
+    const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
+    floatx4 acc2[NT];
+#pragma unroll
+    for (int t = 0; t < NT; t++) acc[t] = acc2[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+    const float* ap = A + r * lda + 4 * q;
+#if YK_ABL == 2
+    acc[0][0] = ap[0] + ws.b[0][0].x;
+    return;
+#endif
+#pragma unroll
+    for (int kb = 0; kb < K / 16; kb++) {
+        const float4 a = *reinterpret_cast<const float4*>(ap + 16 * kb);
+#pragma unroll
+        for (int t = 0; t < NT; t++) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, ws.b[kb][t].x, acc[t], 0, 0, 0);
+#pragma unroll
+        for (int t = 0; t < NT; t++) acc2[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, ws.b[kb][t].y, acc2[t], 0, 0, 0);
+#pragma unroll
+        for (int t = 0; t < NT; t++) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, ws.b[kb][t].z, acc[t], 0, 0, 0);
+#pragma unroll
+        for (int t = 0; t < NT; t++) acc2[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, ws.b[kb][t].w, acc2[t], 0, 0, 0);
+    }
+#pragma unroll
+    for (int t = 0; t < NT; t++) acc[t] += acc2[t];
+}
+
+// D[16 x 16] tile t of the wave: lane holds rows 4(l>>4)+j, column 16(nt0 + t) + (l&15)
 template <int NT>
-__device__ __forceinline__ void store_acc(float* D, int ldd, int n0, const floatx4 (&acc)[NT],
+__device__ __forceinline__ void store_acc(float* D, int ldd, int nt0, const floatx4 (&acc)[NT],
                                           const float* __restrict__ bias) {
     const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
 #pragma unroll
     for (int t = 0; t < NT; t++) {
-        const int c = n0 + 16 * t + r;
+        const int c = 16 * (nt0 + t) + r;
         const float b = bias[c];
 #pragma unroll
         for (int j = 0; j < 4; j++) D[(4 * q + j) * ldd + c] = acc[t][j] + b;
@@ -93,14 +129,18 @@ __device__ __forceinline__ void layernorm(float (&x)[VPL], const float* __restri
     for (int i = 0; i < VPL; i++) x[i] = (x[i] - mean) * rstd * g[c0 + i] + b[c0 + i];
 }
 
+// Dense layers: wave w owns output tiles [NT w, NT (w+1)); row passes (LayerNorm / SiLU /
+// residual): wave w owns row w; policy head: wave w owns tiles w, w + 16, w + 32, ...
 template <int H>
-__global__ __launch_bounds__(256) void k_trunk(NetDev net, const yk_state_t* __restrict__ states,
-                                              const float* __restrict__ xin, const int32_t* __restrict__ rows,
-                                              const int32_t* __restrict__ count, int n, float* __restrict__ a_pi,
-                                              float* __restrict__ vout) {
+__global__ __launch_bounds__(1024) void k_forward(NetDev net, const yk_state_t* __restrict__ states,
+                                                 const float* __restrict__ xin, const int32_t* __restrict__ rows,
+                                                 const int32_t* __restrict__ count, int n,
+                                                 float* __restrict__ logits, float* __restrict__ vout) {
     constexpr int LD = (H > 128 ? H : 128) + 4;  // X also holds the 128-wide v_head hidden
-    constexpr int NT = H / 64;  // 16-col tiles per wave (4 waves split H)
-    constexpr int VPL = H / 64; // values per lane in row passes
+    constexpr int NT = H >= 256 ? H / 256 : 1;    // 16-col tiles per wave in H-wide layers
+    constexpr int NACT = H / (16 * NT);           // waves with columns of the H-wide layers
+    constexpr int VPL = H / 64;                   // values per lane in row passes
+    constexpr int KB = H / 16;
     __shared__ __attribute__((aligned(16))) float X[ROWS * LD];
     __shared__ __attribute__((aligned(16))) float T[ROWS * LD];
     __shared__ __attribute__((aligned(16))) float F[ROWS * FPAD];
@@ -109,11 +149,16 @@ __global__ __launch_bounds__(256) void k_trunk(NetDev net, const yk_state_t* __r
     const int row0 = blockIdx.x * ROWS;
     if (row0 >= n) return;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const bool gw = wave < NACT;           // owns columns of the H-wide layers
+    const bool vw = wave * 16 * NT < 128;  // owns columns of v_head.2
+    const int nt0 = wave * NT;
+    const int r = wave;  // row of the row passes
+    const int c0 = lane * VPL;
 
-    // featurize (state_to_vec, NNet.py:65-86), zero padded to K = 64
-    for (int idx = tid; idx < ROWS * 64; idx += 256) {
-        const int r = idx >> 6, f = idx & 63;
-        const int row = row0 + r;
+    // featurize (state_to_vec, NNet.py:65-86), zero padded to K = 64: one value per thread
+    {
+        const int rr = tid >> 6, f = tid & 63;
+        const int row = row0 + rr;
         float val = 0.f;
         if (row < n && f < FEAT) {
             const int src = rows ? rows[row] : row;
@@ -131,131 +176,157 @@ __global__ __launch_bounds__(256) void k_trunk(NetDev net, const yk_state_t* __r
                 val = feature(s, f);
             }
         }
-        F[r * FPAD + f] = val;
+        F[rr * FPAD + f] = val;
     }
-    __syncthreads();
+    lds_barrier();
 
-    const int n0 = wave * (H / 4);
     floatx4 acc[NT];
+    WSlice<H, NT> ws;  // next dense layer's weights, in flight during the row passes
     // inp: Linear -> LayerNorm -> SiLU (-> Dropout, identity in eval)  YachtNNet.py:30-35
-    gemm16<64, NT>(F, FPAD, net.w_in, 64, n0, acc);
-    store_acc<NT>(T, LD, n0, acc, net.b_in);
-    __syncthreads();
-    for (int rr = 0; rr < 4; rr++) {
-        const int r = wave * 4 + rr;
+    if (gw) {
+        WSlice<64, NT> w0;
+        load_w<64, NT>(w0, net.w_in, nt0);
+        if (net.NB > 0) load_w<H, NT>(ws, net.w1, nt0);
+        mma16<64, NT>(F, FPAD, w0, acc);
+        store_acc<NT>(T, LD, nt0, acc, net.b_in);
+    }
+    lds_barrier();
+    {
         float x[VPL];
 #pragma unroll
-        for (int i = 0; i < VPL; i++) x[i] = T[r * LD + lane * VPL + i];
-        layernorm<VPL>(x, net.g_in, net.be_in, lane * VPL, H);
+        for (int i = 0; i < VPL; i++) x[i] = T[r * LD + c0 + i];
+        layernorm<VPL>(x, net.g_in, net.be_in, c0, H);
 #pragma unroll
-        for (int i = 0; i < VPL; i++) X[r * LD + lane * VPL + i] = silu(x[i]);
+        for (int i = 0; i < VPL; i++) X[r * LD + c0 + i] = silu(x[i]);
     }
-    __syncthreads();
+    lds_barrier();
 
     // ResidualBlock x NB: h = LN1(SiLU(fc1 x)); h = LN2(SiLU(fc2 h)); x + h  YachtNNet.py:17-21
     for (int b = 0; b < net.NB; b++) {
         const long wo = (long)b * H * H, bo = (long)b * H;
-        gemm16<H, NT>(X, LD, net.w1 + wo, H, n0, acc);
-        store_acc<NT>(T, LD, n0, acc, net.b1 + bo);
-        __syncthreads();
-        for (int rr = 0; rr < 4; rr++) {
-            const int r = wave * 4 + rr;
+        if (gw) {
+            mma16<H, NT>(X, LD, ws, acc);
+            load_w<H, NT>(ws, net.w2 + wo, nt0);  // fc2 weights fly during LN1
+            store_acc<NT>(T, LD, nt0, acc, net.b1 + bo);
+        }
+        lds_barrier();
+        {
             float x[VPL];
 #pragma unroll
-            for (int i = 0; i < VPL; i++) x[i] = silu(T[r * LD + lane * VPL + i]);
-            layernorm<VPL>(x, net.g1 + bo, net.be1 + bo, lane * VPL, H);
+            for (int i = 0; i < VPL; i++) x[i] = silu(T[r * LD + c0 + i]);
+            layernorm<VPL>(x, net.g1 + bo, net.be1 + bo, c0, H);
 #pragma unroll
-            for (int i = 0; i < VPL; i++) T[r * LD + lane * VPL + i] = x[i];
+            for (int i = 0; i < VPL; i++) T[r * LD + c0 + i] = x[i];
         }
-        __syncthreads();
-        gemm16<H, NT>(T, LD, net.w2 + wo, H, n0, acc);
-        __syncthreads();
-        store_acc<NT>(T, LD, n0, acc, net.b2 + bo);
-        __syncthreads();
-        for (int rr = 0; rr < 4; rr++) {
-            const int r = wave * 4 + rr;
+        lds_barrier();
+        if (gw) mma16<H, NT>(T, LD, ws, acc);
+        if (b + 1 < net.NB) {
+            if (gw) load_w<H, NT>(ws, net.w1 + wo + (long)H * H, nt0);  // next fc1
+        } else if (vw) {
+            load_w<H, NT>(ws, net.w_v1, nt0);  // v_head.2
+        }
+        lds_barrier();
+        if (gw) store_acc<NT>(T, LD, nt0, acc, net.b2 + bo);
+        lds_barrier();
+        {
             float x[VPL];
 #pragma unroll
-            for (int i = 0; i < VPL; i++) x[i] = silu(T[r * LD + lane * VPL + i]);
-            layernorm<VPL>(x, net.g2 + bo, net.be2 + bo, lane * VPL, H);
+            for (int i = 0; i < VPL; i++) x[i] = silu(T[r * LD + c0 + i]);
+            layernorm<VPL>(x, net.g2 + bo, net.be2 + bo, c0, H);
 #pragma unroll
-            for (int i = 0; i < VPL; i++) X[r * LD + lane * VPL + i] += x[i];
+            for (int i = 0; i < VPL; i++) X[r * LD + c0 + i] += x[i];
         }
-        __syncthreads();
+        lds_barrier();
     }
 
-    // heads: pi_head = LN -> SiLU -> (Linear in k_pihead); v_head = LN -> SiLU -> ...
-    for (int rr = 0; rr < 4; rr++) {
-        const int r = wave * 4 + rr;
-        const int row = row0 + r;
+    // heads: pi_head = LN -> SiLU -> Linear; v_head = LN -> SiLU -> Linear -> SiLU -> Linear -> tanh
+    {
         float x[VPL], y[VPL];
 #pragma unroll
-        for (int i = 0; i < VPL; i++) x[i] = y[i] = X[r * LD + lane * VPL + i];
-        layernorm<VPL>(x, net.g_pi, net.be_pi, lane * VPL, H);
-        layernorm<VPL>(y, net.g_v, net.be_v, lane * VPL, H);
-        if (row < n) {
+        for (int i = 0; i < VPL; i++) x[i] = y[i] = X[r * LD + c0 + i];
+        layernorm<VPL>(x, net.g_pi, net.be_pi, c0, H);
+        layernorm<VPL>(y, net.g_v, net.be_v, c0, H);
 #pragma unroll
-            for (int i = 0; i < VPL; i++) a_pi[(long)row * H + lane * VPL + i] = silu(x[i]);
+        for (int i = 0; i < VPL; i++) {
+            X[r * LD + c0 + i] = silu(x[i]);  // a_pi (each wave rewrites only its own row)
+            T[r * LD + c0 + i] = silu(y[i]);  // a_v
         }
+    }
+    lds_barrier();
+    floatx4 av[NT];
+    if (vw) {  // v_head.2: Linear(H, 128) (weights already in flight)
+        if (net.NB == 0) load_w<H, NT>(ws, net.w_v1, nt0);
+        mma16<H, NT>(T, LD, ws, av);
+    }
+    // policy head (pi_head.2): 204 tiles of 16 columns over the 16 waves, PCH at a time,
+    // with the next k-block's weight fragments in flight
+    for (int c = 0; c * 16 * PCH < PI_TILES; c++) {
+        floatx4 pa[PCH];
+        float4 wb[2][PCH];
+        const int tbase = wave + 16 * PCH * c;  // tile of slot t: tbase + 16 t (wave-uniform)
+        const int ntile = min(PCH, (PI_TILES - tbase + 15) / 16);
+        if (ntile <= 0) break;
 #pragma unroll
-        for (int i = 0; i < VPL; i++) T[r * LD + lane * VPL + i] = silu(y[i]);
+        for (int t = 0; t < PCH; t++) {
+            pa[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+            if (t < ntile) wb[0][t] = ld_frag(net.w_pi, KB, tbase + 16 * t, 0, lane);
+        }
+        const float* ap = X + (lane & 15) * LD + 4 * (lane >> 4);
+#pragma unroll
+        for (int kb = 0; kb < KB; kb++) {
+            if (kb + 1 < KB) {
+#pragma unroll
+                for (int t = 0; t < PCH; t++)
+                    if (t < ntile) wb[(kb + 1) & 1][t] = ld_frag(net.w_pi, KB, tbase + 16 * t, kb + 1, lane);
+            }
+            const float4 a = *reinterpret_cast<const float4*>(ap + 16 * kb);
+            const int cb = kb & 1;
+#if YK_ABL != 2
+            if (ntile == PCH) {
+#pragma unroll
+                for (int t = 0; t < PCH; t++) pa[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, wb[cb][t].x, pa[t], 0, 0, 0);
+#pragma unroll
+                for (int t = 0; t < PCH; t++) pa[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, wb[cb][t].y, pa[t], 0, 0, 0);
+#pragma unroll
+                for (int t = 0; t < PCH; t++) pa[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, wb[cb][t].z, pa[t], 0, 0, 0);
+#pragma unroll
+                for (int t = 0; t < PCH; t++) pa[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, wb[cb][t].w, pa[t], 0, 0, 0);
+            } else {
+#pragma unroll
+                for (int t = 0; t < PCH; t++)
+                    if (t < ntile) {
+                        pa[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, wb[cb][t].x, pa[t], 0, 0, 0);
+                        pa[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, wb[cb][t].y, pa[t], 0, 0, 0);
+                        pa[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, wb[cb][t].z, pa[t], 0, 0, 0);
+                        pa[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, wb[cb][t].w, pa[t], 0, 0, 0);
+                    }
+            }
+#else
+            pa[0][0] += a.x + wb[cb][0].x;
+#endif
+        }
+        const int rr = lane & 15, q = lane >> 4;
+#pragma unroll
+        for (int t = 0; t < PCH; t++) {
+            if (t < ntile) {
+                const int col = 16 * (tbase + 16 * t) + rr;
+                const float bias = net.b_pi[col];
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const int row = row0 + 4 * q + j;
+                    if (row < n) logits[(long)row * PI_LD + col] = pa[t][j] + bias;
+                }
+            }
+        }
     }
-    __syncthreads();
-    {  // v_head.2: Linear(H, 128), 4 waves x 32 columns
-        floatx4 av[2];
-        gemm16<H, 2>(T, LD, net.w_v1, H, wave * 32, av);
-        store_acc<2>(X, LD, wave * 32, av, net.b_v1);
-    }
-    __syncthreads();
-    for (int rr = 0; rr < 4; rr++) {  // SiLU -> Linear(128, 1) -> tanh  YachtNNet.py:49-52,69
-        const int r = wave * 4 + rr;
+    lds_barrier();  // every wave is done reading a_pi (X)
+    if (vw) store_acc<NT>(X, LD, nt0, av, net.b_v1);
+    lds_barrier();
+    {  // SiLU -> Linear(128, 1) -> tanh  YachtNNet.py:49-52,69
         const int row = row0 + r;
         float s = silu(X[r * LD + 2 * lane]) * net.w_v2[2 * lane] + silu(X[r * LD + 2 * lane + 1]) * net.w_v2[2 * lane + 1];
         s = wave_sum(s);
         if (lane == 0 && row < n) vout[row] = tanhf(s + net.b_v2[0]);
-    }
-}
-
-// logits tile 64 x 64 per workgroup; wave w owns rows 16w..16w+15, four 16-col tiles
-template <int H>
-__global__ __launch_bounds__(256) void k_pihead(NetDev net, const float* __restrict__ a_pi,
-                                               const int32_t* __restrict__ count, int n, float* __restrict__ logits) {
-    if (count) n = min(n, *count);
-    const int rb = blockIdx.y * 64;
-    if (rb >= n) return;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
-    const int c0 = blockIdx.x * 64;
-    const int row_a = min(rb + wave * 16 + r, n - 1);
-    const float* arow = a_pi + (long)row_a * H + 4 * q;
-    const float* wrow[4];
-#pragma unroll
-    for (int t = 0; t < 4; t++) wrow[t] = net.w_pi + (long)(c0 + 16 * t + r) * H + 4 * q;
-    floatx4 acc[4];
-#pragma unroll
-    for (int t = 0; t < 4; t++) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 2
-    for (int k0 = 0; k0 < H; k0 += 16) {
-        const float4 a = *reinterpret_cast<const float4*>(arow + k0);
-        float4 b[4];
-#pragma unroll
-        for (int t = 0; t < 4; t++) b[t] = *reinterpret_cast<const float4*>(wrow[t] + k0);
-#pragma unroll
-        for (int t = 0; t < 4; t++) {
-            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b[t].x, acc[t], 0, 0, 0);
-            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b[t].y, acc[t], 0, 0, 0);
-            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b[t].z, acc[t], 0, 0, 0);
-            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b[t].w, acc[t], 0, 0, 0);
-        }
-    }
-#pragma unroll
-    for (int t = 0; t < 4; t++) {
-        const int c = c0 + 16 * t + r;
-        const float b = net.b_pi[c];
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const int row = rb + wave * 16 + 4 * q + j;
-            if (row < n) logits[(long)row * PI_LD + c] = acc[t][j] + b;
-        }
     }
 }
 
@@ -278,30 +349,15 @@ __global__ void k_softmax(const float* __restrict__ logits, float* __restrict__ 
 
 namespace yk {
 
-int launch_trunk(const NetDev& net, const yk_state_t* states, const float* x, const int32_t* rows,
-                 const int32_t* count, int n, float* a_pi, float* v, hipStream_t stream) {
+int launch_forward(const NetDev& net, const yk_state_t* states, const float* x, const int32_t* rows,
+                   const int32_t* count, int n, float* logits, float* v, hipStream_t stream) {
     if (n <= 0) return YK_OK;
-    const dim3 grid((n + ROWS - 1) / ROWS), block(256);
+    const dim3 grid((n + ROWS - 1) / ROWS), block(1024);
     switch (net.H) {
-        case 64: hipLaunchKernelGGL(k_trunk<64>, grid, block, 0, stream, net, states, x, rows, count, n, a_pi, v); break;
-        case 128: hipLaunchKernelGGL(k_trunk<128>, grid, block, 0, stream, net, states, x, rows, count, n, a_pi, v); break;
-        case 256: hipLaunchKernelGGL(k_trunk<256>, grid, block, 0, stream, net, states, x, rows, count, n, a_pi, v); break;
-        case 512: hipLaunchKernelGGL(k_trunk<512>, grid, block, 0, stream, net, states, x, rows, count, n, a_pi, v); break;
-        default: return YK_ERR_ARG;
-    }
-    YK_LAUNCHED();
-    return YK_OK;
-}
-
-int launch_pihead(const NetDev& net, const float* a_pi, const int32_t* count, int n, float* logits,
-                  hipStream_t stream) {
-    if (n <= 0) return YK_OK;
-    const dim3 grid(PI_LD / 64, (n + 63) / 64), block(256);
-    switch (net.H) {
-        case 64: hipLaunchKernelGGL(k_pihead<64>, grid, block, 0, stream, net, a_pi, count, n, logits); break;
-        case 128: hipLaunchKernelGGL(k_pihead<128>, grid, block, 0, stream, net, a_pi, count, n, logits); break;
-        case 256: hipLaunchKernelGGL(k_pihead<256>, grid, block, 0, stream, net, a_pi, count, n, logits); break;
-        case 512: hipLaunchKernelGGL(k_pihead<512>, grid, block, 0, stream, net, a_pi, count, n, logits); break;
+        case 64: hipLaunchKernelGGL(k_forward<64>, grid, block, 0, stream, net, states, x, rows, count, n, logits, v); break;
+        case 128: hipLaunchKernelGGL(k_forward<128>, grid, block, 0, stream, net, states, x, rows, count, n, logits, v); break;
+        case 256: hipLaunchKernelGGL(k_forward<256>, grid, block, 0, stream, net, states, x, rows, count, n, logits, v); break;
+        case 512: hipLaunchKernelGGL(k_forward<512>, grid, block, 0, stream, net, states, x, rows, count, n, logits, v); break;
         default: return YK_ERR_ARG;
     }
     YK_LAUNCHED();
@@ -323,9 +379,21 @@ int yk_net_create(yk_net_t** out, int H, int NB, const float* const* p, int npar
     if (!out || !p) return YK_ERR_ARG;
     if (!(H == 64 || H == 128 || H == 256 || H == 512) || NB < 0 || NB > 64) return YK_ERR_ARG;
     if (nparams != 14 + 8 * NB) return YK_ERR_ARG;
-    // host staging of the device layout
+    // host staging of the device layout (every block 256-byte aligned)
     std::vector<float> h;
     auto put = [&](size_t n) { size_t o = h.size(); h.resize(o + ((n + 63) / 64) * 64, 0.f); return o; };
+    // torch [N][K] row-major (K valid columns) -> fragment order, N padded to Np, K to Kp
+    auto pack = [&](size_t dst, const float* W, int N, int K, int Np, int Kp) {
+        const int KBp = Kp / 16;
+        for (int nt = 0; nt < Np / 16; nt++)
+            for (int kb = 0; kb < KBp; kb++)
+                for (int l = 0; l < 64; l++)
+                    for (int i = 0; i < 4; i++) {
+                        const int nn = 16 * nt + (l & 15), kk = 16 * kb + 4 * (l >> 4) + i;
+                        h[dst + (((size_t)nt * KBp + kb) * 64 + l) * 4 + i] =
+                            (nn < N && kk < K) ? W[(size_t)nn * K + kk] : 0.f;
+                    }
+    };
     const size_t o_win = put((size_t)H * 64), o_bin = put(H), o_gin = put(H), o_bein = put(H);
     const size_t o_w1 = put((size_t)NB * H * H), o_b1 = put((size_t)NB * H), o_g1 = put((size_t)NB * H),
                  o_be1 = put((size_t)NB * H);
@@ -335,19 +403,21 @@ int yk_net_create(yk_net_t** out, int H, int NB, const float* const* p, int npar
     const size_t o_gv = put(H), o_bev = put(H), o_wv1 = put((size_t)128 * H), o_bv1 = put(128), o_wv2 = put(128),
                  o_bv2 = put(1);
     int k = 0;
-    for (int o = 0; o < H; o++)
-        for (int i = 0; i < FEAT; i++) h[o_win + (size_t)o * 64 + i] = p[k][(size_t)o * FEAT + i];
-    k++;
     auto cp = [&](size_t off, size_t n) { std::copy(p[k], p[k] + n, h.begin() + off); k++; };
+    pack(o_win, p[k++], H, FEAT, H, 64);
     cp(o_bin, H); cp(o_gin, H); cp(o_bein, H);
     for (int b = 0; b < NB; b++) {
-        cp(o_w1 + (size_t)b * H * H, (size_t)H * H); cp(o_b1 + (size_t)b * H, H);
+        pack(o_w1 + (size_t)b * H * H, p[k++], H, H, H, H); cp(o_b1 + (size_t)b * H, H);
         cp(o_g1 + (size_t)b * H, H); cp(o_be1 + (size_t)b * H, H);
-        cp(o_w2 + (size_t)b * H * H, (size_t)H * H); cp(o_b2 + (size_t)b * H, H);
+        pack(o_w2 + (size_t)b * H * H, p[k++], H, H, H, H); cp(o_b2 + (size_t)b * H, H);
         cp(o_g2 + (size_t)b * H, H); cp(o_be2 + (size_t)b * H, H);
     }
-    cp(o_gpi, H); cp(o_bepi, H); cp(o_wpi, (size_t)ASIZE * H); cp(o_bpi, ASIZE);
-    cp(o_gv, H); cp(o_bev, H); cp(o_wv1, (size_t)128 * H); cp(o_bv1, 128); cp(o_wv2, 128); cp(o_bv2, 1);
+    cp(o_gpi, H); cp(o_bepi, H);
+    pack(o_wpi, p[k++], ASIZE, H, PI_LD, H);
+    cp(o_bpi, ASIZE);
+    cp(o_gv, H); cp(o_bev, H);
+    pack(o_wv1, p[k++], 128, H, 128, H);
+    cp(o_bv1, 128); cp(o_wv2, 128); cp(o_bv2, 1);
 
     yk_net* net = new yk_net();
     net->bytes = h.size() * sizeof(float);
@@ -384,13 +454,10 @@ static int predict_common(yk_net_t* net, const yk_state_t* states, const float* 
     if (!net || !pi || !v || n < 0) return YK_ERR_ARG;
     if (n == 0) return YK_OK;
     hipStream_t s = as_stream(stream);
-    float *a_pi = nullptr, *logits = nullptr;
-    YK_HIP(hipMallocAsync((void**)&a_pi, sizeof(float) * (size_t)n * net->dev.H, s));
+    float* logits = nullptr;
     YK_HIP(hipMallocAsync((void**)&logits, sizeof(float) * (size_t)n * PI_LD, s));
-    int rc = launch_trunk(net->dev, states, x, nullptr, nullptr, n, a_pi, v, s);
-    if (rc == YK_OK) rc = launch_pihead(net->dev, a_pi, nullptr, n, logits, s);
+    int rc = launch_forward(net->dev, states, x, nullptr, nullptr, n, logits, v, s);
     if (rc == YK_OK) rc = launch_softmax(logits, pi, n, s);
-    (void)hipFreeAsync(a_pi, s);
     (void)hipFreeAsync(logits, s);
     return rc;
 }

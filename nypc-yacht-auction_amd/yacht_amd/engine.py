@@ -50,7 +50,7 @@ class SelfPlayEngine:
             bits = [n for b, n in self.ERROR_BITS.items() if st["errors"] & b]
             raise YkError(f"yk_selfplay [{', '.join(bits)}; stats {st}]", e.code) from None
 
-    KERNEL_CLASSES = ("select", "trunk", "pihead", "expand_backup", "move_begin", "move_end")
+    KERNEL_CLASSES = ("select", "forward", "leaf_scan", "expand_backup", "move_begin", "move_end")
 
     def profile(self, enable: bool = True):
         call("yk_engine_profile", self.handle, int(enable))
