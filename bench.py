@@ -69,6 +69,7 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel event timing")
+    ap.add_argument("--dist-backend", default=None, help="nccl (RCCL, default on GPUs) or gloo (rehearsal)")
     args = ap.parse_args()
 
     import torch
@@ -78,10 +79,10 @@ def main():
     from yacht_amd.engine import SelfPlayEngine
     from yacht_amd.nnet import YachtNNet, YkNet
 
-    rank, world, local = D.setup()
+    rank, world, local = D.setup(args.dist_backend)
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local)
+    torch.cuda.set_device(D.device_index(local))
     torch.manual_seed(args.seed)
     model = YachtNNet(hidden=H, nblocks=NB)  # random init of the reference architecture
     sd = model.state_dict()
@@ -91,6 +92,8 @@ def main():
     env_base = D.env_base(rank, args.envs)
     gathered_bytes = 0
 
+    last_gather = [None]
+
     def step(i):
         nonlocal gathered_bytes
         eng.run(args.seed + i, env_base, stream)
@@ -98,6 +101,7 @@ def main():
             buf = eng.pack_records(stream=stream)
             g = D.allgather_records(buf)
             gathered_bytes = g.numel()
+            last_gather[0] = g
 
     for i in range(args.warmup):
         step(i)
@@ -127,7 +131,7 @@ def main():
         raise SystemExit(f"engine error flags {st['errors']}")
 
     tot = torch.tensor([elapsed, float(exps), float(games)], dtype=torch.float64,
-                       device="cuda" if world > 1 else "cpu")
+                       device="cuda" if world > 1 and dist.get_backend() == "nccl" else "cpu")
     if world > 1:
         t_max = tot[:1].clone()
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
@@ -153,7 +157,15 @@ def main():
         "expansions_per_episode_batch": exps / args.steps,
     }
     if world > 1:
+        # the pooled replay buffer holds every rank's complete games (48 moves each), and
+        # the ranks played different games (global env ids)
+        from yacht_amd.engine import unpack_record_image
+        imgs = [unpack_record_image(last_gather[0][r].cpu().numpy(), args.envs, 64, args.sims) for r in range(world)]
+        ok = all(bool((im["n_moves"] == 48).all()) for im in imgs)
+        ok = ok and len({im["final"].tobytes() for im in imgs}) == world
+        out["allgather_check"] = "ok" if ok else "FAILED"
         out["allgather_bytes"] = gathered_bytes
+        out["dist_backend"] = dist.get_backend()
     if kt:
         # dominant kernel and its roofline (algorithmic work per launch / average launch time)
         per = {k: (ms / n if n else 0.0, n, ms) for k, (ms, n) in kt.items()}

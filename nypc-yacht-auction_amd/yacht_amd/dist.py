@@ -27,6 +27,12 @@ def setup(backend: str = None):
     return rank, world, local
 
 
+def device_index(local: int) -> int:
+    """GPU of this rank: one per rank; ranks share the visible GPUs only in gloo rehearsals."""
+    n = torch.cuda.device_count()
+    return local % n if n else 0
+
+
 def allgather_records(buf: torch.Tensor) -> torch.Tensor:
     """Every rank contributes an equal-size uint8 record image -> [world, nbytes] on all ranks."""
     if not dist.is_initialized() or dist.get_world_size() == 1:
@@ -35,8 +41,10 @@ def allgather_records(buf: torch.Tensor) -> torch.Tensor:
     out = torch.empty((world, buf.numel()), dtype=buf.dtype, device=buf.device)
     if dist.get_backend() == "nccl":
         dist.all_gather_into_tensor(out, buf.contiguous())
-    else:
-        dist.all_gather(list(out.unbind(0)), buf.contiguous())
+    else:  # gloo moves host tensors
+        host = torch.empty((world, buf.numel()), dtype=buf.dtype)
+        dist.all_gather(list(host.unbind(0)), buf.contiguous().cpu())
+        out = host.to(buf.device) if buf.is_cuda else host
     return out
 
 

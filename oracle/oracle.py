@@ -48,6 +48,9 @@ def lib():
                                      C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                      C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                      C.c_void_p, C.c_void_p, C.c_int]
+        _lib.or_arena.restype = C.c_int
+        _lib.or_arena.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_int, C.c_double, C.c_int, C.c_int,
+                                  C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
         for name in ("or_step", "or_valid", "or_ended", "or_canonical", "or_featurize", "or_score_table",
                      "or_score_dice", "or_key_hash_batch", "or_hash_prior", "or_init_board", "or_draws"):
             getattr(_lib, name).restype = None
@@ -227,3 +230,19 @@ def selfplay(envs, seed, sims, cpuct=1.5, temp_threshold=15, mode=MODE_HASH, net
                              _p(values), _p(stats), _p(final), threads)
     return dict(canon=canon, mv=mv, ctr=ctr, counts=counts, values=values, stats=stats, final=final,
                 nerr=nerr)
+
+
+def arena(envs, agent_seat, seed, sims, cpuct=1.5, mode=MODE_HASH, net=None, max_moves=64, threads=1):
+    """Arena.playGame (Arena.py:30-93), MCTS agent (temp 0) in seat agent_seat[i] vs RandomYachtPlayer."""
+    e = np.ascontiguousarray(np.asarray(envs, dtype=np.uint32).reshape(-1))
+    n = len(e)
+    seat = np.ascontiguousarray(np.broadcast_to(np.asarray(agent_seat, dtype=np.int32), (n,)))
+    result = np.zeros(n, dtype=np.float64)
+    totals = np.zeros((n, 2), dtype=np.int32)
+    actions = np.zeros((n, max_moves), dtype=np.int32)
+    stats = np.zeros((n, 8), dtype=np.int64)
+    final = np.zeros((n, 8), dtype=np.uint64)
+    nerr = lib().or_arena(n, _p(e), _p(seat), C.c_uint64(seed), sims, C.c_double(cpuct), max_moves, mode,
+                          C.c_void_p(net.h if net is not None else None), _p(result), _p(totals), _p(actions),
+                          _p(stats), _p(final), threads)
+    return dict(result=result, totals=totals, actions=actions, stats=stats, final=final, nerr=nerr)

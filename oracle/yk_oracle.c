@@ -836,6 +836,75 @@ static int run_episode(const ep_cfg_t* cfg, pred_t* pr, uint64_t seed, uint32_t 
     return err;
 }
 
+/* ------------------------------------------------------------------ Arena.playGame (agent vs random) */
+/* Arena.py:30-93 with player1/player2 = {MCTS agent: np.argmax(mcts.getActionProb(x, temp=0))
+ * (Coach.py:124-125), RandomYachtPlayer.play (YachtPlayers.py:174-183)}.  The agent keeps one
+ * MCTS tree for the whole game.  out: result = curPlayer * getGameEnded (Arena.py:93),
+ * totals, moves, actions[max_moves], final state, stream counter. */
+static int run_arena(const ep_cfg_t* cfg, pred_t* pr, uint64_t seed, uint32_t env, int agent_seat, double* result,
+                     int32_t* totals, int32_t* actions, int64_t* stats, uint64_t* final_state) {
+    init_comb();
+    stream_t rs = {seed, env, 0};
+    mcts_t m;
+    memset(&m, 0, sizeof(m));
+    tree_init(&m.tree);
+    m.pred = pr; m.rs = &rs; m.c32 = (float)cfg->cpuct;
+    st_t board;
+    memset(&board, 0, sizeof(board));
+    board.round = 1; board.phase = 0;
+    roll_five(&rs, board.A); board.hasA = 1;
+    roll_five(&rs, board.B); board.hasB = 1;
+    int cur = 1, it = 0, err = 0;
+    uint8_t* valid = (uint8_t*)malloc(ASIZE);
+    while (game_ended(&board, cur, NULL) == 0.0) {
+        if (it >= cfg->max_moves) { err = 1; break; }
+        st_t canon;
+        canonical(&board, cur, &canon);
+        int action = 0;
+        if (cur == agent_seat) {
+            for (int i = 0; i < cfg->sims; i++) search(&m, &canon);
+            if (m.error || pr->error) { err = m.error ? m.error : 2; break; }
+            uint64_t key[8];
+            pack(&canon, key);
+            int id = tree_find(&m.tree, key, or_key_hash(key));
+            const node_t* nd = id >= 0 ? &m.tree.nodes[id] : NULL;
+            int mx = 0, nb = 0;
+            for (int a = 0; a < ASIZE; a++) {
+                int c = (nd && nd->eidx && nd->eidx[a] >= 0) ? nd->e[nd->eidx[a]].N : 0;
+                if (c > mx) { mx = c; nb = 0; }
+                if (c == mx) nb++;
+            }
+            int pick = st_below(&rs, nb);  /* np.random.choice(bestAs)  MCTS.py:46 */
+            for (int a = 0; a < ASIZE; a++) {
+                int c = (nd && nd->eidx && nd->eidx[a] >= 0) ? nd->e[nd->eidx[a]].N : 0;
+                if (c == mx && pick-- == 0) { action = a; break; }
+            }
+        } else {
+            int nv = valid_moves(&canon, 1, valid);
+            if (nv > 0) {
+                int pick = st_below(&rs, nv);  /* np.random.choice(legal) */
+                for (int a = 0; a < ASIZE; a++) if (valid[a] && pick-- == 0) { action = a; break; }
+            }
+        }
+        if (actions) actions[it] = action;
+        it++;
+        st_t nb_;
+        int np_;
+        int stt = step(&board, cur, action, &rs, &nb_, &np_);
+        if (stt) { err = 200 + stt; break; }
+        board = nb_; cur = np_;
+    }
+    *result = (double)cur * game_ended(&board, cur, totals);
+    if (stats) {
+        stats[0] = it; stats[1] = pr->calls; stats[2] = m.tree.n; stats[3] = m.scanned;
+        stats[4] = (int64_t)rs.ctr; stats[5] = err;
+    }
+    if (final_state) pack(&board, final_state);
+    free(valid);
+    tree_free(&m.tree);
+    return err;
+}
+
 /* ------------------------------------------------------------------ exported batch API (ctypes) */
 void or_score_table(const uint64_t* w, const int32_t* players, int32_t* out, int n) {
     init_comb();
@@ -967,6 +1036,26 @@ int or_selfplay(int n, const uint32_t* envs, uint64_t seed, int sims, double cpu
         o.stats = stats ? stats + (size_t)8 * i : NULL;
         o.final_state = final_state ? final_state + (size_t)8 * i : NULL;
         if (run_episode(&cfg, &pr, seed, envs[i], &o)) nerr++;
+    }
+    return nerr;
+}
+
+int or_arena(int n, const uint32_t* envs, const int32_t* agent_seat, uint64_t seed, int sims, double cpuct,
+             int max_moves, int mode, void* net, double* result, int32_t* totals, int32_t* actions, int64_t* stats,
+             uint64_t* final_state, int threads) {
+    init_comb();
+    ep_cfg_t cfg = {sims, 0, max_moves, cpuct, mode};
+    int nerr = 0;
+#pragma omp parallel for schedule(dynamic, 1) num_threads(threads > 0 ? threads : 1) reduction(+ : nerr)
+    for (int i = 0; i < n; i++) {
+        pred_t pr;
+        memset(&pr, 0, sizeof(pr));
+        pr.mode = mode;
+        pr.net = (const net_t*)net;
+        if (run_arena(&cfg, &pr, seed, envs[i], agent_seat[i], result + i, totals + 2 * i,
+                      actions ? actions + (size_t)max_moves * i : NULL, stats ? stats + 8 * i : NULL,
+                      final_state ? final_state + 8 * i : NULL))
+            nerr++;
     }
     return nerr;
 }

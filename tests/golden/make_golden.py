@@ -300,6 +300,66 @@ def run_episode(seed, env, sims, cpuct=1.5, temp_threshold=15):
                 expansions=nnet.calls, nodes=len(mcts.Es), seconds=dt)
 
 
+def run_arena_game(seed, env, sims, agent_seat, cpuct=1.5):
+    """One reference Arena.playGame (Arena.py:30-93): MCTS agent (np.argmax(getActionProb(x, temp=0)),
+    Coach.py:124-125) in seat agent_seat vs RandomYachtPlayer (YachtPlayers.py:174-183), fresh tree."""
+    from utils import dotdict
+    from Arena import Arena
+    from MCTS import MCTS
+    from yacht.YachtPlayers import RandomYachtPlayer
+    game = YachtGame()
+    args = dotdict(dict(numMCTSSims=sims, cpuct=cpuct))
+    set_stream(seed, env)
+    nnet = HashNet(game)
+    mcts = MCTS(game, nnet, args)
+    agent = lambda x: int(np.argmax(mcts.getActionProb(x, temp=0)))  # noqa: E731
+    rnd = RandomYachtPlayer(game).play
+    actions = []
+    in_search = [False]
+    orig_gap = mcts.getActionProb
+    orig_next = game.getNextState
+
+    def gap(canonical, temp=1):
+        in_search[0] = True
+        try:
+            return orig_gap(canonical, temp=temp)
+        finally:
+            in_search[0] = False
+
+    def nxt(board, player, action):
+        if not in_search[0]:
+            actions.append(int(action))
+        return orig_next(board, player, action)
+
+    mcts.getActionProb = gap
+    game.getNextState = nxt
+    p1, p2 = (agent, rnd) if agent_seat == 1 else (rnd, agent)
+    arena = Arena(p1, p2, game)
+    import logging
+    logging.getLogger("Arena").setLevel(logging.WARNING)
+    result = arena.playGame()
+    return dict(env=env, seat=agent_seat, result=float(result), actions=actions, ctr_end=_STREAM[0].ctr,
+                expansions=nnet.calls)
+
+
+def make_arena(seed=777, n=12, sims=10):
+    rows = []
+    for i in range(n):
+        seat = 1 if i < n // 2 else -1
+        g = run_arena_game(seed, 500 + i, sims, seat)
+        rows.append(g)
+    M = max(len(g["actions"]) for g in rows)
+    acts = np.full((n, M), -1, dtype=np.int32)
+    for i, g in enumerate(rows):
+        acts[i, :len(g["actions"])] = g["actions"]
+    return dict(seed=np.uint64(seed), sims=np.int64(sims), env=np.array([g["env"] for g in rows], dtype=np.int64),
+                seat=np.array([g["seat"] for g in rows], dtype=np.int32),
+                result=np.array([g["result"] for g in rows], dtype=np.float64), actions=acts,
+                n_moves=np.array([len(g["actions"]) for g in rows], dtype=np.int32),
+                ctr_end=np.array([g["ctr_end"] for g in rows], dtype=np.int64),
+                expansions=np.array([g["expansions"] for g in rows], dtype=np.int64))
+
+
 def pack_episodes(eps):
     """Flatten episode dicts into fixed arrays (npz-friendly)."""
     out = {}
@@ -332,6 +392,10 @@ def pack_episodes(eps):
 
 def main():
     t0 = time.time()
+    if len(sys.argv) > 1 and sys.argv[1] == "arena":
+        np.savez_compressed(os.path.join(HERE, "arena_hash.npz"), **make_arena())
+        print(f"arena fixtures in {time.time() - t0:.1f}s")
+        return
     dice, table = make_score_table()
     np.savez_compressed(os.path.join(HERE, "score_table.npz"), dice=dice, score=table)
     print("score table", table.shape, f"{time.time() - t0:.1f}s")
@@ -357,6 +421,7 @@ def main():
         print(f"episode env={env} sims={sims}: {len(ep['moves'])} moves, {ep['expansions']} expansions, "
               f"{ep['nodes']} nodes, {ep['seconds']:.1f}s")
     np.savez_compressed(os.path.join(HERE, "episodes_hash.npz"), **pack_episodes(eps))
+    np.savez_compressed(os.path.join(HERE, "arena_hash.npz"), **make_arena())
     print(f"done in {time.time() - t0:.1f}s")
 
 

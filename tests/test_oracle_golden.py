@@ -135,3 +135,16 @@ def test_selfplay_hash_prior_matches_reference(golden):
             dense[a] = n
             assert np.array_equal(r["counts"][0, j], dense), (i, j)
         assert np.array_equal(r["values"][0, :M], g["values"][i, :M])
+
+
+def test_arena_hash_prior_matches_reference(golden):
+    """Arena.playGame (Arena.py:30-93): MCTS agent at temp 0 vs RandomYachtPlayer, both seats."""
+    g = golden("arena_hash.npz")
+    r = O.arena(g["env"], g["seat"], int(g["seed"]), int(g["sims"]))
+    assert r["nerr"] == 0
+    assert np.array_equal(r["result"], g["result"])
+    assert np.array_equal(r["stats"][:, 0], g["n_moves"])
+    assert np.array_equal(r["stats"][:, 1], g["expansions"])
+    assert np.array_equal(r["stats"][:, 4], g["ctr_end"])
+    for i, n in enumerate(g["n_moves"]):
+        assert np.array_equal(r["actions"][i, :n], g["actions"][i, :n])
