@@ -59,6 +59,33 @@ def cpu_baseline(state_dict, sims, seconds_target=15.0, threads=None):
                       f"same net), {exps} expansions in {dt:.1f}s"}
 
 
+def arena_leg(net, games=1000, sims=25, seed=0, reps=3):
+    """Config 4: Arena.playGames(1000) of MCTS(temp 0, 25 sims) vs the uniform-random player,
+    one lock-step device batch (agent seat 1 for the first half, -1 for the second)."""
+    import numpy as np
+    import torch
+
+    from yacht_amd.engine import SelfPlayEngine
+    seats = np.array([1] * (games // 2) + [-1] * (games - games // 2), dtype=np.int32)
+    eng = SelfPlayEngine(games, sims, 1.5, 0, net=net, max_moves=64)
+    eng.arena(seats, seed + 1000, 0)  # warm-up
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(reps):
+        eng.arena(seats, seed + 1001 + i, 0)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / reps
+    r = eng.arena_results()
+    st = eng.stats()
+    eng.close()
+    agent = r["result"] * seats
+    return {"config": f"Arena.playGames({games}), MCTS temp 0 x {sims} sims vs uniform-random legal player, "
+                      f"random-init YachtNNet", "games_per_s": games / dt, "ms_per_batch": 1000.0 * dt,
+            "agent_won": int((agent == 1).sum()), "random_won": int((agent == -1).sum()),
+            "draws": int(((agent != 1) & (agent != -1)).sum()), "moves": int(r["n_moves"].sum()),
+            "expansions_per_s": st["expansions"] / dt}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -69,6 +96,7 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel event timing")
+    ap.add_argument("--no-arena", action="store_true", help="skip the config-4 Arena leg")
     ap.add_argument("--dist-backend", default=None, help="nccl (RCCL, default on GPUs) or gloo (rehearsal)")
     args = ap.parse_args()
 
@@ -189,6 +217,8 @@ def main():
             out["roofline"] = {"kernel": "k_" + dom, "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS,
                                "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "traffic": None,
                                "work_per_launch": f"{b:.0f} algorithmic bytes"}
+    if world == 1 and not args.no_arena:
+        out["arena"] = arena_leg(net, seed=args.seed)
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(sd, args.sims)
     print(json.dumps(out), flush=True)

@@ -170,6 +170,21 @@ int yk_engine_predictions(yk_engine_t* eng, float* pi, float* v, int32_t* count)
 int64_t yk_engine_record_bytes(yk_engine_t* eng);
 int yk_engine_pack_records(yk_engine_t* eng, void* dst, int64_t capacity, void* stream);
 
+/* ---------------------------------------------------------------- Arena
+ * Batched Arena.playGame (Arena.py:30-93) of the MCTS agent against RandomYachtPlayer
+ * (yacht/YachtPlayers.py:174-183), n_envs games in lock-step, the evaluation leg of
+ * Coach.learn (Coach.py:118-131).  Game i uses stream env_base+i; agent_seat (HOST, [n]) is
+ * 1 (agent moves first) or -1.  The agent is np.argmax(MCTS.getActionProb(board, temp=0))
+ * (Coach.py:124-125) with one tree per game for the whole game; the random player draws
+ * uniformly among the legal actions of its canonical board.  Returns like yk_selfplay. */
+int yk_arena(yk_engine_t* eng, uint64_t seed, uint32_t env_base, const int32_t* agent_seat, void* stream);
+/* HOST outputs of the last yk_arena (any may be NULL): result[n] = curPlayer * getGameEnded
+ * (Arena.py:93, from player 1's view: +1 / -1 / +-1e-4 draw), totals[n][2] (player 1, player 2,
+ * with bonus), n_moves[n], actions[n][max_moves] (-1 past the end), final_states[n][8],
+ * rng_ctr[n] (stream counter at the end).  yk_engine_records also works after yk_arena. */
+int yk_arena_results(yk_engine_t* eng, double* result, int32_t* totals, int32_t* n_moves, int32_t* actions,
+                     uint64_t* final_states, uint64_t* rng_ctr);
+
 /* ---------------------------------------------------------------- MCTS plugin
  * MCTS(game, nnet, args).getActionProb (MCTS.py:28-54) for n_envs independent searches
  * sharing nothing: runs `sims` searches from roots[i] (device, canonical boards) with

@@ -59,6 +59,7 @@ struct EngDev {
     float c32;
     int prior;  // 0 net, 1 hash
     int rec_pred, max_exp;
+    int arena;             // 1 while yk_arena runs: agent (MCTS, temp 0) vs uniform-random mover
     uint64_t seed;
     NodeRec* nodes[2];
     uint32_t* hidx[2];
@@ -78,6 +79,8 @@ struct EngDev {
     uint8_t* done;
     int32_t* nmoves;
     yk_state_t* root;
+    int32_t* seat;         // [E] arena: the agent's seat (1 / -1)
+    uint8_t* idle;         // [E] arena: the random mover is to move (no search this move)
     // per-sim
     yk_state_t* leaf_state;
     uint64_t* leaf_hash;
@@ -102,6 +105,7 @@ struct EngDev {
     int32_t* rec_voff;     // [E][M+1]
     double* final_r;       // [E]
     int32_t* final_cur;    // [E]
+    int32_t* final_tot;    // [E][2] score totals with bonus (getGameEnded, YachtGame.py:408-428)
     float* rec_pi;         // [E][max_exp][3226]  (record_predictions)
     float* rec_v;          // [E][max_exp]
     // stats
@@ -292,10 +296,15 @@ __global__ __launch_bounds__(256) void k_move_begin(EngDev d, int move, int exte
         if (d.done[e]) return;
         const YkS b = ld_state(d.board + e);
         const YkS r = canonical(b, d.cur[e]);
+        const bool idle = d.arena && d.cur[e] != d.seat[e];
         if (lane == 0) {
             st_state(d.root + e, r);
             d.rec_ctr[((long)e * d.M + move) * 2] = d.ctr[e];
+            d.idle[e] = idle ? 1 : 0;
         }
+        if (idle) return;  // Arena: the random player does not search (YachtPlayers.py:174-183)
+    } else if (lane == 0) {
+        d.idle[e] = 0;
     }
     const YkS r = ld_state(d.root + e);
     const int rr = s_round(r);
@@ -367,7 +376,7 @@ __global__ __launch_bounds__(256) void k_select(EngDev d, const uint32_t* env_id
     const int lane = threadIdx.x & 63;
     const int e = blockIdx.x * GAMES_PER_BLOCK + (threadIdx.x >> 6);
     if (e >= d.E) return;
-    if (d.done[e]) {
+    if (d.done[e] || d.idle[e]) {
         if (lane == 0) {
             d.leaf_flag[e] = 0;
             d.path_len[e] = 0;
@@ -726,10 +735,12 @@ __global__ __launch_bounds__(256) void k_move_end(EngDev d, int move) {
     uint32_t* vis = vis_all[w];
     const int g = d.gen[e];
     const YkS r = ld_state(d.root + e);
-    const int nid = lookup(d, g, e, r, key_hash(r));
+    const bool idle = d.idle[e] != 0;
+    const int nid = idle ? -1 : lookup(d, g, e, r, key_hash(r));
     int nvis = 0;
     uint32_t root_ns = 0xFFFFFFFFu;
-    if (nid >= 0) {
+    if (idle) {
+    } else if (nid >= 0) {
         const NodeRec& nd = d.nodes[g][(long)e * d.NCAP + nid];
         root_ns = nd.Ns;
         const VInfo vi = unpack_vinfo(nd.vinfo, nd.nvalid);
@@ -759,10 +770,15 @@ __global__ __launch_bounds__(256) void k_move_end(EngDev d, int move) {
     if (!room) atomicOr(d.err, ERR_VISITS);
     d.rec_voff[(long)e * (d.M + 1) + move + 1] = room ? voff + nvis : voff;
     const int stepi = move + 1;
-    const int temp = stepi < d.temp_threshold ? 1 : 0;  // Coach.py:58
+    const int temp = d.arena ? 0 : (stepi < d.temp_threshold ? 1 : 0);  // Coach.py:58
     Stream rs{d.seed, d.env_id[e], d.ctr[e]};
     int action = 0;
-    if (temp == 0) {
+    if (idle) {
+        // RandomYachtPlayer.play: np.random.choice over the ascending legal actions of the
+        // canonical board (YachtPlayers.py:174-183); no legal action -> 0 without a draw
+        const VInfo vi = valid_info(r, 1);
+        if (vi.V > 0) action = compact_to_action(vi, rs.below(vi.V));
+    } else if (temp == 0) {
         // bestAs = argwhere(counts == max(counts)); np.random.choice(bestAs)  (MCTS.py:44-49)
         uint32_t mx = 0;
         for (int i = 0; i < nvis; i++) mx = max(mx, vis[i] & 0xFFFF);
@@ -778,7 +794,9 @@ __global__ __launch_bounds__(256) void k_move_end(EngDev d, int move) {
                     break;
                 }
         }
-        (void)rs.uniform53();  // np.random.choice(len(pi), p=one-hot) still draws (Coach.py:65)
+        // np.random.choice(len(pi), p=one-hot) still draws in Coach (Coach.py:65); the Arena
+        // agent is np.argmax(pi) (Coach.py:124-125), which does not
+        if (!d.arena) (void)rs.uniform53();
     } else {
         // probs = counts / sum; np.random.choice(len(pi), p=probs): cumsum, /= cdf[-1],
         // searchsorted(u, 'right')
@@ -833,6 +851,8 @@ __global__ __launch_bounds__(256) void k_move_end(EngDev d, int move) {
         d.done[e] = 1;
         d.final_r[e] = rgame;
         d.final_cur[e] = np;
+        d.final_tot[2 * e] = total_with_bonus(b, 0);
+        d.final_tot[2 * e + 1] = total_with_bonus(b, 1);
     } else if (stepi >= d.M) {
         atomicOr(d.err, ERR_MOVES);
         d.done[e] = 1;
@@ -900,6 +920,7 @@ struct yk_engine {
     int32_t* host_done = nullptr;
     uint32_t* mcts_env = nullptr;
     bool have_records = false;
+    bool have_arena = false;
     // profiling (yk_engine_profile): per-kernel-class HIP events, accumulated per move
     bool prof = false;
     std::vector<hipEvent_t> ev;
@@ -1063,6 +1084,9 @@ int yk_engine_create(yk_engine_t** out, const yk_engine_config_t* cfg, yk_net_t*
     A(d.rec_voff, E * (d.M + 1));
     A(d.final_r, E);
     A(d.final_cur, E);
+    A(d.final_tot, 2 * E);
+    A(d.seat, E);
+    A(d.idle, E);
     A(d.gstats, E * 8);
     A(d.err, 1);
     A(eng->done_count, 1);
@@ -1088,6 +1112,7 @@ int yk_engine_create(yk_engine_t** out, const yk_engine_config_t* cfg, yk_net_t*
     YK_LAUNCHED();
     YK_HIP(hipMemset(d.err, 0, sizeof(uint32_t)));
     YK_HIP(hipMemset(d.done, 0, E));
+    YK_HIP(hipMemset(d.idle, 0, E));
     YK_HIP(hipMemset(d.leaf_state, 0, sizeof(yk_state_t) * E));
     std::vector<uint32_t> ids(E);
     for (size_t i = 0; i < E; i++) ids[i] = (uint32_t)i;
@@ -1106,9 +1131,12 @@ int yk_engine_destroy(yk_engine_t* eng) {
     return YK_OK;
 }
 
-int yk_selfplay(yk_engine_t* eng, uint64_t seed, uint32_t env_base, void* stream) {
-    if (!eng) return YK_ERR_ARG;
-    hipStream_t s = as_stream(stream);
+}  // extern "C"
+
+namespace {
+// One lock-step batch of complete games: self-play (Coach.executeEpisode) or, with
+// d.arena set, Arena.playGame against the uniform-random player.
+int play_batch(yk_engine* eng, uint64_t seed, uint32_t env_base, hipStream_t s) {
     EngDev& d = eng->d;
     d.seed = seed;
     const dim3 gb((d.E + GAMES_PER_BLOCK - 1) / GAMES_PER_BLOCK), bb(256);
@@ -1138,6 +1166,59 @@ int yk_selfplay(yk_engine_t* eng, uint64_t seed, uint32_t env_base, void* stream
     YK_LAUNCHED();
     eng->have_records = true;
     return check_errors(eng, s);
+}
+}  // namespace
+
+extern "C" {
+
+int yk_selfplay(yk_engine_t* eng, uint64_t seed, uint32_t env_base, void* stream) {
+    if (!eng) return YK_ERR_ARG;
+    eng->d.arena = 0;
+    eng->have_arena = false;
+    return play_batch(eng, seed, env_base, as_stream(stream));
+}
+
+int yk_arena(yk_engine_t* eng, uint64_t seed, uint32_t env_base, const int32_t* agent_seat, void* stream) {
+    if (!eng || !agent_seat) return YK_ERR_ARG;
+    EngDev& d = eng->d;
+    for (int e = 0; e < d.E; e++)
+        if (agent_seat[e] != 1 && agent_seat[e] != -1) return YK_ERR_ARG;
+    hipStream_t s = as_stream(stream);
+    YK_HIP(hipMemcpyAsync(d.seat, agent_seat, sizeof(int32_t) * (size_t)d.E, hipMemcpyHostToDevice, s));
+    d.arena = 1;
+    eng->have_arena = false;
+    const int rc = play_batch(eng, seed, env_base, s);
+    d.arena = 0;
+    eng->have_arena = rc == YK_OK || rc == YK_ERR_STATE;
+    return rc;
+}
+
+int yk_arena_results(yk_engine_t* eng, double* result, int32_t* totals, int32_t* n_moves, int32_t* actions,
+                     uint64_t* final_states, uint64_t* rng_ctr) {
+    if (!eng) return YK_ERR_ARG;
+    if (!eng->have_arena) return YK_ERR_STATE;
+    EngDev& d = eng->d;
+    const size_t E = d.E, M = d.M;
+    YK_HIP(hipDeviceSynchronize());
+    std::vector<int32_t> nm(E), fc(E), info;
+    std::vector<double> fr(E);
+    YK_HIP(hipMemcpy(nm.data(), d.nmoves, sizeof(int32_t) * E, hipMemcpyDeviceToHost));
+    if (result) {
+        YK_HIP(hipMemcpy(fr.data(), d.final_r, sizeof(double) * E, hipMemcpyDeviceToHost));
+        YK_HIP(hipMemcpy(fc.data(), d.final_cur, sizeof(int32_t) * E, hipMemcpyDeviceToHost));
+        for (size_t e = 0; e < E; e++) result[e] = (double)fc[e] * fr[e];  // Arena.py:93
+    }
+    if (totals) YK_HIP(hipMemcpy(totals, d.final_tot, sizeof(int32_t) * 2 * E, hipMemcpyDeviceToHost));
+    if (n_moves) std::copy(nm.begin(), nm.end(), n_moves);
+    if (actions) {
+        info.resize(E * M * 8);
+        YK_HIP(hipMemcpy(info.data(), d.rec_info, sizeof(int32_t) * info.size(), hipMemcpyDeviceToHost));
+        for (size_t e = 0; e < E; e++)
+            for (size_t m = 0; m < M; m++) actions[e * M + m] = (int)m < nm[e] ? info[(e * M + m) * 8 + 2] : -1;
+    }
+    if (final_states) YK_HIP(hipMemcpy(final_states, d.board, sizeof(yk_state_t) * E, hipMemcpyDeviceToHost));
+    if (rng_ctr) YK_HIP(hipMemcpy(rng_ctr, d.ctr, sizeof(uint64_t) * E, hipMemcpyDeviceToHost));
+    return YK_OK;
 }
 
 int yk_engine_profile(yk_engine_t* eng, int enable) {

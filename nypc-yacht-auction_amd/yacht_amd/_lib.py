@@ -61,6 +61,8 @@ SIGNATURES = {
     "yk_engine_create": [C.POINTER(P), C.POINTER(YkEngineConfig), P],
     "yk_engine_destroy": [P],
     "yk_selfplay": [P, U64, U32, P],
+    "yk_arena": [P, U64, U32, P, P],
+    "yk_arena_results": [P, P, P, P, P, P, P],
     "yk_engine_stats": [P, P],
     "yk_engine_profile": [P, I],
     "yk_engine_kernel_times": [P, P, P],

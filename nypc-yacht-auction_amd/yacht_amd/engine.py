@@ -50,6 +50,31 @@ class SelfPlayEngine:
             bits = [n for b, n in self.ERROR_BITS.items() if st["errors"] & b]
             raise YkError(f"yk_selfplay [{', '.join(bits)}; stats {st}]", e.code) from None
 
+    def arena(self, agent_seat, seed: int, env_base: int = 0, stream=None):
+        """Batched Arena.playGame of the MCTS agent (temp 0) vs the uniform-random player
+        (yk_arena): game i uses stream (seed, env_base + i), agent in seat agent_seat[i]."""
+        from ._lib import YkError
+        seat = np.ascontiguousarray(np.broadcast_to(np.asarray(agent_seat, dtype=np.int32), (self.n_envs,)))
+        try:
+            call("yk_arena", self.handle, seed & (2**64 - 1), env_base & (2**32 - 1), seat.ctypes.data,
+                 stream_ptr(stream))
+        except YkError as e:
+            st = self.stats()
+            bits = [n for b, n in self.ERROR_BITS.items() if st["errors"] & b]
+            raise YkError(f"yk_arena [{', '.join(bits)}; stats {st}]", e.code) from None
+
+    def arena_results(self) -> dict:
+        E, M = self.n_envs, self.max_moves
+        result = np.zeros(E, dtype=np.float64)
+        totals = np.zeros((E, 2), dtype=np.int32)
+        nm = np.zeros(E, dtype=np.int32)
+        actions = np.zeros((E, M), dtype=np.int32)
+        final = np.zeros((E, 8), dtype=np.uint64)
+        ctr = np.zeros(E, dtype=np.uint64)
+        call("yk_arena_results", self.handle, result.ctypes.data, totals.ctypes.data, nm.ctypes.data,
+             actions.ctypes.data, final.ctypes.data, ctr.ctypes.data)
+        return dict(result=result, totals=totals, n_moves=nm, actions=actions, final=final, ctr=ctr)
+
     KERNEL_CLASSES = ("select", "forward", "leaf_scan", "expand_backup", "move_begin", "move_end")
 
     def profile(self, enable: bool = True):

@@ -50,7 +50,8 @@ def lib():
                                      C.c_void_p, C.c_void_p, C.c_int]
         _lib.or_arena.restype = C.c_int
         _lib.or_arena.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_int, C.c_double, C.c_int, C.c_int,
-                                  C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+                                  C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                  C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
         for name in ("or_step", "or_valid", "or_ended", "or_canonical", "or_featurize", "or_score_table",
                      "or_score_dice", "or_key_hash_batch", "or_hash_prior", "or_init_board", "or_draws"):
             getattr(_lib, name).restype = None
@@ -197,6 +198,15 @@ class Net:
 MODE_HASH, MODE_MLP, MODE_REPLAY = 0, 1, 2
 
 
+def _replay_ptrs(replay, keep):
+    pis = [np.ascontiguousarray(p, dtype=np.float32) for p, _ in replay]
+    vs = [np.ascontiguousarray(v, dtype=np.float32) for _, v in replay]
+    rn_arr = np.array([len(v) for v in vs], dtype=np.int64)
+    keep += pis + vs + [rn_arr]
+    n = len(pis)
+    return (C.c_void_p * n)(*[p.ctypes.data for p in pis]), (C.c_void_p * n)(*[v.ctypes.data for v in vs]), _p(rn_arr)
+
+
 def selfplay(envs, seed, sims, cpuct=1.5, temp_threshold=15, mode=MODE_HASH, net=None, replay=None,
              max_moves=64, want_counts=True, threads=1):
     """Coach.executeEpisode for each env id (fresh MCTS per game, Coach.py:93).
@@ -216,14 +226,7 @@ def selfplay(envs, seed, sims, cpuct=1.5, temp_threshold=15, mode=MODE_HASH, net
     rpi = rv = rn = None
     keep = []
     if mode == MODE_REPLAY:
-        pis = [np.ascontiguousarray(p, dtype=np.float32) for p, _ in replay]
-        vs = [np.ascontiguousarray(v, dtype=np.float32) for _, v in replay]
-        keep += pis + vs
-        rpi = (C.c_void_p * n)(*[p.ctypes.data for p in pis])
-        rv = (C.c_void_p * n)(*[v.ctypes.data for v in vs])
-        rn_arr = np.array([len(v) for v in vs], dtype=np.int64)
-        keep.append(rn_arr)
-        rn = _p(rn_arr)
+        rpi, rv, rn = _replay_ptrs(replay, keep)
     nerr = lib().or_selfplay(n, _p(e), C.c_uint64(seed), sims, C.c_double(cpuct), temp_threshold, M, mode,
                              C.c_void_p(net.h if net is not None else None), rpi, rv, rn,
                              _p(canon), _p(mv), _p(ctr), _p(counts) if counts is not None else None,
@@ -232,8 +235,10 @@ def selfplay(envs, seed, sims, cpuct=1.5, temp_threshold=15, mode=MODE_HASH, net
                 nerr=nerr)
 
 
-def arena(envs, agent_seat, seed, sims, cpuct=1.5, mode=MODE_HASH, net=None, max_moves=64, threads=1):
-    """Arena.playGame (Arena.py:30-93), MCTS agent (temp 0) in seat agent_seat[i] vs RandomYachtPlayer."""
+def arena(envs, agent_seat, seed, sims, cpuct=1.5, mode=MODE_HASH, net=None, replay=None, max_moves=64,
+          threads=1):
+    """Arena.playGame (Arena.py:30-93), MCTS agent (temp 0) in seat agent_seat[i] vs RandomYachtPlayer.
+    replay as in selfplay (MODE_REPLAY)."""
     e = np.ascontiguousarray(np.asarray(envs, dtype=np.uint32).reshape(-1))
     n = len(e)
     seat = np.ascontiguousarray(np.broadcast_to(np.asarray(agent_seat, dtype=np.int32), (n,)))
@@ -242,7 +247,11 @@ def arena(envs, agent_seat, seed, sims, cpuct=1.5, mode=MODE_HASH, net=None, max
     actions = np.zeros((n, max_moves), dtype=np.int32)
     stats = np.zeros((n, 8), dtype=np.int64)
     final = np.zeros((n, 8), dtype=np.uint64)
+    keep = []
+    rpi = rv = rn = None
+    if mode == MODE_REPLAY:
+        rpi, rv, rn = _replay_ptrs(replay, keep)
     nerr = lib().or_arena(n, _p(e), _p(seat), C.c_uint64(seed), sims, C.c_double(cpuct), max_moves, mode,
-                          C.c_void_p(net.h if net is not None else None), _p(result), _p(totals), _p(actions),
+                          C.c_void_p(net.h if net is not None else None), rpi, rv, rn, _p(result), _p(totals), _p(actions),
                           _p(stats), _p(final), threads)
     return dict(result=result, totals=totals, actions=actions, stats=stats, final=final, nerr=nerr)

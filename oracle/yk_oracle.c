@@ -1041,7 +1041,8 @@ int or_selfplay(int n, const uint32_t* envs, uint64_t seed, int sims, double cpu
 }
 
 int or_arena(int n, const uint32_t* envs, const int32_t* agent_seat, uint64_t seed, int sims, double cpuct,
-             int max_moves, int mode, void* net, double* result, int32_t* totals, int32_t* actions, int64_t* stats,
+             int max_moves, int mode, void* net, const float* const* rpi, const float* const* rv,
+             const int64_t* rn, double* result, int32_t* totals, int32_t* actions, int64_t* stats,
              uint64_t* final_state, int threads) {
     init_comb();
     ep_cfg_t cfg = {sims, 0, max_moves, cpuct, mode};
@@ -1052,6 +1053,7 @@ int or_arena(int n, const uint32_t* envs, const int32_t* agent_seat, uint64_t se
         memset(&pr, 0, sizeof(pr));
         pr.mode = mode;
         pr.net = (const net_t*)net;
+        if (mode == 2) { pr.rpi = rpi[i]; pr.rv = rv[i]; pr.rn = rn[i]; }
         if (run_arena(&cfg, &pr, seed, envs[i], agent_seat[i], result + i, totals + 2 * i,
                       actions ? actions + (size_t)max_moves * i : NULL, stats ? stats + 8 * i : NULL,
                       final_state ? final_state + 8 * i : NULL))
