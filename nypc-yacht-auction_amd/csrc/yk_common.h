@@ -33,6 +33,7 @@ struct Tables {
     uint16_t vcnt[16];          // number of combos with max < n  (= C(n,5))
     uint16_t voff[16];          // offset into vids
     uint8_t vids[512];          // those combo ids, ascending, for n = 5..10
+    uint8_t vrank[6][NCOMB];    // rank of combo i among those with max < n (n = 5..10; valid ones only)
     float die_scale[16];        // _scale_die(d) = (d - 3.5) / 3.5  (NNet.py:50-51), f32
     float round_feat[16];       // round / 13.0 as f32 (NNet.py:69)
 };
@@ -57,6 +58,8 @@ constexpr Tables make_tables() {
             for (int i = 0; i < NCOMB; i++)
                 if (t.comb_max[i] < n) t.vids[off + cnt++] = (uint8_t)i;
         t.vcnt[n] = (uint16_t)cnt;
+        if (n >= 5 && n <= 10)
+            for (int r = 0; r < cnt; r++) t.vrank[n - 5][t.vids[off + r]] = (uint8_t)r;
         off += cnt;
     }
     for (int d = 0; d < 16; d++) t.die_scale[d] = (float)(((double)d - 3.5) / 3.5);

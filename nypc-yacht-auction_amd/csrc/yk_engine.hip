@@ -86,9 +86,6 @@ struct EngDev {
     uint64_t* leaf_hash;
     uint8_t* leaf_flag;
     uint64_t* path;        // [E][MAXD]: (p_off + j) << 32 | node id
-    int32_t* leaf_row;     // [E]: compact predict row of this game's leaf (-1: none)
-    int32_t* rows;         // [E]: leaf rows -> game
-    int32_t* nrows;        // [1]
     uint8_t* path_len;
     double* res_v;
     uint32_t* res_t;
@@ -145,6 +142,63 @@ constexpr PwPlan make_plan() {
 }
 static __constant__ PwPlan c_pw = make_plan();
 static_assert(make_plan().nleaf <= 64 && make_plan().nop <= 64, "pairwise plan too large");
+// The expand kernel evaluates the plan as a register butterfly: that is exact iff the tree is
+// perfect over 32 in-order leaves, every leaf 8-aligned with 8 <= len <= 128.
+constexpr bool plan_is_butterfly() {
+    const PwPlan p = make_plan();
+    if (p.nleaf != 32 || p.nop != 31) return false;
+    int first[128] = {}, cnt[128] = {};
+    for (int i = 0; i < p.nleaf; i++) {
+        if (p.start[i] % 8 != 0 || p.len[i] < 8 || p.len[i] > 128) return false;
+        if (i > 0 && p.start[i] != p.start[i - 1] + p.len[i - 1]) return false;
+        first[i] = i;
+        cnt[i] = 1;
+    }
+    for (int o = 0; o < p.nop; o++) {
+        const int a = p.a[o], b = p.b[o];
+        if (cnt[a] != cnt[b] || first[a] + cnt[a] != first[b] || first[a] % (2 * cnt[a]) != 0) return false;
+        first[64 + o] = first[a];
+        cnt[64 + o] = 2 * cnt[a];
+    }
+    return p.root == 64 + p.nop - 1 && cnt[p.root] == 32;
+}
+static_assert(plan_is_butterfly(), "numpy's pairwise tree for 3226 is no longer a perfect 32-leaf tree");
+constexpr int pw_gmax() {
+    const PwPlan p = make_plan();
+    int g = 0;
+    for (int i = 0; i < p.nleaf; i++) g = p.len[i] / 8 > g ? p.len[i] / 8 : g;
+    return g;
+}
+constexpr int pw_tmax() {
+    const PwPlan p = make_plan();
+    int t = 0;
+    for (int i = 0; i < p.nleaf; i++) t = p.len[i] % 8 > t ? p.len[i] % 8 : t;
+    return t;
+}
+constexpr int PW_GMAX = pw_gmax();  // 8-element groups in the longest leaf
+constexpr int PW_TMAX = pw_tmax() > 0 ? pw_tmax() : 1;  // longest n % 8 tail
+
+// getValidMoves of player 1 as wave-uniform scalars (the same test as action_valid)
+struct ValidQ {
+    int mode;       // 1: bid phase (a < 202), 0: score phase, -1: nothing valid
+    int n;          // carry length
+    uint32_t used;  // used categories
+    __device__ __forceinline__ bool operator()(int a) const {
+        if (mode == 1) return a < NBID;
+        if (mode != 0 || a < NBID) return false;
+        const int base = a - NBID, cat = base / NCOMB, ci = base - cat * NCOMB;
+        return !((used >> cat) & 1u) && c_tab.comb_max[ci] < n;
+    }
+};
+__device__ __forceinline__ ValidQ valid_q(const YkS& s) {
+    ValidQ q;
+    const int round = s_round(s), phase = s_phase(s);
+    const uint64_t wa = s_pw(s, 0, 0);
+    q.n = __builtin_amdgcn_readfirstlane(wa_n(wa));
+    q.used = __builtin_amdgcn_readfirstlane((uint32_t)wa_used(wa));
+    q.mode = __builtin_amdgcn_readfirstlane((phase == 0 && round != 13) ? 1 : (phase == 1 && q.n >= 5) ? 0 : -1);
+    return q;
+}
 
 __device__ __forceinline__ YkS ld_state(const yk_state_t* p) {
     const uint4* q = reinterpret_cast<const uint4*>(p);
@@ -497,44 +551,8 @@ __global__ __launch_bounds__(256) void k_select(EngDev d, const uint32_t* env_id
     }
 }
 
-// Compact the games that reached a leaf into predict rows (order-preserving block scan).
-__global__ __launch_bounds__(1024) void k_leaf_scan(EngDev d) {
-    __shared__ int part[1024];
-    const int t = threadIdx.x;
-    const int per = (d.E + 1023) / 1024;
-    const int b0 = t * per;
-    int c = 0;
-    for (int i = 0; i < per; i++) {
-        const int e = b0 + i;
-        if (e < d.E && !d.done[e] && d.leaf_flag[e]) c++;
-    }
-    part[t] = c;
-    __syncthreads();
-    for (int o = 1; o < 1024; o <<= 1) {  // Hillis-Steele inclusive scan
-        const int v = t >= o ? part[t - o] : 0;
-        __syncthreads();
-        part[t] += v;
-        __syncthreads();
-    }
-    int r = part[t] - c;
-    for (int i = 0; i < per; i++) {
-        const int e = b0 + i;
-        if (e >= d.E) break;
-        if (!d.done[e] && d.leaf_flag[e]) {
-            d.leaf_row[e] = r;
-            d.rows[r] = e;
-            r++;
-        } else {
-            d.leaf_row[e] = -1;
-        }
-    }
-    if (t == 1023) *d.nrows = part[1023];
-}
-
 // Leaf expansion (MCTS.py:84-115) and backup (MCTS.py:154-164).  One wave per game.
-__global__ __launch_bounds__(256) void k_expand_backup(EngDev d) {
-    __shared__ float buf_all[GAMES_PER_BLOCK][ASIZE + 2];
-    __shared__ float vals_all[GAMES_PER_BLOCK][128];
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_expand_backup(EngDev d) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int e = blockIdx.x * GAMES_PER_BLOCK + w;
     if (e >= d.E) return;
@@ -542,99 +560,116 @@ __global__ __launch_bounds__(256) void k_expand_backup(EngDev d) {
     const int g = d.gen[e];
     PyV res{d.res_v[e], d.res_t[e]};
     if (d.leaf_flag[e]) {
-        float* buf = buf_all[w];
-        float* vals = vals_all[w];
         const YkS s = ld_state(d.leaf_state + e);
         const uint64_t hsh = d.leaf_hash[e];
         const VInfo vi = valid_info(s, 1);
+        const ValidQ valid = valid_q(s);
         const int V = vi.V;
-        // ---- predict row -> pi = exp(log_softmax(logits))  (NNet.py:193)
-        float v;
+        // ---- prior, Ps * valids (MCTS.py:88) and np.sum(Ps) (MCTS.py:89), in registers.
+        // Lane pair (2k, 2k+1) owns leaf k of numpy's float32 pairwise tree for n = 3226 (32
+        // in-order leaves, 8-aligned): lane 2k+h holds elements 8j + 4h .. 8j + 4h + 3 of the
+        // leaf (numpy's accumulators r[4h .. 4h+3]) and, for h = 0, its n % 8 tail.
+        const int leaf = lane >> 1, h = lane & 1;
+        const int st = c_pw.start[leaf], nl = c_pw.len[leaf], G = nl >> 3, R = nl & 7;
+        float4 q[PW_GMAX];
+        float qt[PW_TMAX];
+        float v, mx = 0.f, lse = 0.f;
         const int pidx = (int)d.gstats[(long)e * 8 + 0];
         const bool rec = d.rec_pred && pidx < d.max_exp;
         float* rpi = rec ? d.rec_pi + ((long)e * d.max_exp + pidx) * ASIZE : nullptr;
         if (d.prior == 0) {
-            // the whole logits row in registers: 13 float4 per lane, one latency
-            const int row = d.leaf_row[e];
-            const float4* x4 = reinterpret_cast<const float4*>(d.logits + (long)row * PI_LD);
-            constexpr int NV = (PI_LD / 4 + 63) / 64;  // 13
-            float4 xv[NV];
+            // pi = exp(log_softmax(logits))  (NNet.py:193); predict row = game
+            const float* x = d.logits + (long)e * PI_LD + st;
+            const float NEG = -INFINITY;
 #pragma unroll
-            for (int i = 0; i < NV; i++) {
-                const int k = lane + 64 * i;
-                xv[i] = k < PI_LD / 4 ? x4[k] : make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
-            }
-            float m = -INFINITY;
+            for (int j = 0; j < PW_GMAX; j++)
+                q[j] = j < G ? *reinterpret_cast<const float4*>(x + 8 * j + 4 * h) : make_float4(NEG, NEG, NEG, NEG);
 #pragma unroll
-            for (int i = 0; i < NV; i++) {
-                const int a = 4 * (lane + 64 * i);
-                if (a + 0 < ASIZE) m = fmaxf(m, xv[i].x);
-                if (a + 1 < ASIZE) m = fmaxf(m, xv[i].y);
-                if (a + 2 < ASIZE) m = fmaxf(m, xv[i].z);
-                if (a + 3 < ASIZE) m = fmaxf(m, xv[i].w);
-            }
+            for (int r = 0; r < PW_TMAX; r++) qt[r] = (h == 0 && r < R) ? x[8 * G + r] : NEG;
+            float m = NEG;
+#pragma unroll
+            for (int j = 0; j < PW_GMAX; j++) m = fmaxf(fmaxf(m, fmaxf(q[j].x, q[j].y)), fmaxf(q[j].z, q[j].w));
+#pragma unroll
+            for (int r = 0; r < PW_TMAX; r++) m = fmaxf(m, qt[r]);
             m = wave_max(m);
             float se = 0.f;
 #pragma unroll
-            for (int i = 0; i < NV; i++) {
-                const int a = 4 * (lane + 64 * i);
-                if (a + 0 < ASIZE) se += expf(xv[i].x - m);
-                if (a + 1 < ASIZE) se += expf(xv[i].y - m);
-                if (a + 2 < ASIZE) se += expf(xv[i].z - m);
-                if (a + 3 < ASIZE) se += expf(xv[i].w - m);
-            }
-            const float lse = logf(wave_sumf(se));
+            for (int j = 0; j < PW_GMAX; j++)
+                se += (expf(q[j].x - m) + expf(q[j].y - m)) + (expf(q[j].z - m) + expf(q[j].w - m));
 #pragma unroll
-            for (int i = 0; i < NV; i++) {
-                const int a0 = 4 * (lane + 64 * i);
-                const float xs[4] = {xv[i].x, xv[i].y, xv[i].z, xv[i].w};
+            for (int r = 0; r < PW_TMAX; r++) se += expf(qt[r] - m);
+            lse = logf(wave_sumf(se));
+            mx = m;
 #pragma unroll
-                for (int t = 0; t < 4; t++) {
-                    const int a = a0 + t;
-                    if (a < ASIZE) {
-                        const float p = expf(xs[t] - m - lse);
-                        if (rec) rpi[a] = p;
-                        buf[a] = action_valid(s, 1, a) ? p : 0.0f;  // Ps * valids (MCTS.py:88)
-                    }
-                }
+            for (int j = 0; j < PW_GMAX; j++) {
+                q[j].x = expf(q[j].x - m - lse);
+                q[j].y = expf(q[j].y - m - lse);
+                q[j].z = expf(q[j].z - m - lse);
+                q[j].w = expf(q[j].w - m - lse);
             }
-            v = d.vpred[row];
+#pragma unroll
+            for (int r = 0; r < PW_TMAX; r++) qt[r] = expf(qt[r] - m - lse);
+            v = d.vpred[e];
         } else {
-            for (int a = lane; a < ASIZE; a += 64) {
-                const float p = hash_prior_pi(hsh, a);
-                if (rec) rpi[a] = p;
-                buf[a] = action_valid(s, 1, a) ? p : 0.0f;
+#pragma unroll
+            for (int j = 0; j < PW_GMAX; j++) {
+                const int a = st + 8 * j + 4 * h;
+                q[j] = j < G ? make_float4(hash_prior_pi(hsh, a), hash_prior_pi(hsh, a + 1), hash_prior_pi(hsh, a + 2),
+                                           hash_prior_pi(hsh, a + 3))
+                             : make_float4(0.f, 0.f, 0.f, 0.f);
             }
+#pragma unroll
+            for (int r = 0; r < PW_TMAX; r++) qt[r] = (h == 0 && r < R) ? hash_prior_pi(hsh, st + 8 * G + r) : 0.f;
             v = hash_prior_v(hsh);
         }
-        if (rec && lane == 0) d.rec_v[(long)e * d.max_exp + pidx] = v;
-        wave_sync();
-        // ---- np.sum(Ps) with numpy's float32 pairwise summation (MCTS.py:89)
-        if (lane < c_pw.nleaf) {
-            const int st = c_pw.start[lane], n = c_pw.len[lane];
-            const float* a = buf + st;
-            float res_s;
-            if (n < 8) {
-                res_s = 0.0f;
-                for (int i = 0; i < n; i++) res_s += a[i];
-            } else {
-                float r0 = a[0], r1 = a[1], r2 = a[2], r3 = a[3], r4 = a[4], r5 = a[5], r6 = a[6], r7 = a[7];
-                int i;
-                for (i = 8; i < n - (n % 8); i += 8) {
-                    r0 += a[i]; r1 += a[i + 1]; r2 += a[i + 2]; r3 += a[i + 3];
-                    r4 += a[i + 4]; r5 += a[i + 5]; r6 += a[i + 6]; r7 += a[i + 7];
-                }
-                res_s = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
-                for (; i < n; i++) res_s += a[i];
+        if (rec) {
+#pragma unroll
+            for (int j = 0; j < PW_GMAX; j++)
+                if (j < G) *reinterpret_cast<float4*>(rpi + st + 8 * j + 4 * h) = q[j];
+#pragma unroll
+            for (int r = 0; r < PW_TMAX; r++)
+                if (h == 0 && r < R) rpi[st + 8 * G + r] = qt[r];
+            if (lane == 0) d.rec_v[(long)e * d.max_exp + pidx] = v;
+        }
+        // mask with the valid moves
+#pragma unroll
+        for (int j = 0; j < PW_GMAX; j++) {
+            const int a = st + 8 * j + 4 * h;
+            if (j < G) {
+                if (!valid(a)) q[j].x = 0.f;
+                if (!valid(a + 1)) q[j].y = 0.f;
+                if (!valid(a + 2)) q[j].z = 0.f;
+                if (!valid(a + 3)) q[j].w = 0.f;
             }
-            vals[lane] = res_s;
         }
-        wave_sync();
-        if (lane == 0) {
-            for (int o = 0; o < c_pw.nop; o++) vals[64 + o] = vals[c_pw.a[o]] + vals[c_pw.b[o]];
+#pragma unroll
+        for (int r = 0; r < PW_TMAX; r++)
+            if (h == 0 && r < R && !valid(st + 8 * G + r)) qt[r] = 0.f;
+        // numpy pairwise_sum on the leaf: r_k = a[k] + a[8 + k] + ..., then
+        // ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)), then the tail one by one
+        float4 racc = q[0];
+#pragma unroll
+        for (int j = 1; j < PW_GMAX; j++)
+            if (j < G) {
+                racc.x += q[j].x;
+                racc.y += q[j].y;
+                racc.z += q[j].z;
+                racc.w += q[j].w;
+            }
+        const float half = (racc.x + racc.y) + (racc.z + racc.w);
+        const float other = __shfl_xor(half, 1, 64);
+        float lsum = h == 0 ? half + other : other + half;
+#pragma unroll
+        for (int r = 0; r < PW_TMAX; r++)
+            if (r < R) lsum += qt[r];  // h = 0 holds the tail
+        lsum = __shfl(lsum, lane & ~1, 64);
+        // the perfect tree over the 32 leaves, left + right at every level
+#pragma unroll
+        for (int o = 2; o <= 32; o <<= 1) {
+            const float y = __shfl_xor(lsum, o, 64);
+            lsum = (lane & o) ? y + lsum : lsum + y;
         }
-        wave_sync();
-        const float sum = vals[c_pw.root];
+        const float sum = lsum;
         // ---- allocate + write P over the compact valid set, zero edge slots
         const int VP = pad4(V);
         const uint32_t off = d.arena_top[e];
@@ -652,9 +687,17 @@ __global__ __launch_bounds__(256) void k_expand_backup(EngDev d) {
             float* P = d.arenaP + (long)e * d.AE + off;
             uint16_t* S = d.arenaS + (long)e * d.AE + off;
             const float inv_fallback = V > 0 ? 1.0f / (float)V : 0.0f;
+            // P over the compact valid set (ascending action): Ps / sum, or the uniform fallback
+            // (MCTS.py:90-107).  Written in compact order (coalesced), recomputing each prior
+            // exactly as above from the L2-resident logits row (or the hash).
+            const float* xr = d.logits + (long)e * PI_LD;
             for (int j = lane; j < VP; j += 64) {
                 float p = 0.0f;
-                if (j < V) p = sum > 0.0f ? buf[compact_to_action(vi, j)] / sum : inv_fallback;  // MCTS.py:90-107
+                if (j < V) {
+                    const int a = compact_to_action(vi, j);
+                    const float pa = d.prior == 0 ? expf(xr[a] - mx - lse) : hash_prior_pi(hsh, a);
+                    p = sum > 0.0f ? pa / sum : inv_fallback;
+                }
                 P[j] = p;
                 S[j] = 0;
             }
@@ -986,11 +1029,10 @@ int run_sims(yk_engine* eng, int sims, const uint32_t* env_ids, uint64_t* ctr, h
         hipLaunchKernelGGL(k_select, gb, bb, 0, s, d, env_ids, ctr);
         YK_LAUNCHED();
         if (d.prior == 0) {
-            prof_mark(eng, KC_SCAN, s);
-            hipLaunchKernelGGL(k_leaf_scan, dim3(1), dim3(1024), 0, s, d);
-            YK_LAUNCHED();
             prof_mark(eng, KC_FORWARD, s);
-            int rc = launch_forward(eng->net->dev, d.leaf_state, nullptr, d.rows, d.nrows, d.E, eng->logits, eng->vpred, s);
+            // predict row = game: no compaction; workgroups without a leaf exit at once
+            int rc = launch_forward(eng->net->dev, d.leaf_state, nullptr, nullptr, nullptr, d.E, eng->logits, eng->vpred, s,
+                                    d.leaf_flag);
             if (rc) return rc;
         }
         prof_mark(eng, KC_EXPAND, s);
@@ -1068,9 +1110,6 @@ int yk_engine_create(yk_engine_t** out, const yk_engine_config_t* cfg, yk_net_t*
     A(d.leaf_flag, E);
     A(d.path, E * MAXD);
     A(d.path_len, E);
-    A(d.leaf_row, E);
-    A(d.rows, E);
-    A(d.nrows, 1);
     A(d.res_v, E);
     A(d.res_t, E);
     A(eng->vpred, E);

@@ -20,13 +20,21 @@ struct NetDev {
     const float *w2, *b2, *g2, *be2;
     const float *g_pi, *be_pi, *w_pi, *b_pi;  // w_pi packed [204][H/16][64][4] (rows >= 3226 zero), b_pi [3264]
     const float *g_v, *be_v, *w_v1, *b_v1, *w_v2, *b_v2;  // w_v1 packed [8][H/16][64][4], w_v2 [128], b_v2 [1]
+    const float* vstat;  // copies staged to LDS once: [VS_* x H] + b_v1[128] w_v2[128] + b_pi[3264]
+    const float* vblk;   // per block b: b1 g1 be1 b2 g2 be2 ([6][H]), staged to LDS per block
 };
+// vstat offsets in units of H (b_v1 at VS_BV1*H, w_v2 right after it, b_pi at vs_bpi(H))
+enum { VS_BIN = 0, VS_GIN = 1, VS_BEIN = 2, VS_GPI = 3, VS_BEPI = 4, VS_GV = 5, VS_BEV = 6, VS_BV1 = 7 };
+constexpr int vs_bpi(int H) { return 7 * H + 256; }
+constexpr int vstat_size(int H) { return vs_bpi(H) + PI_LD; }
 
 // Full forward: features (from packed states, or explicit rows x[n][59]) ->
 // logits[n][PI_LD] (pi_head before softmax) and v[n] = tanh(v_head).  `rows` (optional) maps
-// output row i to input index rows[i]; `count` (optional, device) overrides n.
+// output row i to input index rows[i]; `count` (optional, device) overrides n; `active`
+// (optional, device, [n]) lets a workgroup whose 16 rows are all inactive exit at once.
 int launch_forward(const NetDev& net, const yk_state_t* states, const float* x, const int32_t* rows,
-                   const int32_t* count, int n, float* logits, float* v, hipStream_t stream);
+                   const int32_t* count, int n, float* logits, float* v, hipStream_t stream,
+                   const uint8_t* active = nullptr);
 // pi[n][3226] = exp(log_softmax(logits[:, :3226]))
 int launch_softmax(const float* logits, float* pi, int n, hipStream_t stream);
 

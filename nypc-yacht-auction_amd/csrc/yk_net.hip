@@ -2,13 +2,19 @@
 // (yacht/pytorch/YachtNNet.py:8-70), batched over all pending leaves, float32.
 //
 // One kernel, k_forward, carries all 3,320,576 FLOP per row (hidden 256, 6 blocks): a
-// 1024-thread workgroup (16 waves, 4 per SIMD) owns 16 rows and keeps their activations in
-// LDS through featurize -> Linear/LN/SiLU -> 6 x ResidualBlock -> head LayerNorms ->
-// policy logits (204 x 16 columns) and the value head.  Every dense layer runs on
-// v_mfma_f32_16x16x4_f32 (exact f32: fmaf chains), so results track torch's float32 CPU
-// path within the north star's 1e-5 (tests/test_gpu_net.py).  Weights are pre-packed in
-// MFMA fragment order (yk_net.h) so each wave streams them as contiguous 1 KB loads, and
-// the next layer's slice is issued before the LayerNorm phase so it flies under it.
+// 512-thread workgroup (8 waves, 2 per SIMD, up to 256 VGPRs each) owns 16 rows and keeps
+// their activations in LDS through featurize -> Linear/LN/SiLU -> 6 x ResidualBlock -> head
+// LayerNorms -> value head and policy logits (204 x 16 columns).  Every dense layer runs on
+// v_mfma_f32_16x16x4_f32 (exact f32: fmaf chains), so results track torch's float32 CPU path
+// within the north star's 1e-5 (tests/test_gpu_net.py).
+//
+// The kernel is latency-bound per workgroup (one per CU), so the weight stream must never
+// stop: weights are pre-packed in MFMA fragment order (yk_net.h), each wave keeps a ring of
+// W k-blocks of its fragments in registers, and as soon as a k-block is consumed its
+// registers are refilled with the fragment W k-blocks ahead - across layer boundaries, so the
+// next layer streams in under the current GEMM and the LayerNorm phase.  Nothing the kernel
+// waits on is ever issued behind that stream (vmcnt retires in order): biases and LayerNorm
+// vectors live in LDS, and the kernel must not spill (scratch also counts in vmcnt).
 #include <vector>
 
 #include "yk_api.h"
@@ -19,101 +25,123 @@ using namespace yk;
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
-// Diagnostic builds only (tools/trunk_ablate.cpp): 2 = no MFMA, 3 = no weight loads.
-#ifndef YK_ABL
-#define YK_ABL 0
-#endif
-
 namespace {
 
-constexpr int ROWS = 16;  // rows per workgroup
-constexpr int FPAD = 68;  // feature tile row stride (64 + 4)
-constexpr int PCH = 4;    // policy-head tiles per chunk (accumulators in flight per wave)
+// Diagnostic builds only: per-phase s_memtime stamps of wave 0 (tools/trunk_ablate.cpp).
+#ifdef YK_TIMING
+__device__ unsigned long long g_tstamp[4096 * 32];
+#define TSTAMP(i) \
+    if (threadIdx.x == 0) g_tstamp[blockIdx.x * 32 + (i)] = __builtin_amdgcn_s_memtime()
+#define WSTAMP(i) /* per wave: slots i + wave */ \
+    if ((threadIdx.x & 63) == 0) g_tstamp[blockIdx.x * 32 + (i) + (threadIdx.x >> 6)] = __builtin_amdgcn_s_memtime()
+#else
+#define TSTAMP(i)
+#define WSTAMP(i)
+#endif
 
-__device__ __forceinline__ float silu(float x) { return x / (1.0f + expf(-x)); }
+constexpr int ROWS = 16;     // rows per workgroup (the MFMA M)
+constexpr int WAVES = 8;     // waves per workgroup
+constexpr int NTHR = 64 * WAVES;
+constexpr int RPW = ROWS / WAVES;  // rows per wave in the row passes
+constexpr int FPAD = 68;     // feature tile row stride (64 + 4)
+constexpr int PCH = 4;       // policy-head tiles per chunk
+constexpr int PW = 8;        // policy-head ring depth (k-blocks)
 
+// SiLU with the hardware exp / reciprocal (<= 2 ulp each; well inside the 1e-5 contract)
+__device__ __forceinline__ float silu(float x) { return x * __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
+
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ float dpp_f(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, ROW_MASK, 0xF, false));
+}
+// full-wave sum with DPP (quad perms, half-row / row mirrors, row broadcasts) -> lane 63
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+    v += dpp_f<0xB1, 0xF>(v);   // quad_perm [1,0,3,2]
+    v += dpp_f<0x4E, 0xF>(v);   // quad_perm [2,3,0,1]
+    v += dpp_f<0x141, 0xF>(v);  // row_half_mirror
+    v += dpp_f<0x140, 0xF>(v);  // row_mirror: every lane holds its 16-lane row sum
+    v += dpp_f<0x142, 0xA>(v);  // row_bcast15 into rows 1, 3
+    v += dpp_f<0x143, 0xC>(v);  // row_bcast31 into rows 2, 3
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
 }
 
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops, NOT for its
-// outstanding global loads (a __syncthreads() would drain vmcnt and expose the weight
-// stream's latency at every layer).
+// outstanding global loads (a __syncthreads() would drain vmcnt and the weight stream).
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// fragment (tile nt, k-block kb) of a packed [N][K] matrix with KB k-blocks: 1 KB per wave
 __device__ __forceinline__ float4 ld_frag(const float* __restrict__ P, int KB, int nt, int kb, int lane) {
-#if YK_ABL == 3
-    return make_float4(1e-3f * kb, 1e-3f * nt, 2e-3f, 3e-3f + P[0] * 0.f);
-#else
     return *reinterpret_cast<const float4*>(P + ((long)(nt * KB + kb) * 64 + lane) * 4);
-#endif
 }
 
-// A wave's weight slice for one dense layer: NT 16-column tiles starting at tile nt0, all K.
-template <int K, int NT>
-struct WSlice {
-    float4 b[K / 16][NT];
-};
-template <int K, int NT>
-__device__ __forceinline__ void load_w(WSlice<K, NT>& ws, const float* __restrict__ P, int nt0) {
+__device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// acc[t] = A[16 x K] (LDS, row stride lda) x W^T over this wave's NT tiles (nt0 ...), with the
+// fragments taken from the ring; k-block kb lives in slot kb % RW.  After use, the slot is
+// refilled with k-block kb + RW of this layer (cur) or, past its end, of the next layer (nxt,
+// same shape).  Lane l supplies A[l&15][16kb + 4(l>>4) + i] to MFMA i of a k-block.  One tile
+// alternates two accumulators (40-cycle dependent latency vs 32-cycle issue).
+template <int K, int NT, int RW, bool NEXT = true>
+__device__ __forceinline__ void mma_ring(const float* A, int lda, float4 (&ring)[RW][NT], floatx4 (&acc)[NT],
+                                         const float* __restrict__ cur, const float* __restrict__ nxt, int nt0) {
+    constexpr int KB = K / 16;
     const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int kb = 0; kb < K / 16; kb++)
-#pragma unroll
-        for (int t = 0; t < NT; t++) ws.b[kb][t] = ld_frag(P, K / 16, nt0 + t, kb, lane);
-    __builtin_amdgcn_sched_barrier(0);  // issue them here, ahead of the work that hides them
-}
-
-// acc[t] = A[16 x K] (LDS, row stride lda) x slice^T.  Lane l supplies A[l&15][16kb + 4(l>>4) + i]
-// and W[.][16kb + 4(l>>4) + i] to MFMA i of each 16-deep k-block.  Two partial accumulators
-// keep consecutive MFMAs independent (40-cycle dependent latency vs 32-cycle issue).
-template <int K, int NT>
-__device__ __forceinline__ void mma16(const float* A, int lda, const WSlice<K, NT>& ws, floatx4 (&acc)[NT]) {
-    const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
+    const float* ap = A + (lane & 15) * lda + 4 * (lane >> 4);
     floatx4 acc2[NT];
 #pragma unroll
     for (int t = 0; t < NT; t++) acc[t] = acc2[t] = floatx4{0.f, 0.f, 0.f, 0.f};
-    const float* ap = A + r * lda + 4 * q;
-#if YK_ABL == 2
-    acc[0][0] = ap[0] + ws.b[0][0].x;
-    return;
-#endif
+    float4 a = *reinterpret_cast<const float4*>(ap);
 #pragma unroll
-    for (int kb = 0; kb < K / 16; kb++) {
-        const float4 a = *reinterpret_cast<const float4*>(ap + 16 * kb);
+    for (int kb = 0; kb < KB; kb++) {
+        const float4 an = *reinterpret_cast<const float4*>(ap + 16 * ((kb + 1) % KB));
+        float4(&w)[NT] = ring[kb % RW];
+        if constexpr (NT == 1) {
+            acc[0] = mfma4(a.x, w[0].x, acc[0]);
+            acc2[0] = mfma4(a.y, w[0].y, acc2[0]);
+            acc[0] = mfma4(a.z, w[0].z, acc[0]);
+            acc2[0] = mfma4(a.w, w[0].w, acc2[0]);
+        } else {
 #pragma unroll
-        for (int t = 0; t < NT; t++) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, ws.b[kb][t].x, acc[t], 0, 0, 0);
+            for (int t = 0; t < NT; t++) acc[t] = mfma4(a.x, w[t].x, acc[t]);
 #pragma unroll
-        for (int t = 0; t < NT; t++) acc2[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, ws.b[kb][t].y, acc2[t], 0, 0, 0);
+            for (int t = 0; t < NT; t++) acc[t] = mfma4(a.y, w[t].y, acc[t]);
 #pragma unroll
-        for (int t = 0; t < NT; t++) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, ws.b[kb][t].z, acc[t], 0, 0, 0);
+            for (int t = 0; t < NT; t++) acc[t] = mfma4(a.z, w[t].z, acc[t]);
 #pragma unroll
-        for (int t = 0; t < NT; t++) acc2[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, ws.b[kb][t].w, acc2[t], 0, 0, 0);
+            for (int t = 0; t < NT; t++) acc[t] = mfma4(a.w, w[t].w, acc[t]);
+        }
+        const int g = kb + RW;
+        if (g < KB || NEXT) {
+#pragma unroll
+            for (int t = 0; t < NT; t++)
+                w[t] = g < KB ? ld_frag(cur, KB, nt0 + t, g, lane) : ld_frag(nxt, KB, nt0 + t, g - KB, lane);
+        }
+        __builtin_amdgcn_sched_barrier(0);  // keep the refill here, a ring's depth ahead of its use
+        a = an;
     }
-#pragma unroll
-    for (int t = 0; t < NT; t++) acc[t] += acc2[t];
+    if constexpr (NT == 1) acc[0] += acc2[0];
 }
 
-// D[16 x 16] tile t of the wave: lane holds rows 4(l>>4)+j, column 16(nt0 + t) + (l&15)
+// D[16 x 16] tile t of the wave: lane holds rows 4(l>>4)+j, column 16(nt0 + t) + (l&15).
+// bias == nullptr: raw accumulators (the row pass adds the bias).
 template <int NT>
-__device__ __forceinline__ void store_acc(float* D, int ldd, int nt0, const floatx4 (&acc)[NT],
-                                          const float* __restrict__ bias) {
+__device__ __forceinline__ void store_acc(float* D, int ldd, int nt0, const floatx4 (&acc)[NT], const float* bias) {
     const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
 #pragma unroll
     for (int t = 0; t < NT; t++) {
         const int c = 16 * (nt0 + t) + r;
-        const float b = bias[c];
+        const float b = bias ? bias[c] : 0.f;
 #pragma unroll
-        for (int j = 0; j < 4; j++) D[(4 * q + j) * ldd + c] = acc[t][j] + b;
+        for (int j = 0; j < 4; j++) D[(4 * q + j) * ldd + c] = bias ? acc[t][j] + b : acc[t][j];
     }
 }
 
-// nn.LayerNorm over H values held VPL per lane (two-pass, biased variance, eps 1e-5)
+// nn.LayerNorm over H values held VPL per lane (two-pass, biased variance, eps 1e-5);
+// g / b point into LDS
 template <int VPL>
-__device__ __forceinline__ void layernorm(float (&x)[VPL], const float* __restrict__ g, const float* __restrict__ b,
-                                          int c0, int H) {
+__device__ __forceinline__ void layernorm(float (&x)[VPL], const float* g, const float* b, int c0, int H) {
     float s = 0.f;
 #pragma unroll
     for (int i = 0; i < VPL; i++) s += x[i];
@@ -129,35 +157,125 @@ __device__ __forceinline__ void layernorm(float (&x)[VPL], const float* __restri
     for (int i = 0; i < VPL; i++) x[i] = (x[i] - mean) * rstd * g[c0 + i] + b[c0 + i];
 }
 
-// Dense layers: wave w owns output tiles [NT w, NT (w+1)); row passes (LayerNorm / SiLU /
-// residual): wave w owns row w; policy head: wave w owns tiles w, w + 16, w + 32, ...
+// Policy head chunks: wave w owns tiles w + WAVES j; a chunk holds NTL <= PCH of them
+// (tiles tb, tb + WAVES, ...).  The ring (PW k-blocks of PCH fragments) streams across chunk
+// boundaries: past the last k-block it refills with the next chunk's first k-blocks (NXT
+// tiles, from tb_next).  Tiles >= PI_TILES (the padded last chunk) are computed on a
+// duplicate of tile tb and not stored.
+__device__ __forceinline__ int pi_tile(int tb, int t) {  // real tile to load for slot t
+    const int x = tb + WAVES * t;
+#ifdef YK_DIAG_L1
+    return x & 1;  // diagnostic: a 2-tile footprint, L1-resident
+#else
+    return x < PI_TILES ? x : tb;
+#endif
+}
+template <int KB, int NTL, int NXT, int RD = (PW < KB ? PW : KB)>
+__device__ __forceinline__ void ring_chunk(const float* A, int lda, float4 (&ring)[RD][PCH], floatx4 (&pa)[NTL],
+                                           const float* __restrict__ W, int tb, const float* __restrict__ Wn,
+                                           int tb_next) {
+    const int lane = threadIdx.x & 63;
+    const float* ap = A + (lane & 15) * lda + 4 * (lane >> 4);
+#pragma unroll
+    for (int t = 0; t < NTL; t++) pa[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+    float4 a = *reinterpret_cast<const float4*>(ap);
+#pragma unroll
+    for (int kb = 0; kb < KB; kb++) {
+        const float4 an = *reinterpret_cast<const float4*>(ap + 16 * ((kb + 1) % KB));
+        float4(&w)[PCH] = ring[kb % RD];
+#pragma unroll
+        for (int t = 0; t < NTL; t++) pa[t] = mfma4(a.x, w[t].x, pa[t]);
+#pragma unroll
+        for (int t = 0; t < NTL; t++) pa[t] = mfma4(a.y, w[t].y, pa[t]);
+#pragma unroll
+        for (int t = 0; t < NTL; t++) pa[t] = mfma4(a.z, w[t].z, pa[t]);
+#pragma unroll
+        for (int t = 0; t < NTL; t++) pa[t] = mfma4(a.w, w[t].w, pa[t]);
+        const int g = kb + RD;
+        if (g < KB) {
+#pragma unroll
+            for (int t = 0; t < NTL; t++) w[t] = ld_frag(W, KB, pi_tile(tb, t), g, lane);
+        } else {
+#pragma unroll
+            for (int t = 0; t < NXT; t++) w[t] = ld_frag(Wn, KB, pi_tile(tb_next, t), g - KB, lane);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        a = an;
+    }
+}
+template <int KB, int NTL, int NXT, int RD = (PW < KB ? PW : KB)>
+__device__ __forceinline__ void pi_chunk(const float* A, int lda, float4 (&ring)[RD][PCH], const float* __restrict__ W,
+                                         int tb, int tb_next, const float* bias, float* __restrict__ logits, int row0,
+                                         int n) {
+    const int lane = threadIdx.x & 63;
+    floatx4 pa[NTL];
+    ring_chunk<KB, NTL, NXT, RD>(A, lda, ring, pa, W, tb, W, tb_next);
+    const int rr = lane & 15, q = lane >> 4;
+#pragma unroll
+    for (int t = 0; t < NTL; t++) {
+        const int tile = tb + WAVES * t;
+        if (tile < PI_TILES) {
+            const int col = 16 * tile + rr;
+            const float b = bias[col];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int row = row0 + 4 * q + j;
+                if (row < n) logits[(long)row * PI_LD + col] = pa[t][j] + b;
+            }
+        }
+    }
+}
+
+// Row passes (LayerNorm / SiLU / residual): wave w owns rows RPW w ... RPW w + RPW - 1.
 template <int H>
-__global__ __launch_bounds__(1024) void k_forward(NetDev net, const yk_state_t* __restrict__ states,
+__global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* __restrict__ states,
                                                  const float* __restrict__ xin, const int32_t* __restrict__ rows,
                                                  const int32_t* __restrict__ count, int n,
-                                                 float* __restrict__ logits, float* __restrict__ vout) {
-    constexpr int LD = (H > 128 ? H : 128) + 4;  // X also holds the 128-wide v_head hidden
-    constexpr int NT = H >= 256 ? H / 256 : 1;    // 16-col tiles per wave in H-wide layers
-    constexpr int NACT = H / (16 * NT);           // waves with columns of the H-wide layers
-    constexpr int VPL = H / 64;                   // values per lane in row passes
+                                                 float* __restrict__ logits, float* __restrict__ vout,
+                                                 const uint8_t* __restrict__ active) {
+    constexpr int LD = (H > 128 ? H : 128) + 4;      // X also holds the 128-wide v_head hidden
+    constexpr int NT = H >= 16 * WAVES ? H / (16 * WAVES) : 1;  // 16-col tiles per wave, H-wide layers
+    constexpr int NACT = H / (16 * NT);              // waves owning columns of the H-wide layers
+    constexpr int VPL = H / 64;                      // values per lane in row passes
     constexpr int KB = H / 16;
+    constexpr int RW = KB * NT <= 32 ? KB : 32 / NT;  // trunk ring depth: <= 32 fragments per lane
+    constexpr int NVS = vstat_size(H), NVB = 6 * H;
+    static_assert(128 / 16 == WAVES, "v_head.2 maps one 16-column tile to each wave");
     __shared__ __attribute__((aligned(16))) float X[ROWS * LD];
     __shared__ __attribute__((aligned(16))) float T[ROWS * LD];
     __shared__ __attribute__((aligned(16))) float F[ROWS * FPAD];
+    __shared__ __attribute__((aligned(16))) float VS[NVS];  // static vectors (yk_net.h VS_*)
+    __shared__ __attribute__((aligned(16))) float VB[NVB];  // this block's b1 g1 be1 b2 g2 be2
 
     if (count) n = min(n, *count);
     const int row0 = blockIdx.x * ROWS;
     if (row0 >= n) return;
+    if (active) {  // uniform: every wave reads the same 16 flags
+        bool any = false;
+#pragma unroll
+        for (int i = 0; i < ROWS; i++) any |= row0 + i < n && active[row0 + i];
+        if (!any) return;
+    }
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const bool gw = wave < NACT;           // owns columns of the H-wide layers
-    const bool vw = wave * 16 * NT < 128;  // owns columns of v_head.2
+    const bool gw = wave < NACT;  // owns columns of the H-wide layers
     const int nt0 = wave * NT;
-    const int r = wave;  // row of the row passes
     const int c0 = lane * VPL;
+    TSTAMP(0);
 
-    // featurize (state_to_vec, NNet.py:65-86), zero padded to K = 64: one value per thread
+    // static vectors first: their LDS writes must not wait behind the weight stream
     {
-        const int rr = tid >> 6, f = tid & 63;
+        constexpr int NV4 = NVS / 4, PER = (NV4 + NTHR - 1) / NTHR;
+        float4 v[PER];
+#pragma unroll
+        for (int k = 0; k < PER; k++) v[k] = reinterpret_cast<const float4*>(net.vstat)[min(tid + NTHR * k, NV4 - 1)];
+#pragma unroll
+        for (int k = 0; k < PER; k++)
+            if (tid + NTHR * k < NV4) reinterpret_cast<float4*>(VS)[tid + NTHR * k] = v[k];
+    }
+    // featurize (state_to_vec, NNet.py:65-86), zero padded to K = 64
+#pragma unroll
+    for (int k = 0; k < ROWS * 64 / NTHR; k++) {
+        const int idx = tid + NTHR * k, rr = idx >> 6, f = idx & 63;
         const int row = row0 + rr;
         float val = 0.f;
         if (row < n && f < FEAT) {
@@ -168,166 +286,184 @@ __global__ __launch_bounds__(1024) void k_forward(NetDev net, const yk_state_t* 
                 const uint4* p = reinterpret_cast<const uint4*>(states + src);
                 YkS s;
 #pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    uint4 u = p[k];
-                    s.w[2 * k] = (uint64_t)u.x | ((uint64_t)u.y << 32);
-                    s.w[2 * k + 1] = (uint64_t)u.z | ((uint64_t)u.w << 32);
+                for (int q = 0; q < 4; q++) {
+                    uint4 u = p[q];
+                    s.w[2 * q] = (uint64_t)u.x | ((uint64_t)u.y << 32);
+                    s.w[2 * q + 1] = (uint64_t)u.z | ((uint64_t)u.w << 32);
                 }
                 val = feature(s, f);
             }
         }
         F[rr * FPAD + f] = val;
     }
-    lds_barrier();
-
-    floatx4 acc[NT];
-    WSlice<H, NT> ws;  // next dense layer's weights, in flight during the row passes
-    // inp: Linear -> LayerNorm -> SiLU (-> Dropout, identity in eval)  YachtNNet.py:30-35
+    // weight stream: the input layer, then the trunk ring's first RW k-blocks of fc1 (block 0)
+    float4 w0[4][NT];
+    float4 ring[RW][NT];
+    const float* w_first = net.NB > 0 ? net.w1 : net.w_v1;
     if (gw) {
-        WSlice<64, NT> w0;
-        load_w<64, NT>(w0, net.w_in, nt0);
-        if (net.NB > 0) load_w<H, NT>(ws, net.w1, nt0);
-        mma16<64, NT>(F, FPAD, w0, acc);
-        store_acc<NT>(T, LD, nt0, acc, net.b_in);
+#pragma unroll
+        for (int kb = 0; kb < 4; kb++)
+#pragma unroll
+            for (int t = 0; t < NT; t++) w0[kb][t] = ld_frag(net.w_in, 4, nt0 + t, kb, lane);
+#pragma unroll
+        for (int kb = 0; kb < RW; kb++)
+#pragma unroll
+            for (int t = 0; t < NT; t++) ring[kb][t] = ld_frag(w_first, KB, nt0 + t, kb, lane);
     }
     lds_barrier();
-    {
+    TSTAMP(1);
+
+    floatx4 acc[NT];
+    // inp: Linear -> LayerNorm -> SiLU (-> Dropout, identity in eval)  YachtNNet.py:30-35
+    if (gw) {
+        const float* ap = F + (lane & 15) * FPAD + 4 * (lane >> 4);
+        floatx4 acc2[NT];
+#pragma unroll
+        for (int t = 0; t < NT; t++) acc[t] = acc2[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kb = 0; kb < 4; kb++) {
+            const float4 a = *reinterpret_cast<const float4*>(ap + 16 * kb);
+#pragma unroll
+            for (int t = 0; t < NT; t++) {
+                acc[t] = mfma4(a.x, w0[kb][t].x, acc[t]);
+                acc2[t] = mfma4(a.y, w0[kb][t].y, acc2[t]);
+                acc[t] = mfma4(a.z, w0[kb][t].z, acc[t]);
+                acc2[t] = mfma4(a.w, w0[kb][t].w, acc2[t]);
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < NT; t++) acc[t] += acc2[t];
+        store_acc<NT>(T, LD, nt0, acc, nullptr);
+    }
+    lds_barrier();
+#pragma unroll
+    for (int rr = 0; rr < RPW; rr++) {
+        const int r = wave * RPW + rr;
         float x[VPL];
 #pragma unroll
-        for (int i = 0; i < VPL; i++) x[i] = T[r * LD + c0 + i];
-        layernorm<VPL>(x, net.g_in, net.be_in, c0, H);
+        for (int i = 0; i < VPL; i++) x[i] = T[r * LD + c0 + i] + VS[VS_BIN * H + c0 + i];
+        layernorm<VPL>(x, VS + VS_GIN * H, VS + VS_BEIN * H, c0, H);
 #pragma unroll
         for (int i = 0; i < VPL; i++) X[r * LD + c0 + i] = silu(x[i]);
     }
     lds_barrier();
+    TSTAMP(2);
 
     // ResidualBlock x NB: h = LN1(SiLU(fc1 x)); h = LN2(SiLU(fc2 h)); x + h  YachtNNet.py:17-21
     for (int b = 0; b < net.NB; b++) {
-        const long wo = (long)b * H * H, bo = (long)b * H;
-        if (gw) {
-            mma16<H, NT>(X, LD, ws, acc);
-            load_w<H, NT>(ws, net.w2 + wo, nt0);  // fc2 weights fly during LN1
-            store_acc<NT>(T, LD, nt0, acc, net.b1 + bo);
-        }
+        const long wo = (long)b * H * H;
+        const float* after = net.w1 + wo + (long)H * H;  // the stream after fc2: the next block's fc1
+        constexpr int NB4 = NVB / 4, PB = (NB4 + NTHR - 1) / NTHR;
+        float4 vb[PB];
+#pragma unroll
+        for (int k = 0; k < PB; k++) vb[k] = reinterpret_cast<const float4*>(net.vblk + (long)b * NVB)[min(tid + NTHR * k, NB4 - 1)];
+        if (gw) mma_ring<H, NT, RW>(X, LD, ring, acc, net.w1 + wo, net.w2 + wo, nt0);
+        if (b == 2) TSTAMP(16);
+#pragma unroll
+        for (int k = 0; k < PB; k++)  // the previous block's readers passed a barrier
+            if (tid + NTHR * k < NB4) reinterpret_cast<float4*>(VB)[tid + NTHR * k] = vb[k];
+        if (gw) store_acc<NT>(T, LD, nt0, acc, nullptr);
         lds_barrier();
-        {
+        if (b == 2) TSTAMP(17);
+#pragma unroll
+        for (int rr = 0; rr < RPW; rr++) {
+            const int r = wave * RPW + rr;
             float x[VPL];
 #pragma unroll
-            for (int i = 0; i < VPL; i++) x[i] = silu(T[r * LD + c0 + i]);
-            layernorm<VPL>(x, net.g1 + bo, net.be1 + bo, c0, H);
+            for (int i = 0; i < VPL; i++) x[i] = silu(T[r * LD + c0 + i] + VB[c0 + i]);
+            layernorm<VPL>(x, VB + H, VB + 2 * H, c0, H);
 #pragma unroll
             for (int i = 0; i < VPL; i++) T[r * LD + c0 + i] = x[i];
         }
         lds_barrier();
-        if (gw) mma16<H, NT>(T, LD, ws, acc);
-        if (b + 1 < net.NB) {
-            if (gw) load_w<H, NT>(ws, net.w1 + wo + (long)H * H, nt0);  // next fc1
-        } else if (vw) {
-            load_w<H, NT>(ws, net.w_v1, nt0);  // v_head.2
+        if (b == 2) TSTAMP(18);
+        if (gw) {
+            if (b + 1 < net.NB) mma_ring<H, NT, RW>(T, LD, ring, acc, net.w2 + wo, after, nt0);
+            else mma_ring<H, NT, RW, false>(T, LD, ring, acc, net.w2 + wo, nullptr, nt0);
         }
+        if (b == 2) TSTAMP(19);
+        lds_barrier();  // every wave is done reading T
+        if (b == 2) TSTAMP(20);
+        if (gw) store_acc<NT>(T, LD, nt0, acc, nullptr);
         lds_barrier();
-        if (gw) store_acc<NT>(T, LD, nt0, acc, net.b2 + bo);
-        lds_barrier();
-        {
+        if (b == 2) TSTAMP(21);
+#pragma unroll
+        for (int rr = 0; rr < RPW; rr++) {
+            const int r = wave * RPW + rr;
             float x[VPL];
 #pragma unroll
-            for (int i = 0; i < VPL; i++) x[i] = silu(T[r * LD + c0 + i]);
-            layernorm<VPL>(x, net.g2 + bo, net.be2 + bo, c0, H);
+            for (int i = 0; i < VPL; i++) x[i] = silu(T[r * LD + c0 + i] + VB[3 * H + c0 + i]);
+            layernorm<VPL>(x, VB + 4 * H, VB + 5 * H, c0, H);
 #pragma unroll
             for (int i = 0; i < VPL; i++) X[r * LD + c0 + i] += x[i];
         }
         lds_barrier();
+        if (b < 6) TSTAMP(3 + b);
     }
 
-    // heads: pi_head = LN -> SiLU -> Linear; v_head = LN -> SiLU -> Linear -> SiLU -> Linear -> tanh
-    {
+    // heads: pi_head = LN -> SiLU -> Linear; v_head = LN -> SiLU -> Linear -> SiLU -> Linear -> tanh.
+    // One ring streams v_head.2 (one 16-column tile per wave, first) and then the policy head;
+    // its first k-blocks fly under the LayerNorms.
+    constexpr int RD = PW < KB ? PW : KB;  // policy ring depth (k-blocks)
+    float4 pring[RD][PCH];
+#pragma unroll
+    for (int kb = 0; kb < RD; kb++) pring[kb][0] = ld_frag(net.w_v1, KB, wave, kb, lane);
+#pragma unroll
+    for (int rr = 0; rr < RPW; rr++) {
+        const int r = wave * RPW + rr;
         float x[VPL], y[VPL];
 #pragma unroll
         for (int i = 0; i < VPL; i++) x[i] = y[i] = X[r * LD + c0 + i];
-        layernorm<VPL>(x, net.g_pi, net.be_pi, c0, H);
-        layernorm<VPL>(y, net.g_v, net.be_v, c0, H);
+        layernorm<VPL>(x, VS + VS_GPI * H, VS + VS_BEPI * H, c0, H);
+        layernorm<VPL>(y, VS + VS_GV * H, VS + VS_BEV * H, c0, H);
 #pragma unroll
         for (int i = 0; i < VPL; i++) {
-            X[r * LD + c0 + i] = silu(x[i]);  // a_pi (each wave rewrites only its own row)
+            X[r * LD + c0 + i] = silu(x[i]);  // a_pi (each wave rewrites only its own rows)
             T[r * LD + c0 + i] = silu(y[i]);  // a_v
         }
     }
     lds_barrier();
-    floatx4 av[NT];
-    if (vw) {  // v_head.2: Linear(H, 128) (weights already in flight)
-        if (net.NB == 0) load_w<H, NT>(ws, net.w_v1, nt0);
-        mma16<H, NT>(T, LD, ws, av);
+    TSTAMP(9);
+    floatx4 av[1];  // v_head.2: Linear(H, 128), tile `wave`; its refills stream the first policy chunk
+    // policy head (pi_head.2): 204 tiles of 16 columns; wave w owns tiles w + 8 j: FULL chunks
+    // of PCH tiles, then one padded chunk of LASTN, all through one ring
+    constexpr int FULL = PI_TILES / (WAVES * PCH);
+    constexpr int LASTN = (PI_TILES - FULL * WAVES * PCH + WAVES - 1) / WAVES;
+    static_assert(LASTN >= 1 && LASTN <= PCH, "policy-head remainder shape");
+    const float* bpi = VS + vs_bpi(H);
+    // the workgroups of an XCD walk the full chunks in rotated orders, so they do not all read
+    // the same weight lines at the same moment (each tile's k order, hence the numerics, is fixed)
+    const int rot = blockIdx.x % FULL;
+    auto chunk_tb = [&](int c) { return wave + WAVES * PCH * ((c + rot) % FULL); };
+    ring_chunk<KB, 1, PCH>(T, LD, pring, av, net.w_v1, wave, net.w_pi, chunk_tb(0));
+#pragma unroll 1
+    for (int c = 0; c + 1 < FULL; c++) {
+        pi_chunk<KB, PCH, PCH>(X, LD, pring, net.w_pi, chunk_tb(c), chunk_tb(c + 1), bpi, logits, row0, n);
+        if (c & 1) TSTAMP(10 + (c >> 1));  // stamps 10, 11 after chunk pairs
     }
-    // policy head (pi_head.2): 204 tiles of 16 columns over the 16 waves, PCH at a time,
-    // with the next k-block's weight fragments in flight
-    for (int c = 0; c * 16 * PCH < PI_TILES; c++) {
-        floatx4 pa[PCH];
-        float4 wb[2][PCH];
-        const int tbase = wave + 16 * PCH * c;  // tile of slot t: tbase + 16 t (wave-uniform)
-        const int ntile = min(PCH, (PI_TILES - tbase + 15) / 16);
-        if (ntile <= 0) break;
-#pragma unroll
-        for (int t = 0; t < PCH; t++) {
-            pa[t] = floatx4{0.f, 0.f, 0.f, 0.f};
-            if (t < ntile) wb[0][t] = ld_frag(net.w_pi, KB, tbase + 16 * t, 0, lane);
-        }
-        const float* ap = X + (lane & 15) * LD + 4 * (lane >> 4);
-#pragma unroll
-        for (int kb = 0; kb < KB; kb++) {
-            if (kb + 1 < KB) {
-#pragma unroll
-                for (int t = 0; t < PCH; t++)
-                    if (t < ntile) wb[(kb + 1) & 1][t] = ld_frag(net.w_pi, KB, tbase + 16 * t, kb + 1, lane);
-            }
-            const float4 a = *reinterpret_cast<const float4*>(ap + 16 * kb);
-            const int cb = kb & 1;
-#if YK_ABL != 2
-            if (ntile == PCH) {
-#pragma unroll
-                for (int t = 0; t < PCH; t++) pa[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, wb[cb][t].x, pa[t], 0, 0, 0);
-#pragma unroll
-                for (int t = 0; t < PCH; t++) pa[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, wb[cb][t].y, pa[t], 0, 0, 0);
-#pragma unroll
-                for (int t = 0; t < PCH; t++) pa[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, wb[cb][t].z, pa[t], 0, 0, 0);
-#pragma unroll
-                for (int t = 0; t < PCH; t++) pa[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, wb[cb][t].w, pa[t], 0, 0, 0);
-            } else {
-#pragma unroll
-                for (int t = 0; t < PCH; t++)
-                    if (t < ntile) {
-                        pa[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, wb[cb][t].x, pa[t], 0, 0, 0);
-                        pa[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, wb[cb][t].y, pa[t], 0, 0, 0);
-                        pa[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, wb[cb][t].z, pa[t], 0, 0, 0);
-                        pa[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, wb[cb][t].w, pa[t], 0, 0, 0);
-                    }
-            }
-#else
-            pa[0][0] += a.x + wb[cb][0].x;
-#endif
-        }
-        const int rr = lane & 15, q = lane >> 4;
-#pragma unroll
-        for (int t = 0; t < PCH; t++) {
-            if (t < ntile) {
-                const int col = 16 * (tbase + 16 * t) + rr;
-                const float bias = net.b_pi[col];
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    const int row = row0 + 4 * q + j;
-                    if (row < n) logits[(long)row * PI_LD + col] = pa[t][j] + bias;
-                }
-            }
-        }
+    {
+        const int tl = wave + WAVES * PCH * FULL;  // the padded last chunk
+        pi_chunk<KB, PCH, LASTN>(X, LD, pring, net.w_pi, chunk_tb(FULL - 1), tl, bpi, logits, row0, n);
+        TSTAMP(12);
+        pi_chunk<KB, LASTN, 0>(X, LD, pring, net.w_pi, tl, 0, bpi, logits, row0, n);
     }
+    TSTAMP(14);
+    WSTAMP(24);
     lds_barrier();  // every wave is done reading a_pi (X)
-    if (vw) store_acc<NT>(X, LD, nt0, av, net.b_v1);
+    TSTAMP(22);
+    store_acc<1>(X, LD, wave, av, VS + VS_BV1 * H);
     lds_barrier();
-    {  // SiLU -> Linear(128, 1) -> tanh  YachtNNet.py:49-52,69
+    TSTAMP(23);
+#pragma unroll
+    for (int rr = 0; rr < RPW; rr++) {  // SiLU -> Linear(128, 1) -> tanh  YachtNNet.py:49-52,69
+        const int r = wave * RPW + rr;
         const int row = row0 + r;
-        float s = silu(X[r * LD + 2 * lane]) * net.w_v2[2 * lane] + silu(X[r * LD + 2 * lane + 1]) * net.w_v2[2 * lane + 1];
+        const float* wv2 = VS + VS_BV1 * H + 128;
+        float s = silu(X[r * LD + 2 * lane]) * wv2[2 * lane] + silu(X[r * LD + 2 * lane + 1]) * wv2[2 * lane + 1];
         s = wave_sum(s);
         if (lane == 0 && row < n) vout[row] = tanhf(s + net.b_v2[0]);
     }
+    TSTAMP(15);
 }
 
 // exp(log_softmax(x)) over the first 3226 columns; one wavefront per row
@@ -350,14 +486,14 @@ __global__ void k_softmax(const float* __restrict__ logits, float* __restrict__ 
 namespace yk {
 
 int launch_forward(const NetDev& net, const yk_state_t* states, const float* x, const int32_t* rows,
-                   const int32_t* count, int n, float* logits, float* v, hipStream_t stream) {
+                   const int32_t* count, int n, float* logits, float* v, hipStream_t stream, const uint8_t* active) {
     if (n <= 0) return YK_OK;
-    const dim3 grid((n + ROWS - 1) / ROWS), block(1024);
+    const dim3 grid((n + ROWS - 1) / ROWS), block(NTHR);
     switch (net.H) {
-        case 64: hipLaunchKernelGGL(k_forward<64>, grid, block, 0, stream, net, states, x, rows, count, n, logits, v); break;
-        case 128: hipLaunchKernelGGL(k_forward<128>, grid, block, 0, stream, net, states, x, rows, count, n, logits, v); break;
-        case 256: hipLaunchKernelGGL(k_forward<256>, grid, block, 0, stream, net, states, x, rows, count, n, logits, v); break;
-        case 512: hipLaunchKernelGGL(k_forward<512>, grid, block, 0, stream, net, states, x, rows, count, n, logits, v); break;
+        case 64: hipLaunchKernelGGL(k_forward<64>, grid, block, 0, stream, net, states, x, rows, count, n, logits, v, active); break;
+        case 128: hipLaunchKernelGGL(k_forward<128>, grid, block, 0, stream, net, states, x, rows, count, n, logits, v, active); break;
+        case 256: hipLaunchKernelGGL(k_forward<256>, grid, block, 0, stream, net, states, x, rows, count, n, logits, v, active); break;
+        case 512: hipLaunchKernelGGL(k_forward<512>, grid, block, 0, stream, net, states, x, rows, count, n, logits, v, active); break;
         default: return YK_ERR_ARG;
     }
     YK_LAUNCHED();
@@ -402,6 +538,7 @@ int yk_net_create(yk_net_t** out, int H, int NB, const float* const* p, int npar
     const size_t o_gpi = put(H), o_bepi = put(H), o_wpi = put((size_t)PI_LD * H), o_bpi = put(PI_LD);
     const size_t o_gv = put(H), o_bev = put(H), o_wv1 = put((size_t)128 * H), o_bv1 = put(128), o_wv2 = put(128),
                  o_bv2 = put(1);
+    const size_t o_vs = put(vstat_size(H)), o_vb = put((size_t)NB * 6 * H);
     int k = 0;
     auto cp = [&](size_t off, size_t n) { std::copy(p[k], p[k] + n, h.begin() + off); k++; };
     pack(o_win, p[k++], H, FEAT, H, 64);
@@ -418,6 +555,18 @@ int yk_net_create(yk_net_t** out, int H, int NB, const float* const* p, int npar
     cp(o_gv, H); cp(o_bev, H);
     pack(o_wv1, p[k++], 128, H, 128, H);
     cp(o_bv1, 128); cp(o_wv2, 128); cp(o_bv2, 1);
+    // LDS-staged copies of the vectors (yk_net.h): static set, then per block b1 g1 be1 b2 g2 be2
+    auto dup = [&](size_t dst, size_t src, size_t n) { std::copy(h.begin() + src, h.begin() + src + n, h.begin() + dst); };
+    dup(o_vs + VS_BIN * H, o_bin, H); dup(o_vs + VS_GIN * H, o_gin, H); dup(o_vs + VS_BEIN * H, o_bein, H);
+    dup(o_vs + VS_GPI * H, o_gpi, H); dup(o_vs + VS_BEPI * H, o_bepi, H);
+    dup(o_vs + VS_GV * H, o_gv, H); dup(o_vs + VS_BEV * H, o_bev, H);
+    dup(o_vs + VS_BV1 * H, o_bv1, 128); dup(o_vs + VS_BV1 * H + 128, o_wv2, 128);
+    dup(o_vs + vs_bpi(H), o_bpi, PI_LD);
+    for (int b = 0; b < NB; b++) {
+        const size_t d0 = o_vb + (size_t)b * 6 * H, v0 = (size_t)b * H;
+        dup(d0, o_b1 + v0, H); dup(d0 + H, o_g1 + v0, H); dup(d0 + 2 * H, o_be1 + v0, H);
+        dup(d0 + 3 * H, o_b2 + v0, H); dup(d0 + 4 * H, o_g2 + v0, H); dup(d0 + 5 * H, o_be2 + v0, H);
+    }
 
     yk_net* net = new yk_net();
     net->bytes = h.size() * sizeof(float);
@@ -438,6 +587,7 @@ int yk_net_create(yk_net_t** out, int H, int NB, const float* const* p, int npar
     d.w2 = B + o_w2; d.b2 = B + o_b2; d.g2 = B + o_g2; d.be2 = B + o_be2;
     d.g_pi = B + o_gpi; d.be_pi = B + o_bepi; d.w_pi = B + o_wpi; d.b_pi = B + o_bpi;
     d.g_v = B + o_gv; d.be_v = B + o_bev; d.w_v1 = B + o_wv1; d.b_v1 = B + o_bv1; d.w_v2 = B + o_wv2; d.b_v2 = B + o_bv2;
+    d.vstat = B + o_vs; d.vblk = B + o_vb;
     *out = net;
     return YK_OK;
 }
