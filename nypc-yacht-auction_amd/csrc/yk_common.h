@@ -242,14 +242,37 @@ __device__ __host__ inline int resolve_bids(YkS& s, Stream& rs) {
     return YK_ST_OK;
 }
 
+// WAVE: called by all 64 lanes of a wave together (wave-per-game kernels): lanes 0-9 draw
+// the ten dice (counters ctr .. ctr + 9) at once and three ballots assemble them - the same
+// values, in the same stream order, as the sequential path.
+template <bool WAVE = false>
 __device__ __host__ inline void new_round_rolls(YkS& s, Stream& rs) {
-    uint64_t ra = rs.roll5();
-    uint64_t rb = rs.roll5();
+    uint64_t ra = 0, rb = 0;
+#ifdef __HIP_DEVICE_COMPILE__
+    if constexpr (WAVE) {
+        const int lane = threadIdx.x & 63;
+        int die = 0;
+        if (lane < 10) die = 1 + (int)(((philox_draw(rs.seed, rs.env, rs.ctr + (uint64_t)lane) >> 32) * 6ull) >> 32);
+        const uint64_t b0 = __ballot(die & 1), b1 = __ballot(die & 2), b2 = __ballot(die & 4);
+#pragma unroll
+        for (int i = 0; i < 10; i++) {
+            const uint64_t dv = ((b0 >> i) & 1) | (((b1 >> i) & 1) << 1) | (((b2 >> i) & 1) << 2);
+            if (i < 5) ra |= dv << (4 * i);
+            else rb |= dv << (4 * (i - 5));
+        }
+        rs.ctr += 10;
+    } else
+#endif
+    {
+        ra = rs.roll5();
+        rb = rs.roll5();
+    }
     s.w[0] = (s.w[0] & ((1ull << 24) - 1)) | (1ull << 5) | (1ull << 6) | (ra << 24) | (rb << 44);
 }
 
 // getNextState  YachtGame.py:260-372, in place on a register copy (the reference copies,
 // :264).  Returns YK_ST_*.
+template <bool WAVE = false>
 __device__ __host__ inline int step_state(YkS& s, int player, int action, Stream& rs, int& next_player) {
     const int round = s_round(s), phase = s_phase(s);
     if (phase == 0 && round != 13) {
@@ -268,7 +291,7 @@ __device__ __host__ inline int step_state(YkS& s, int player, int action, Stream
             s.w[0] |= 1ull << 4;  // PHASE_SCORE, bids and stale rolls kept (:290-293)
         } else {
             s.w[0] = (s.w[0] & ~0xFull & ~(1ull << 4)) | 2ull | NO_BIDS;  // round 2, BID
-            new_round_rolls(s, rs);
+            new_round_rolls<WAVE>(s, rs);
         }
         next_player = 1;
         return YK_ST_OK;
@@ -327,7 +350,7 @@ __device__ __host__ inline int step_state(YkS& s, int player, int action, Stream
             const int nr = round + 1;
             s.w[0] = (s.w[0] & ~0xFull) | (uint64_t)nr | NO_BIDS;
             if (nr != 13) {
-                new_round_rolls(s, rs);
+                new_round_rolls<WAVE>(s, rs);
                 s.w[0] &= ~(1ull << 4);
             } else {
                 s.w[0] |= 1ull << 4;

@@ -279,6 +279,7 @@ __device__ __forceinline__ float wave_max(float v) {
     for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
     return v;
 }
+__device__ __forceinline__ float softmax_p(float x, float m, float lse) { return __expf(x - m - lse); }
 __device__ __forceinline__ float wave_sumf(float v) {
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -425,11 +426,21 @@ __global__ __launch_bounds__(256) void k_move_begin(EngDev d, int move, int exte
     }
 }
 
+// Diagnostic builds only (-DYK_SEL_TIMING, tools/diag_select.py): per-game s_memtime
+// accumulators of the descent's phases.
+#ifdef YK_SEL_TIMING
+__device__ unsigned long long g_sel[16384 * 8];
+#define SEL_T0(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define SEL_ACC(k, t0) \
+    if (lane == 0) g_sel[(long)e * 8 + (k)] += __builtin_amdgcn_s_memtime() - (t0)
+#else
+#define SEL_T0(v)
+#define SEL_ACC(k, t0)
+#endif
+
 // One simulation's descent (MCTS.search, MCTS.py:56-152 up to the recursion).
-__global__ __launch_bounds__(256) void k_select(EngDev d, const uint32_t* env_ids, uint64_t* ctr_arr) {
-    const int lane = threadIdx.x & 63;
-    const int e = blockIdx.x * GAMES_PER_BLOCK + (threadIdx.x >> 6);
-    if (e >= d.E) return;
+// All 64 lanes of the game's wave call it together.
+__device__ __forceinline__ void select_game(const EngDev& d, int e, int lane, const uint32_t* env_ids, uint64_t* ctr_arr) {
     if (d.done[e] || d.idle[e]) {
         if (lane == 0) {
             d.leaf_flag[e] = 0;
@@ -449,7 +460,9 @@ __global__ __launch_bounds__(256) void k_select(EngDev d, const uint32_t* env_id
     uint64_t scanned = 0;
     int leaf = 0;
     PyV res{0.0, T_INT};
+    SEL_T0(t_all);
     while (true) {
+        SEL_T0(t_lv);
         const double es = game_ended(s, 1);  // Es (MCTS.py:78-82)
         if (es != 0.0) {
             res = PyV{-es, T_F64};
@@ -457,6 +470,7 @@ __global__ __launch_bounds__(256) void k_select(EngDev d, const uint32_t* env_id
         }
         const uint64_t hsh = key_hash(s);
         const int nid = lookup(d, g, e, s, hsh);
+        SEL_ACC(0, t_lv);
         if (nid < 0) {  // leaf: predict (MCTS.py:84-115)
             leaf = 1;
             if (lane == 0) {
@@ -481,15 +495,30 @@ __global__ __launch_bounds__(256) void k_select(EngDev d, const uint32_t* env_id
             sq = (float)sqrt((double)Ns);
             sqe = (float)sqrt((double)Ns + 1e-8);
         }
+        SEL_T0(t_sc);
         const float* P = Pbase + nd.p_off;
         const uint16_t* S = Sbase + nd.p_off;
         float best = -INFINITY;
         int bj = 0x7FFFFFFF;
+        // software-pipelined scan: iteration it+1's P / slot loads fly while iteration it's
+        // visited-edge gathers resolve
+        float4 p4 = make_float4(0.f, 0.f, 0.f, 0.f);
+        ushort4 s4 = make_ushort4(0, 0, 0, 0);
+        if (lane * 4 < V) {
+            p4 = *reinterpret_cast<const float4*>(P + lane * 4);
+            s4 = *reinterpret_cast<const ushort4*>(S + lane * 4);
+        }
         for (int j0 = lane * 4; j0 < V; j0 += 256) {
-            const float4 p4 = *reinterpret_cast<const float4*>(P + j0);
-            const ushort4 s4 = *reinterpret_cast<const ushort4*>(S + j0);
             const float pv[4] = {p4.x, p4.y, p4.z, p4.w};
             const uint16_t sv[4] = {s4.x, s4.y, s4.z, s4.w};
+            Edge ev[4];
+#pragma unroll
+            for (int t = 0; t < 4; t++)
+                if (j0 + t < V && sv[t]) ev[t] = edges[sv[t] - 1];
+            if (j0 + 256 < V) {
+                p4 = *reinterpret_cast<const float4*>(P + j0 + 256);
+                s4 = *reinterpret_cast<const ushort4*>(S + j0 + 256);
+            }
 #pragma unroll
             for (int t = 0; t < 4; t++) {
                 const int j = j0 + t;
@@ -497,8 +526,7 @@ __global__ __launch_bounds__(256) void k_select(EngDev d, const uint32_t* env_id
                     float u;
                     const float cp = d.c32 * pv[t];
                     if (sv[t]) {
-                        const Edge ed = edges[sv[t] - 1];
-                        u = (float)ed.Q + (cp * sq) / (float)(ed.N + 1);
+                        u = (float)ev[t].Q + (cp * sq) / (float)(ev[t].N + 1);
                     } else {
                         u = cp * sqe;
                     }
@@ -519,6 +547,8 @@ __global__ __launch_bounds__(256) void k_select(EngDev d, const uint32_t* env_id
             }
         }
         scanned += (uint64_t)V;
+        SEL_ACC(1, t_sc);
+        SEL_T0(t_st);
         int j = bj;
         if (j == 0x7FFFFFFF) j = 0;  // MCTS.py:138-143: first valid action
         if (depth >= MAXD) {
@@ -531,14 +561,22 @@ __global__ __launch_bounds__(256) void k_select(EngDev d, const uint32_t* env_id
         const VInfo vi = unpack_vinfo(nd.vinfo, nd.nvalid);
         const int a = compact_to_action(vi, j);
         int np = 1;
-        const int st = step_state(s, 1, a, rs, np);  // MCTS.py:149
+        const int st = step_state<true>(s, 1, a, rs, np);  // MCTS.py:149 (all lanes: wave-parallel dice)
         if (st != YK_ST_OK) {
             if (lane == 0) atomicOr(d.err, ERR_STEP);
             res = PyV{0.0, T_INT};
             break;
         }
         s = canonical(s, np);  // MCTS.py:150
+        SEL_ACC(2, t_st);
+        if (lane == 0) {
+#ifdef YK_SEL_TIMING
+            g_sel[(long)e * 8 + 4] += 1;
+            g_sel[(long)e * 8 + 5] += (unsigned long long)V;
+#endif
+        }
     }
+    SEL_ACC(3, t_all);
     if (lane == 0) {
         d.leaf_flag[e] = (uint8_t)leaf;
         d.path_len[e] = (uint8_t)depth;
@@ -551,12 +589,31 @@ __global__ __launch_bounds__(256) void k_select(EngDev d, const uint32_t* env_id
     }
 }
 
-// Leaf expansion (MCTS.py:84-115) and backup (MCTS.py:154-164).  One wave per game.
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_expand_backup(EngDev d) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int e = blockIdx.x * GAMES_PER_BLOCK + w;
+__global__ __launch_bounds__(256) void k_select(EngDev d, const uint32_t* env_ids, uint64_t* ctr_arr) {
+    const int lane = threadIdx.x & 63;
+    const int e = blockIdx.x * GAMES_PER_BLOCK + (threadIdx.x >> 6);
+    if (e >= d.E) return;
+    select_game(d, e, lane, env_ids, ctr_arr);
+}
+
+// Leaf expansion (MCTS.py:84-115) and backup (MCTS.py:154-164) of this simulation, then -
+// when do_select - the next simulation's descent for the same game (one kernel boundary per
+// simulation fewer).  One wave per game.
+__device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int lane);
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_expand_backup(
+    EngDev d, int do_select, const uint32_t* env_ids, uint64_t* ctr_arr) {
+    const int lane = threadIdx.x & 63;
+    const int e = blockIdx.x * GAMES_PER_BLOCK + (threadIdx.x >> 6);
     if (e >= d.E) return;
     if (d.done[e]) return;
+    expand_backup_game(d, e, lane);
+    if (do_select) {
+        wave_sync();  // this wave's backup writes (edges, slots, Ns) precede its descent's reads
+        select_game(d, e, lane, env_ids, ctr_arr);
+    }
+}
+
+__device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int lane) {
     const int g = d.gen[e];
     PyV res{d.res_v[e], d.res_t[e]};
     if (d.leaf_flag[e]) {
@@ -592,23 +649,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
 #pragma unroll
             for (int r = 0; r < PW_TMAX; r++) m = fmaxf(m, qt[r]);
             m = wave_max(m);
+            // hardware exp (<= 2 ulp; the 1e-5 contract holds, tests/test_gpu_selfplay.py); the
+            // same softmax_p() produces the recorded prior, the pairwise sum and P below
             float se = 0.f;
 #pragma unroll
             for (int j = 0; j < PW_GMAX; j++)
-                se += (expf(q[j].x - m) + expf(q[j].y - m)) + (expf(q[j].z - m) + expf(q[j].w - m));
+                se += (__expf(q[j].x - m) + __expf(q[j].y - m)) + (__expf(q[j].z - m) + __expf(q[j].w - m));
 #pragma unroll
-            for (int r = 0; r < PW_TMAX; r++) se += expf(qt[r] - m);
-            lse = logf(wave_sumf(se));
+            for (int r = 0; r < PW_TMAX; r++) se += __expf(qt[r] - m);
+            lse = __logf(wave_sumf(se));
             mx = m;
 #pragma unroll
             for (int j = 0; j < PW_GMAX; j++) {
-                q[j].x = expf(q[j].x - m - lse);
-                q[j].y = expf(q[j].y - m - lse);
-                q[j].z = expf(q[j].z - m - lse);
-                q[j].w = expf(q[j].w - m - lse);
+                q[j].x = softmax_p(q[j].x, m, lse);
+                q[j].y = softmax_p(q[j].y, m, lse);
+                q[j].z = softmax_p(q[j].z, m, lse);
+                q[j].w = softmax_p(q[j].w, m, lse);
             }
 #pragma unroll
-            for (int r = 0; r < PW_TMAX; r++) qt[r] = expf(qt[r] - m - lse);
+            for (int r = 0; r < PW_TMAX; r++) qt[r] = softmax_p(qt[r], m, lse);
             v = d.vpred[e];
         } else {
 #pragma unroll
@@ -690,16 +749,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
             // P over the compact valid set (ascending action): Ps / sum, or the uniform fallback
             // (MCTS.py:90-107).  Written in compact order (coalesced), recomputing each prior
             // exactly as above from the L2-resident logits row (or the hash).
-            const float* xr = d.logits + (long)e * PI_LD;
-            for (int j = lane; j < VP; j += 64) {
-                float p = 0.0f;
-                if (j < V) {
-                    const int a = compact_to_action(vi, j);
-                    const float pa = d.prior == 0 ? expf(xr[a] - mx - lse) : hash_prior_pi(hsh, a);
-                    p = sum > 0.0f ? pa / sum : inv_fallback;
+            const float* __restrict__ xr = d.logits + (long)e * PI_LD;
+            for (int j0 = lane; j0 < VP; j0 += 256) {  // four gathers in flight per lane
+                float xa[4];
+                int aa[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const int j = j0 + 64 * u;
+                    aa[u] = j < V ? compact_to_action(vi, j) : 0;
+                    xa[u] = (d.prior == 0 && j < V) ? xr[aa[u]] : 0.f;
                 }
-                P[j] = p;
-                S[j] = 0;
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const int j = j0 + 64 * u;
+                    if (j < VP) {
+                        float p = 0.0f;
+                        if (j < V) {
+                            const float pa = d.prior == 0 ? softmax_p(xa[u], mx, lse) : hash_prior_pi(hsh, aa[u]);
+                            p = sum > 0.0f ? pa / sum : inv_fallback;
+                        }
+                        P[j] = p;
+                        S[j] = 0;
+                    }
+                }
             }
             if (lane == 0) {
                 NodeRec r;
@@ -1024,10 +1096,11 @@ int check_errors(yk_engine* eng, hipStream_t s) {
 int run_sims(yk_engine* eng, int sims, const uint32_t* env_ids, uint64_t* ctr, hipStream_t s) {
     EngDev& d = eng->d;
     const dim3 gb((d.E + GAMES_PER_BLOCK - 1) / GAMES_PER_BLOCK), bb(256);
+    if (sims <= 0) return YK_OK;
+    prof_mark(eng, KC_SELECT, s);  // the first descent; later ones run in k_expand_backup's tail
+    hipLaunchKernelGGL(k_select, gb, bb, 0, s, d, env_ids, ctr);
+    YK_LAUNCHED();
     for (int k = 0; k < sims; k++) {
-        prof_mark(eng, KC_SELECT, s);
-        hipLaunchKernelGGL(k_select, gb, bb, 0, s, d, env_ids, ctr);
-        YK_LAUNCHED();
         if (d.prior == 0) {
             prof_mark(eng, KC_FORWARD, s);
             // predict row = game: no compaction; workgroups without a leaf exit at once
@@ -1036,7 +1109,7 @@ int run_sims(yk_engine* eng, int sims, const uint32_t* env_ids, uint64_t* ctr, h
             if (rc) return rc;
         }
         prof_mark(eng, KC_EXPAND, s);
-        hipLaunchKernelGGL(k_expand_backup, gb, bb, 0, s, d);
+        hipLaunchKernelGGL(k_expand_backup, gb, bb, 0, s, d, k + 1 < sims ? 1 : 0, env_ids, ctr);
         YK_LAUNCHED();
     }
     prof_mark(eng, -1, s);
@@ -1045,6 +1118,16 @@ int run_sims(yk_engine* eng, int sims, const uint32_t* env_ids, uint64_t* ctr, h
 }  // namespace
 
 extern "C" {
+
+#ifdef YK_SEL_TIMING
+int yk_diag_select(uint64_t* out, int n) {  // HOST out[n][8]; resets the accumulators
+    YK_HIP(hipDeviceSynchronize());
+    YK_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sel), sizeof(uint64_t) * 8 * (size_t)n));
+    std::vector<uint64_t> z((size_t)8 * n, 0);
+    YK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_sel), z.data(), sizeof(uint64_t) * z.size()));
+    return YK_OK;
+}
+#endif
 
 int yk_engine_create(yk_engine_t** out, const yk_engine_config_t* cfg, yk_net_t* net) {
     if (!out || !cfg) return YK_ERR_ARG;

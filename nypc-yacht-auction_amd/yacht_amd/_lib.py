@@ -12,7 +12,8 @@ import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.dirname(HERE)
-LIB_PATH = os.path.join(HERE, "libyacht_hip.so")
+# YK_LIB_PATH: diagnostic builds only (tools/diag_select.py); the product loads the in-tree library
+LIB_PATH = os.environ.get("YK_LIB_PATH") or os.path.join(HERE, "libyacht_hip.so")
 
 YK_OK, YK_ERR_ARG, YK_ERR_HIP, YK_ERR_NOMEM, YK_ERR_CAPACITY, YK_ERR_STATE = 0, -1, -2, -3, -4, -5
 _ERR_NAMES = {YK_ERR_ARG: "bad argument", YK_ERR_HIP: "HIP error", YK_ERR_NOMEM: "out of device memory",

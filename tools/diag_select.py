@@ -1,0 +1,37 @@
+"""Diagnostic: where k_select's time goes (needs the -DYK_SEL_TIMING library, tools/diag_select.sh)."""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "nypc-yacht-auction_amd"))
+from yacht_amd._lib import lib  # noqa: E402
+from yacht_amd.engine import SelfPlayEngine  # noqa: E402
+from yacht_amd.nnet import YachtNNet, YkNet  # noqa: E402
+
+E, sims = int(sys.argv[1]) if len(sys.argv) > 1 else 4096, 100
+torch.manual_seed(0)
+net = YkNet(YachtNNet(hidden=256, nblocks=6).state_dict(), 256, 6)
+eng = SelfPlayEngine(E, sims, 1.5, 15, net=net, max_moves=64)
+L = lib()
+L.yk_diag_select.argtypes = [C.c_void_p, C.c_int]
+out = np.zeros((E, 8), dtype=np.uint64)
+eng.run(0, 0)
+L.yk_diag_select(out.ctypes.data, E)  # discard the warm-up
+eng.profile(True)
+eng.run(1, 0)
+L.yk_diag_select(out.ctypes.data, E)
+kt = eng.kernel_times()
+st = eng.stats()
+lv = out[:, 4].sum()
+tot = out[:, 3].astype(np.float64)
+print(f"select kernel: {kt['select'][0] / kt['select'][1] * 1e3:.1f} us avg over {kt['select'][1]} launches")
+print(f"levels per game-sim: {lv / (E * st['sims']):.2f}; valid entries scanned per level: {out[:, 5].sum() / lv:.0f}")
+names = ["lookup (ended+hash+probe)", "UCB scan + argmax", "step + canonical", "whole descent"]
+per = tot.sum()
+for k, nm in enumerate(names):
+    c = out[:, k].astype(np.float64).sum()
+    print(f"  {nm:28s} {c / (E * st['sims']):9.0f} cycles per game-sim  ({100 * c / per:5.1f}% of descent)")
+print(f"  max descent per game-sim    {tot.max() / st['sims']:9.0f}")
