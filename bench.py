@@ -59,6 +59,20 @@ def cpu_baseline(state_dict, sims, seconds_target=15.0, threads=None):
                       f"same net), {exps} expansions in {dt:.1f}s"}
 
 
+def measured_traffic(args):
+    """HBM bytes per k_forward launch from the committed rocprofv3 PMC passes of this exact
+    configuration (profiles/*_forward_traffic.json, tools/profile_bench.sh); None otherwise."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_forward_traffic.json"))):
+        with open(f) as fh:
+            t = json.load(fh)
+        c = t.get("config", {})
+        if (c.get("envs"), c.get("sims"), c.get("hidden"), c.get("nblocks")) == (args.envs, args.sims, H, NB):
+            best = (t["hbm_bytes_per_launch"], os.path.relpath(f, REPO))
+    return best
+
+
 def arena_leg(net, games=1000, sims=25, seed=0, reps=3):
     """Config 4: Arena.playGames(1000) of MCTS(temp 0, 25 sims) vs the uniform-random player,
     one lock-step device batch (agent seat 1 for the first half, -1 for the second)."""
@@ -205,9 +219,11 @@ def main():
             exp_per_launch = exps / world / max(per["forward"][1], 1)
             flop = PREDICT_FLOP * exp_per_launch
             ach = flop / (per[dom][0] * 1e-3) / 1e12
+            tr = measured_traffic(args)  # per-GPU configuration, so per-launch bytes hold at any N
             out["roofline"] = {"kernel": "k_forward", "bound": "mfma", "achieved": ach,
                                "peak": F32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": ach / F32_MFMA_PEAK_TFLOPS,
-                               "traffic": None,
+                               "traffic": tr[0] if tr else None,
+                               "traffic_source": tr[1] if tr else None,
                                "work_per_launch": f"{exp_per_launch:.0f} expansions x {PREDICT_FLOP} FLOP (f32)"}
         else:
             # env/MCTS kernels: algorithmic bytes = 4*S_scan + 16*D + 4*V_new + 364 per expansion

@@ -140,8 +140,9 @@ int yk_engine_destroy(yk_engine_t* eng);
 int yk_selfplay(yk_engine_t* eng, uint64_t seed, uint32_t env_base, void* stream);
 /* Per-kernel timing with HIP events on the engine's stream (adds an event pair around each
  * launch while enabled; resets the accumulators).  yk_engine_kernel_times: HOST ms[8],
- * launches[8] for classes 0 select, 1 forward (all predict layers), 2 leaf-row scan, 3 expand+backup,
- * 4 move begin (root / tree compaction), 5 move end (policy, sampling, real step). */
+ * launches[8] for classes 0 first descent of a move, 1 forward (the whole predict), 2 unused,
+ * 3 expand + backup + the next descent, 4 move begin (root / tree compaction), 5 move end
+ * (policy, sampling, real step). */
 int yk_engine_profile(yk_engine_t* eng, int enable);
 int yk_engine_kernel_times(yk_engine_t* eng, double* ms, int64_t* launches);
 /* HOST out[16]: 0 expansions, 1 valid entries scanned by UCB, 2 real moves (max over games),

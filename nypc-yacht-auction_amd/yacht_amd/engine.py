@@ -75,7 +75,8 @@ class SelfPlayEngine:
              actions.ctypes.data, final.ctypes.data, ctr.ctypes.data)
         return dict(result=result, totals=totals, n_moves=nm, actions=actions, final=final, ctr=ctr)
 
-    KERNEL_CLASSES = ("select", "forward", "leaf_scan", "expand_backup", "move_begin", "move_end")
+    # class 0: the first descent of each move; class 3: expand + backup + the next descent
+    KERNEL_CLASSES = ("select", "forward", "unused", "expand_backup_select", "move_begin", "move_end")
 
     def profile(self, enable: bool = True):
         call("yk_engine_profile", self.handle, int(enable))
@@ -84,7 +85,7 @@ class SelfPlayEngine:
         ms = np.zeros(8, dtype=np.float64)
         n = np.zeros(8, dtype=np.int64)
         call("yk_engine_kernel_times", self.handle, ms.ctypes.data, n.ctypes.data)
-        return {k: (float(ms[i]), int(n[i])) for i, k in enumerate(self.KERNEL_CLASSES)}
+        return {k: (float(ms[i]), int(n[i])) for i, k in enumerate(self.KERNEL_CLASSES) if k != "unused"}
 
     STAT_NAMES = ("expansions", "scanned", "moves", "errors", "max_nodes", "max_edges", "max_arena", "vnew",
                   "path_edges", "sims", "node_cap", "edge_cap", "arena_cap", "visit_cap")
