@@ -49,11 +49,13 @@ def lib():
                                      C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                      C.c_void_p, C.c_void_p, C.c_int]
         _lib.or_arena.restype = C.c_int
-        _lib.or_arena.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_int, C.c_double, C.c_int, C.c_int,
+        _lib.or_arena.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_uint64, C.c_int, C.c_double,
+                                  C.c_int, C.c_int,
                                   C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                   C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
         for name in ("or_step", "or_valid", "or_ended", "or_canonical", "or_featurize", "or_score_table",
-                     "or_score_dice", "or_key_hash_batch", "or_hash_prior", "or_init_board", "or_draws"):
+                     "or_score_dice", "or_key_hash_batch", "or_hash_prior", "or_init_board", "or_draws",
+                     "or_greedy_heuristic", "or_greedy_play"):
             getattr(_lib, name).restype = None
     return _lib
 
@@ -196,6 +198,28 @@ class Net:
 
 
 MODE_HASH, MODE_MLP, MODE_REPLAY = 0, 1, 2
+PLAYERS = {"mcts": 0, "random": 1, "greedy": 2}
+
+
+def greedy_play(states, seed, envs, ctr=0):
+    """GreedyYachtPlayer.play (YachtPlayers.py:199-214) per state, drawing any fallback from the
+    state's stream; returns (actions, counters after)."""
+    w = _w(states)
+    n = len(w)
+    e = np.ascontiguousarray(np.broadcast_to(np.asarray(envs, dtype=np.uint32), (n,)))
+    c = np.ascontiguousarray(np.broadcast_to(np.asarray(ctr, dtype=np.uint64), (n,))).copy()
+    out = np.zeros(n, dtype=np.int32)
+    lib().or_greedy_play(_p(w), C.c_uint64(seed), _p(e), _p(c), _p(out), C.c_int(n))
+    return out, c
+
+
+def greedy_heuristic(states):
+    """GreedyYachtPlayer's heuristic action for canonical boards (-1: it would fall back to a
+    random legal action)."""
+    w = _w(states)
+    out = np.zeros(len(w), dtype=np.int32)
+    lib().or_greedy_heuristic(_p(w), _p(out), C.c_int(len(w)))
+    return out
 
 
 def _replay_ptrs(replay, keep):
@@ -236,8 +260,9 @@ def selfplay(envs, seed, sims, cpuct=1.5, temp_threshold=15, mode=MODE_HASH, net
 
 
 def arena(envs, agent_seat, seed, sims, cpuct=1.5, mode=MODE_HASH, net=None, replay=None, max_moves=64,
-          threads=1):
-    """Arena.playGame (Arena.py:30-93), MCTS agent (temp 0) in seat agent_seat[i] vs RandomYachtPlayer.
+          threads=1, agent="mcts", opponent="random"):
+    """Arena.playGame (Arena.py:30-93): `agent` in seat agent_seat[i] vs `opponent`, each one of
+    mcts (temp 0, fresh tree per game), random (RandomYachtPlayer), greedy (GreedyYachtPlayer).
     replay as in selfplay (MODE_REPLAY)."""
     e = np.ascontiguousarray(np.asarray(envs, dtype=np.uint32).reshape(-1))
     n = len(e)
@@ -251,7 +276,8 @@ def arena(envs, agent_seat, seed, sims, cpuct=1.5, mode=MODE_HASH, net=None, rep
     rpi = rv = rn = None
     if mode == MODE_REPLAY:
         rpi, rv, rn = _replay_ptrs(replay, keep)
-    nerr = lib().or_arena(n, _p(e), _p(seat), C.c_uint64(seed), sims, C.c_double(cpuct), max_moves, mode,
+    nerr = lib().or_arena(n, _p(e), _p(seat), PLAYERS[agent], PLAYERS[opponent], C.c_uint64(seed), sims,
+                          C.c_double(cpuct), max_moves, mode,
                           C.c_void_p(net.h if net is not None else None), rpi, rv, rn, _p(result), _p(totals), _p(actions),
                           _p(stats), _p(final), threads)
     return dict(result=result, totals=totals, actions=actions, stats=stats, final=final, nerr=nerr)

@@ -836,13 +836,140 @@ static int run_episode(const ep_cfg_t* cfg, pred_t* pr, uint64_t seed, uint32_t 
     return err;
 }
 
+/* ------------------------------------------------------------------ GreedyYachtPlayer */
+/* YachtPlayers.py:38-171, 186-214 on a canonical board.  Points are the game's units (x1000). */
+#define BASIC_BONUS 35000
+#define BASIC_BONUS_THRESHOLD 63000
+static int basic_sum(const pl_t* q) {
+    int b = 0;
+    for (int c = 0; c < 6; c++) b += q->cat[c];
+    return b;
+}
+/* best immediate gain (score + basic bonus when it crosses the threshold) over unused
+ * categories x combos of `dice`; the scorer walks combos in order and stops at the first one
+ * reaching past the carry (YachtPlayers.py:151-153); the bid potential filters max(comb) < n
+ * (:67) - identical for carries of 0, 5 and 10 dice.  *best_action = first maximum. */
+static int greedy_best(const pl_t* me, const int* dice, int n, int stop_at_first_invalid, int* best_action) {
+    const int basic_before = basic_sum(me);
+    int best = INT32_MIN, ba = -1;
+    for (int c = 0; c < NCAT; c++) {
+        if ((me->used >> c) & 1) continue;
+        for (int ci = 0; ci < NCOMB; ci++) {
+            if (COMB[ci][4] >= n) {
+                if (stop_at_first_invalid) break;
+                continue;
+            }
+            int chosen[5];
+            for (int k = 0; k < 5; k++) chosen[k] = dice[COMB[ci][k]];
+            const int sc = or_score_category(c, chosen);
+            int gain = sc;
+            if (c < 6 && basic_before < BASIC_BONUS_THRESHOLD && BASIC_BONUS_THRESHOLD <= basic_before + sc)
+                gain += BASIC_BONUS;
+            if (gain > best) { best = gain; ba = NBID + c * NCOMB + ci; }
+        }
+    }
+    if (best_action) *best_action = ba;
+    return best;
+}
+/* _score_potential_after_bid  YachtPlayers.py:38-87 */
+static int greedy_potential(const st_t* s, const pl_t* me, const int* bundle) {
+    int dice[15], n = 0;
+    for (int i = 0; i < me->n; i++) dice[n++] = me->d[i];
+    for (int i = 0; i < 5; i++) dice[n++] = bundle[i];
+    if (s->round == 1) {
+        int sum = 0, counts[7] = {0}, mx = 0;
+        for (int i = 0; i < n; i++) { sum += dice[i]; counts[dice[i]]++; }
+        int v = 1000 * sum;
+        for (int f = 1; f <= 6; f++) if (counts[f] > mx) mx = counts[f];
+        if (mx >= 4) v += 6000;
+        else if (mx == 3) v += 3000;
+        const int e1 = counts[1] > 0, e2 = counts[2] > 0, e3 = counts[3] > 0, e4 = counts[4] > 0,
+                  e5 = counts[5] > 0, e6 = counts[6] > 0;
+        if ((e1 && e2 && e3 && e4) || (e2 && e3 && e4 && e5) || (e3 && e4 && e5 && e6)) v += 5000;
+        return v;
+    }
+    if (n < 5) return 0;
+    const int best = greedy_best(me, dice, n, 0, NULL);
+    return best == INT32_MIN ? 0 : best;
+}
+static int total_bb(const pl_t* q) {
+    int all = 0;
+    for (int c = 0; c < NCAT; c++) all += q->cat[c];
+    return q->bid + all + (basic_sum(q) >= BASIC_BONUS_THRESHOLD ? BASIC_BONUS : 0);
+}
+/* _choose_bid  YachtPlayers.py:90-127: the action may encode past index 100 (bids up to 100,000) */
+static int greedy_choose_bid(const st_t* s) {
+    const pl_t* me = &s->p[0];
+    const int valA = greedy_potential(s, me, s->A), valB = greedy_potential(s, me, s->B);
+    int target, gap;
+    if (valA >= valB) { target = 0; gap = valA - valB > 0 ? valA - valB : 0; }
+    else { target = 1; gap = valB - valA > 0 ? valB - valA : 0; }
+    const int diff = total_bb(me) - total_bb(&s->p[1]);
+    const double bid_k = 0.5 * ((double)gap / 1000.0) - 0.15 * ((double)diff / 1000.0);
+    double r = nearbyint(1000.0 * bid_k);  /* python round(): half to even */
+    long bid = (long)r;
+    if (bid > 100000) bid = 100000;
+    if (bid < 0) bid = 0;
+    bid = (bid / 500) * 500;
+    return target * BID_LEVELS + (int)(bid / 500);
+}
+/* _choose_scoring  YachtPlayers.py:131-171 */
+static int greedy_choose_scoring(const st_t* s) {
+    const pl_t* me = &s->p[0];
+    if (me->n < 5) return 0;
+    int ba = -1;
+    greedy_best(me, me->d, me->n, 1, &ba);
+    return ba >= 0 ? ba : 0;
+}
+/* GreedyYachtPlayer.play  YachtPlayers.py:199-214: the heuristic's action if valid, else
+ * np.random.choice(legal) (one below(n) draw), else 0 */
+static int greedy_action(const st_t* s, uint8_t* valid, stream_t* rs) {
+    const int nv = valid_moves(s, 1, valid);
+    const int a = (s->phase == 0 && s->round != 13) ? greedy_choose_bid(s) : greedy_choose_scoring(s);
+    if (a >= 0 && a < ASIZE && valid[a]) return a;
+    if (nv == 0) return 0;
+    int pick = st_below(rs, nv);
+    for (int b = 0; b < ASIZE; b++) if (valid[b] && pick-- == 0) return b;
+    return 0;
+}
+/* the heuristic alone (for fixtures / the device kernel): -1 when the player would fall back */
+void or_greedy_heuristic(const uint64_t* states, int32_t* actions, int n) {
+    init_comb();
+    uint8_t* valid = (uint8_t*)malloc(ASIZE);
+    for (int i = 0; i < n; i++) {
+        st_t s;
+        unpack(states + 8 * i, &s);
+        valid_moves(&s, 1, valid);
+        const int a = (s.phase == 0 && s.round != 13) ? greedy_choose_bid(&s) : greedy_choose_scoring(&s);
+        actions[i] = (a >= 0 && a < ASIZE && valid[a]) ? a : -1;
+    }
+    free(valid);
+}
+
+/* GreedyYachtPlayer.play with each state's stream (seed, envs[i], ctr[i]); ctr advanced */
+void or_greedy_play(const uint64_t* states, uint64_t seed, const uint32_t* envs, uint64_t* ctr, int32_t* actions,
+                    int n) {
+    init_comb();
+    uint8_t* valid = (uint8_t*)malloc(ASIZE);
+    for (int i = 0; i < n; i++) {
+        st_t s;
+        unpack(states + 8 * i, &s);
+        stream_t rs = {seed, envs[i], ctr[i]};
+        actions[i] = greedy_action(&s, valid, &rs);
+        ctr[i] = rs.ctr;
+    }
+    free(valid);
+}
+
 /* ------------------------------------------------------------------ Arena.playGame (agent vs random) */
 /* Arena.py:30-93 with player1/player2 = {MCTS agent: np.argmax(mcts.getActionProb(x, temp=0))
  * (Coach.py:124-125), RandomYachtPlayer.play (YachtPlayers.py:174-183)}.  The agent keeps one
  * MCTS tree for the whole game.  out: result = curPlayer * getGameEnded (Arena.py:93),
  * totals, moves, actions[max_moves], final state, stream counter. */
-static int run_arena(const ep_cfg_t* cfg, pred_t* pr, uint64_t seed, uint32_t env, int agent_seat, double* result,
-                     int32_t* totals, int32_t* actions, int64_t* stats, uint64_t* final_state) {
+enum { PK_MCTS = 0, PK_RANDOM = 1, PK_GREEDY = 2 };
+static int run_arena(const ep_cfg_t* cfg, pred_t* pr, uint64_t seed, uint32_t env, int agent_seat, int agent_kind,
+                     int opp_kind, double* result, int32_t* totals, int32_t* actions, int64_t* stats,
+                     uint64_t* final_state) {
     init_comb();
     stream_t rs = {seed, env, 0};
     mcts_t m;
@@ -861,7 +988,8 @@ static int run_arena(const ep_cfg_t* cfg, pred_t* pr, uint64_t seed, uint32_t en
         st_t canon;
         canonical(&board, cur, &canon);
         int action = 0;
-        if (cur == agent_seat) {
+        const int kind = cur == agent_seat ? agent_kind : opp_kind;
+        if (kind == PK_MCTS) {
             for (int i = 0; i < cfg->sims; i++) search(&m, &canon);
             if (m.error || pr->error) { err = m.error ? m.error : 2; break; }
             uint64_t key[8];
@@ -879,6 +1007,8 @@ static int run_arena(const ep_cfg_t* cfg, pred_t* pr, uint64_t seed, uint32_t en
                 int c = (nd && nd->eidx && nd->eidx[a] >= 0) ? nd->e[nd->eidx[a]].N : 0;
                 if (c == mx && pick-- == 0) { action = a; break; }
             }
+        } else if (kind == PK_GREEDY) {
+            action = greedy_action(&canon, valid, &rs);
         } else {
             int nv = valid_moves(&canon, 1, valid);
             if (nv > 0) {
@@ -1040,8 +1170,8 @@ int or_selfplay(int n, const uint32_t* envs, uint64_t seed, int sims, double cpu
     return nerr;
 }
 
-int or_arena(int n, const uint32_t* envs, const int32_t* agent_seat, uint64_t seed, int sims, double cpuct,
-             int max_moves, int mode, void* net, const float* const* rpi, const float* const* rv,
+int or_arena(int n, const uint32_t* envs, const int32_t* agent_seat, int agent_kind, int opp_kind, uint64_t seed,
+             int sims, double cpuct, int max_moves, int mode, void* net, const float* const* rpi, const float* const* rv,
              const int64_t* rn, double* result, int32_t* totals, int32_t* actions, int64_t* stats,
              uint64_t* final_state, int threads) {
     init_comb();
@@ -1054,7 +1184,7 @@ int or_arena(int n, const uint32_t* envs, const int32_t* agent_seat, uint64_t se
         pr.mode = mode;
         pr.net = (const net_t*)net;
         if (mode == 2) { pr.rpi = rpi[i]; pr.rv = rv[i]; pr.rn = rn[i]; }
-        if (run_arena(&cfg, &pr, seed, envs[i], agent_seat[i], result + i, totals + 2 * i,
+        if (run_arena(&cfg, &pr, seed, envs[i], agent_seat[i], agent_kind, opp_kind, result + i, totals + 2 * i,
                       actions ? actions + (size_t)max_moves * i : NULL, stats ? stats + 8 * i : NULL,
                       final_state ? final_state + 8 * i : NULL))
             nerr++;

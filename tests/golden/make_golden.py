@@ -300,20 +300,28 @@ def run_episode(seed, env, sims, cpuct=1.5, temp_threshold=15):
                 expansions=nnet.calls, nodes=len(mcts.Es), seconds=dt)
 
 
-def run_arena_game(seed, env, sims, agent_seat, cpuct=1.5):
-    """One reference Arena.playGame (Arena.py:30-93): MCTS agent (np.argmax(getActionProb(x, temp=0)),
-    Coach.py:124-125) in seat agent_seat vs RandomYachtPlayer (YachtPlayers.py:174-183), fresh tree."""
+def run_arena_game(seed, env, sims, agent_seat, cpuct=1.5, agent_kind="mcts", opp_kind="random"):
+    """One reference Arena.playGame (Arena.py:30-93): `agent_kind` in seat agent_seat vs `opp_kind`,
+    each the MCTS agent (np.argmax(getActionProb(x, temp=0)), Coach.py:124-125, fresh tree),
+    RandomYachtPlayer or GreedyYachtPlayer (YachtPlayers.py:174-214)."""
     from utils import dotdict
     from Arena import Arena
     from MCTS import MCTS
-    from yacht.YachtPlayers import RandomYachtPlayer
+    from yacht.YachtPlayers import GreedyYachtPlayer, RandomYachtPlayer
     game = YachtGame()
     args = dotdict(dict(numMCTSSims=sims, cpuct=cpuct))
     set_stream(seed, env)
     nnet = HashNet(game)
     mcts = MCTS(game, nnet, args)
-    agent = lambda x: int(np.argmax(mcts.getActionProb(x, temp=0)))  # noqa: E731
-    rnd = RandomYachtPlayer(game).play
+
+    def make(kind):
+        if kind == "mcts":
+            return lambda x: int(np.argmax(mcts.getActionProb(x, temp=0)))
+        if kind == "greedy":
+            return GreedyYachtPlayer(game).play
+        return RandomYachtPlayer(game).play
+    agent = make(agent_kind)
+    rnd = make(opp_kind)
     actions = []
     in_search = [False]
     orig_gap = mcts.getActionProb
@@ -342,11 +350,11 @@ def run_arena_game(seed, env, sims, agent_seat, cpuct=1.5):
                 expansions=nnet.calls)
 
 
-def make_arena(seed=777, n=12, sims=10):
+def make_arena(seed=777, n=12, sims=10, agent_kind="mcts", opp_kind="random", env0=500):
     rows = []
     for i in range(n):
         seat = 1 if i < n // 2 else -1
-        g = run_arena_game(seed, 500 + i, sims, seat)
+        g = run_arena_game(seed, env0 + i, sims, seat, agent_kind=agent_kind, opp_kind=opp_kind)
         rows.append(g)
     M = max(len(g["actions"]) for g in rows)
     acts = np.full((n, M), -1, dtype=np.int32)
@@ -358,6 +366,39 @@ def make_arena(seed=777, n=12, sims=10):
                 n_moves=np.array([len(g["actions"]) for g in rows], dtype=np.int32),
                 ctr_end=np.array([g["ctr_end"] for g in rows], dtype=np.int64),
                 expansions=np.array([g["expansions"] for g in rows], dtype=np.int64))
+
+
+def to_ref_state(w):
+    """8 x u64 -> the reference's YachtState (fields per YachtGame.py:115-147)."""
+    d = spec.unpack_words(w)
+    ps = {k: PlayerState(carry=list(d[k]["carry"]), used_mask=d[k]["used_mask"],
+                         cat_scores=list(d[k]["cat_scores"]), bid_score=d[k]["bid_score"]) for k in ("p1", "p2")}
+    return YachtState(round_no=d["round_no"], phase=d["phase"], rollA=list(d["rollA"]), rollB=list(d["rollB"]),
+                      p1_bid=d["p1_bid"], p2_bid=d["p2_bid"], p1=ps["p1"], p2=ps["p2"])
+
+
+def make_greedy(seed=31):
+    """GreedyYachtPlayer.play (YachtPlayers.py:199-214) on every fixture state, each with its own
+    stream (env = index) so a random-legal fallback is recorded as a draw."""
+    from yacht.YachtPlayers import GreedyYachtPlayer
+    st = np.load(os.path.join(HERE, "states.npz"))["states"]
+    game = YachtGame()
+    player = GreedyYachtPlayer(game)
+    acts, drew = [], []
+    for i, w in enumerate(st):
+        set_stream(seed, i)
+        acts.append(player.play(to_ref_state(w)))
+        drew.append(_STREAM[0].ctr)
+    return dict(seed=np.uint64(seed), states=st, action=np.array(acts, dtype=np.int32),
+                draws=np.array(drew, dtype=np.int32))
+
+
+def make_players():
+    np.savez_compressed(os.path.join(HERE, "greedy.npz"), **make_greedy())
+    np.savez_compressed(os.path.join(HERE, "arena_greedy_random.npz"),
+                        **make_arena(seed=778, n=12, sims=1, agent_kind="greedy", opp_kind="random", env0=600))
+    np.savez_compressed(os.path.join(HERE, "arena_mcts_greedy.npz"),
+                        **make_arena(seed=779, n=8, sims=8, agent_kind="mcts", opp_kind="greedy", env0=700))
 
 
 def pack_episodes(eps):
@@ -394,6 +435,7 @@ def main():
     t0 = time.time()
     if len(sys.argv) > 1 and sys.argv[1] == "arena":
         np.savez_compressed(os.path.join(HERE, "arena_hash.npz"), **make_arena())
+        make_players()
         print(f"arena fixtures in {time.time() - t0:.1f}s")
         return
     dice, table = make_score_table()
@@ -422,6 +464,7 @@ def main():
               f"{ep['nodes']} nodes, {ep['seconds']:.1f}s")
     np.savez_compressed(os.path.join(HERE, "episodes_hash.npz"), **pack_episodes(eps))
     np.savez_compressed(os.path.join(HERE, "arena_hash.npz"), **make_arena())
+    make_players()
     print(f"done in {time.time() - t0:.1f}s")
 
 

@@ -148,3 +148,33 @@ def test_arena_hash_prior_matches_reference(golden):
     assert np.array_equal(r["stats"][:, 4], g["ctr_end"])
     for i, n in enumerate(g["n_moves"]):
         assert np.array_equal(r["actions"][i, :n], g["actions"][i, :n])
+
+
+def test_greedy_player_matches_reference(golden):
+    """GreedyYachtPlayer.play (YachtPlayers.py:186-214) on all 11,403 fixture states: bid
+    heuristic (float64, round-half-even, index overflow past 100), greedy scorer, and the
+    random-legal fallback drawn from the state's stream."""
+    g = golden("greedy.npz")
+    n = len(g["action"])
+    acts, ctr = O.greedy_play(g["states"], int(g["seed"]), np.arange(n), 0)
+    assert np.array_equal(acts, g["action"])
+    assert np.array_equal(ctr, g["draws"].astype(np.uint64))
+    # the heuristic alone: the played action, or -1 where play fell back (a draw, or no legal move)
+    h = O.greedy_heuristic(g["states"])
+    drew = g["draws"] > 0
+    _, counts = O.valid(g["states"], np.ones(n, dtype=np.int32))
+    assert ((h == g["action"]) | (h == -1)).all()
+    assert (h[drew] == -1).all() and (h[(counts == 0)] == -1).all()
+    assert ((h != -1) | drew | (counts == 0)).all()
+
+
+@pytest.mark.parametrize("fixture,agent,opponent", [("arena_greedy_random.npz", "greedy", "random"),
+                                                     ("arena_mcts_greedy.npz", "mcts", "greedy")])
+def test_arena_player_pairings_match_reference(golden, fixture, agent, opponent):
+    g = golden(fixture)
+    r = O.arena(g["env"], g["seat"], int(g["seed"]), int(g["sims"]), agent=agent, opponent=opponent)
+    assert r["nerr"] == 0
+    assert np.array_equal(r["result"], g["result"])
+    assert np.array_equal(r["stats"][:, 4], g["ctr_end"])
+    for i, n in enumerate(g["n_moves"]):
+        assert np.array_equal(r["actions"][i, :n], g["actions"][i, :n])
