@@ -74,30 +74,37 @@ def measured_traffic(args):
 
 
 def arena_leg(net, games=1000, sims=25, seed=0, reps=3):
-    """Config 4: Arena.playGames(1000) of MCTS(temp 0, 25 sims) vs the uniform-random player,
-    one lock-step device batch (agent seat 1 for the first half, -1 for the second)."""
+    """Config 4: Arena.playGames(1000) in one lock-step device batch (agent seat 1 for the first
+    half, -1 for the second): MCTS(temp 0, 25 sims) vs the uniform-random legal player, and the
+    reference's GreedyYachtPlayer vs random (9.9 games/s on the reference)."""
     import numpy as np
     import torch
 
     from yacht_amd.engine import SelfPlayEngine
     seats = np.array([1] * (games // 2) + [-1] * (games - games // 2), dtype=np.int32)
-    eng = SelfPlayEngine(games, sims, 1.5, 0, net=net, max_moves=64)
-    eng.arena(seats, seed + 1000, 0)  # warm-up
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(reps):
-        eng.arena(seats, seed + 1001 + i, 0)
-    torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / reps
-    r = eng.arena_results()
-    st = eng.stats()
-    eng.close()
-    agent = r["result"] * seats
-    return {"config": f"Arena.playGames({games}), MCTS temp 0 x {sims} sims vs uniform-random legal player, "
-                      f"random-init YachtNNet", "games_per_s": games / dt, "ms_per_batch": 1000.0 * dt,
-            "agent_won": int((agent == 1).sum()), "random_won": int((agent == -1).sum()),
-            "draws": int(((agent != 1) & (agent != -1)).sum()), "moves": int(r["n_moves"].sum()),
-            "expansions_per_s": st["expansions"] / dt}
+    out = {}
+    for name, agent, s in (("mcts_vs_random", "mcts", sims), ("greedy_vs_random", "greedy", 1)):
+        eng = SelfPlayEngine(games, s, 1.5, 0, net=net, max_moves=64)
+        eng.arena(seats, seed + 1000, 0, agent=agent)  # warm-up
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(reps):
+            eng.arena(seats, seed + 1001 + i, 0, agent=agent)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / reps
+        r = eng.arena_results()
+        st = eng.stats()
+        eng.close()
+        won = r["result"] * seats
+        out[name] = {"config": f"Arena.playGames({games}), {agent}" + (f" (temp 0, {s} sims, random-init YachtNNet)"
+                                                                      if agent == "mcts" else "") +
+                               " vs uniform-random legal player",
+                     "games_per_s": games / dt, "ms_per_batch": 1000.0 * dt,
+                     "agent_won": int((won == 1).sum()), "random_won": int((won == -1).sum()),
+                     "draws": int(((won != 1) & (won != -1)).sum()), "moves": int(r["n_moves"].sum())}
+        if agent == "mcts":
+            out[name]["expansions_per_s"] = st["expansions"] / dt
+    return out
 
 
 def main():

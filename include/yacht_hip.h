@@ -98,6 +98,10 @@ int yk_score_dice(const int8_t* dice, int32_t* out, int n, void* stream);
 int yk_featurize(const yk_state_t* in, float* x, int n, void* stream);
 /* 64-bit transposition-key hash (stands in for stringRepresentation, YachtGame.py:448-467). */
 int yk_key_hash(const yk_state_t* in, uint64_t* out, int n, void* stream);
+/* GreedyYachtPlayer's heuristic (yacht/YachtPlayers.py:38-171) on canonical boards (device):
+ * actions[i] = the heuristic's action, or -1 when it is not a valid move (the player then
+ * plays np.random.choice(legal), YachtPlayers.py:199-214). */
+int yk_greedy_action(const yk_state_t* states, int32_t* actions, int n, void* stream);
 /* Deterministic test prior (oracle/spec.py hash_prior): pi[i*3226 + a], v[i]. */
 int yk_hash_prior(const yk_state_t* in, float* pi, float* v, int n, void* stream);
 
@@ -172,13 +176,17 @@ int64_t yk_engine_record_bytes(yk_engine_t* eng);
 int yk_engine_pack_records(yk_engine_t* eng, void* dst, int64_t capacity, void* stream);
 
 /* ---------------------------------------------------------------- Arena
- * Batched Arena.playGame (Arena.py:30-93) of the MCTS agent against RandomYachtPlayer
- * (yacht/YachtPlayers.py:174-183), n_envs games in lock-step, the evaluation leg of
- * Coach.learn (Coach.py:118-131).  Game i uses stream env_base+i; agent_seat (HOST, [n]) is
- * 1 (agent moves first) or -1.  The agent is np.argmax(MCTS.getActionProb(board, temp=0))
- * (Coach.py:124-125) with one tree per game for the whole game; the random player draws
- * uniformly among the legal actions of its canonical board.  Returns like yk_selfplay. */
-int yk_arena(yk_engine_t* eng, uint64_t seed, uint32_t env_base, const int32_t* agent_seat, void* stream);
+ * Batched Arena.playGame (Arena.py:30-93), n_envs games in lock-step: `agent` in seat
+ * agent_seat[i] (HOST, [n]; 1 = moves first, -1) against `opponent` in the other seat, each a
+ * YK_PLAYER_*: MCTS = np.argmax(MCTS.getActionProb(board, temp=0)) (Coach.py:124-125) with the
+ * engine's net / prior and sims, one tree per game for the whole game; RANDOM =
+ * RandomYachtPlayer (YachtPlayers.py:174-183); GREEDY = GreedyYachtPlayer (:186-214).  Game i
+ * uses stream env_base+i for every draw.  Returns like yk_selfplay. */
+#define YK_PLAYER_MCTS 0
+#define YK_PLAYER_RANDOM 1
+#define YK_PLAYER_GREEDY 2
+int yk_arena(yk_engine_t* eng, uint64_t seed, uint32_t env_base, const int32_t* agent_seat, int agent, int opponent,
+             void* stream);
 /* HOST outputs of the last yk_arena (any may be NULL): result[n] = curPlayer * getGameEnded
  * (Arena.py:93, from player 1's view: +1 / -1 / +-1e-4 draw), totals[n][2] (player 1, player 2,
  * with bonus), n_moves[n], actions[n][max_moves] (-1 past the end), final_states[n][8],

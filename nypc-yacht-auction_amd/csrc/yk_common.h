@@ -14,6 +14,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <climits>
+
 #include "yacht_hip.h"
 
 namespace yk {
@@ -453,6 +455,107 @@ __device__ __host__ inline bool action_valid(const YkS& s, int player, int a) {
     const Tables& T = h_tab;
 #endif
     return !((wa_used(wa) >> cat) & 1) && T.comb_max[ci] < n;
+}
+
+// ------------------------------------------------------------------ GreedyYachtPlayer
+// Best immediate gain (score + the basic bonus when it crosses 63,000) over unused categories x
+// combos of `dice` (nibbles, n of them), all 64 lanes together; *best_t = the first maximum in
+// (category, combo) order.  stop_first_invalid: the scorer's walk stops at the first combo
+// reaching past the carry (YachtPlayers.py:151-153); otherwise combos with max(comb) < n
+// (the bid potential, :67).  INT_MIN when nothing is eligible.
+__device__ inline int greedy_best_wave(uint64_t dice, int n, uint32_t used, int basic_before, bool stop_first_invalid,
+                                       int lane, int* best_t) {
+    const int lim = n >= 10 ? NCOMB : (n >= 5 ? n - 4 : 0);
+    int best = INT_MIN, bt = 0x7FFFFFFF;
+    for (int t = lane; t < NCAT * NCOMB; t += 64) {
+        const int cat = t / NCOMB, ci = t - cat * NCOMB;
+        if ((used >> cat) & 1u) continue;
+        if (stop_first_invalid ? ci >= lim : c_tab.comb_max[ci] >= n) continue;
+        const uint32_t pos = c_tab.comb_pos[ci];
+        uint32_t chosen = 0;
+#pragma unroll
+        for (int k = 0; k < 5; k++) chosen |= (uint32_t)((dice >> (4 * ((pos >> (4 * k)) & 0xF))) & 0xF) << (4 * k);
+        const int sc = 1000 * score_k(cat, chosen);
+        const int gain = sc + ((cat < 6 && basic_before < 63000 && 63000 <= basic_before + sc) ? 35000 : 0);
+        if (gain > best) {
+            best = gain;
+            bt = t;
+        }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const int ob = __shfl_xor(best, o, 64), ot = __shfl_xor(bt, o, 64);
+        if (ob > best || (ob == best && ot < bt)) {
+            best = ob;
+            bt = ot;
+        }
+    }
+    *best_t = bt;
+    return best;
+}
+// _score_potential_after_bid  YachtPlayers.py:38-87 (bundle: 5 nibbles, or absent)
+__device__ inline int greedy_potential_wave(const YkS& s, uint64_t bundle, bool has_bundle, int lane) {
+    const uint64_t wa = s_pw(s, 0, 0);
+    const int nc = wa_n(wa);
+    const uint64_t dice = (wa & ((1ull << 40) - 1)) | (has_bundle ? bundle << (4 * nc) : 0ull);
+    const int n = nc + (has_bundle ? 5 : 0);
+    if (s_round(s) == 1) {
+        int sum = 0, cnt[7] = {0, 0, 0, 0, 0, 0, 0};
+        for (int i = 0; i < n; i++) {
+            const int d = (int)((dice >> (4 * i)) & 0xF);
+            sum += d;
+            cnt[d] += 1;
+        }
+        int v = 1000 * sum, mx = 0;
+        for (int f = 1; f <= 6; f++) mx = cnt[f] > mx ? cnt[f] : mx;
+        if (mx >= 4) v += 6000;
+        else if (mx == 3) v += 3000;
+        const bool e1 = cnt[1] > 0, e2 = cnt[2] > 0, e3 = cnt[3] > 0, e4 = cnt[4] > 0, e5 = cnt[5] > 0, e6 = cnt[6] > 0;
+        if ((e1 && e2 && e3 && e4) || (e2 && e3 && e4 && e5) || (e3 && e4 && e5 && e6)) v += 5000;
+        return v;
+    }
+    if (n < 5) return 0;
+    int basic;
+    cat_sum(s_pw(s, 0, 1), s_pw(s, 0, 2), &basic);
+    int t;
+    const int best = greedy_best_wave(dice, n, (uint32_t)wa_used(wa), 1000 * basic, false, lane, &t);
+    return best == INT_MIN ? 0 : best;
+}
+// GreedyYachtPlayer.play's heuristic (YachtPlayers.py:90-171, 199-214) on a canonical board,
+// all 64 lanes together: the chosen action if it is valid, else -1 (the player then draws a
+// random legal action).  The bid may encode past index 100 (bids up to 100,000, :124-127).
+__device__ inline int greedy_heuristic_wave(const YkS& s, int lane) {
+    const int round = s_round(s), phase = s_phase(s);
+    if (phase == 0 && round != 13) {
+        const uint64_t w0 = s.w[0];
+        const int valA = greedy_potential_wave(s, (w0 >> 24) & 0xFFFFF, (w0 >> 5) & 1, lane);
+        const int valB = greedy_potential_wave(s, (w0 >> 44) & 0xFFFFF, (w0 >> 6) & 1, lane);
+        int target, gap;
+        if (valA >= valB) {
+            target = 0;
+            gap = valA - valB > 0 ? valA - valB : 0;
+        } else {
+            target = 1;
+            gap = valB - valA > 0 ? valB - valA : 0;
+        }
+        const int diff = total_with_bonus(s, 0) - total_with_bonus(s, 1);
+        const double bid_k = 0.5 * ((double)gap / 1000.0) - 0.15 * ((double)diff / 1000.0);
+        long bid = (long)rint(1000.0 * bid_k);  // python round(): half to even
+        bid = bid > 100000 ? 100000 : (bid < 0 ? 0 : bid);
+        bid = (bid / 500) * 500;
+        const int a = target * BID_LEVELS + (int)(bid / 500);
+        return a < NBID ? a : -1;
+    }
+    const uint64_t wa = s_pw(s, 0, 0);
+    const int n = wa_n(wa);
+    if (n < 5) return -1;  // the scorer returns 0, never valid in the score phase
+    int basic;
+    cat_sum(s_pw(s, 0, 1), s_pw(s, 0, 2), &basic);
+    int t;
+    const int best = greedy_best_wave(wa & ((1ull << 40) - 1), n, (uint32_t)wa_used(wa), 1000 * basic, true, lane, &t);
+    if (best == INT_MIN) return -1;
+    const int a = NBID + t;
+    return phase == 1 ? a : -1;  // valid only in the score phase
 }
 
 // ------------------------------------------------------------------ features

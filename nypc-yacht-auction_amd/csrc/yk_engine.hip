@@ -59,7 +59,8 @@ struct EngDev {
     float c32;
     int prior;  // 0 net, 1 hash
     int rec_pred, max_exp;
-    int arena;             // 1 while yk_arena runs: agent (MCTS, temp 0) vs uniform-random mover
+    int arena;             // 1 while yk_arena runs
+    int arena_agent, arena_opp;  // YK_PLAYER_* of the seat-agent_seat player and of the other seat
     uint64_t seed;
     NodeRec* nodes[2];
     uint32_t* hidx[2];
@@ -80,7 +81,7 @@ struct EngDev {
     int32_t* nmoves;
     yk_state_t* root;
     int32_t* seat;         // [E] arena: the agent's seat (1 / -1)
-    uint8_t* idle;         // [E] arena: the random mover is to move (no search this move)
+    uint8_t* idle;         // [E] arena: a non-MCTS player is to move (no search this move)
     // per-sim
     yk_state_t* leaf_state;
     uint64_t* leaf_hash;
@@ -351,13 +352,13 @@ __global__ __launch_bounds__(256) void k_move_begin(EngDev d, int move, int exte
         if (d.done[e]) return;
         const YkS b = ld_state(d.board + e);
         const YkS r = canonical(b, d.cur[e]);
-        const bool idle = d.arena && d.cur[e] != d.seat[e];
+        const bool idle = d.arena && (d.cur[e] == d.seat[e] ? d.arena_agent : d.arena_opp) != YK_PLAYER_MCTS;
         if (lane == 0) {
             st_state(d.root + e, r);
             d.rec_ctr[((long)e * d.M + move) * 2] = d.ctr[e];
             d.idle[e] = idle ? 1 : 0;
         }
-        if (idle) return;  // Arena: the random player does not search (YachtPlayers.py:174-183)
+        if (idle) return;  // Arena: the random / greedy players do not search (YachtPlayers.py:174-214)
     } else if (lane == 0) {
         d.idle[e] = 0;
     }
@@ -874,6 +875,10 @@ __global__ __launch_bounds__(256) void k_move_end(EngDev d, int move) {
     } else if (lane == 0) {
         atomicOr(d.err, ERR_ROOT);
     }
+    // GreedyYachtPlayer's heuristic needs the whole wave (YachtPlayers.py:186-214)
+    int gact = -1;
+    if (idle && (d.cur[e] == d.seat[e] ? d.arena_agent : d.arena_opp) == YK_PLAYER_GREEDY)
+        gact = greedy_heuristic_wave(r, lane);
     wave_sync();
     // record the visit counts (sparse, ascending action)
     const long vbase = (long)e * d.VCAP;
@@ -888,9 +893,12 @@ __global__ __launch_bounds__(256) void k_move_end(EngDev d, int move) {
     const int temp = d.arena ? 0 : (stepi < d.temp_threshold ? 1 : 0);  // Coach.py:58
     Stream rs{d.seed, d.env_id[e], d.ctr[e]};
     int action = 0;
-    if (idle) {
-        // RandomYachtPlayer.play: np.random.choice over the ascending legal actions of the
-        // canonical board (YachtPlayers.py:174-183); no legal action -> 0 without a draw
+    if (idle && gact >= 0) {
+        action = gact;  // the greedy heuristic's (valid) choice
+    } else if (idle) {
+        // RandomYachtPlayer.play, and GreedyYachtPlayer's fallback: np.random.choice over the
+        // ascending legal actions of the canonical board (YachtPlayers.py:174-183, 204-214);
+        // no legal action -> 0 without a draw
         const VInfo vi = valid_info(r, 1);
         if (vi.V > 0) action = compact_to_action(vi, rs.below(vi.V));
     } else if (temp == 0) {
@@ -1271,8 +1279,10 @@ int play_batch(yk_engine* eng, uint64_t seed, uint32_t env_base, hipStream_t s) 
         prof_mark(eng, KC_MOVE_BEGIN, s);
         hipLaunchKernelGGL(k_move_begin, gb, bb, 0, s, d, move, 0);
         YK_LAUNCHED();
-        int rc = run_sims(eng, d.sims, d.env_id, d.ctr, s);
-        if (rc) return rc;
+        if (!d.arena || d.arena_agent == YK_PLAYER_MCTS || d.arena_opp == YK_PLAYER_MCTS) {
+            int rc = run_sims(eng, d.sims, d.env_id, d.ctr, s);
+            if (rc) return rc;
+        }
         prof_mark(eng, KC_MOVE_END, s);
         hipLaunchKernelGGL(k_move_end, gb, bb, 0, s, d, move);
         YK_LAUNCHED();
@@ -1300,14 +1310,19 @@ int yk_selfplay(yk_engine_t* eng, uint64_t seed, uint32_t env_base, void* stream
     return play_batch(eng, seed, env_base, as_stream(stream));
 }
 
-int yk_arena(yk_engine_t* eng, uint64_t seed, uint32_t env_base, const int32_t* agent_seat, void* stream) {
+int yk_arena(yk_engine_t* eng, uint64_t seed, uint32_t env_base, const int32_t* agent_seat, int agent, int opponent,
+             void* stream) {
     if (!eng || !agent_seat) return YK_ERR_ARG;
+    if (agent < YK_PLAYER_MCTS || agent > YK_PLAYER_GREEDY || opponent < YK_PLAYER_MCTS || opponent > YK_PLAYER_GREEDY)
+        return YK_ERR_ARG;
     EngDev& d = eng->d;
     for (int e = 0; e < d.E; e++)
         if (agent_seat[e] != 1 && agent_seat[e] != -1) return YK_ERR_ARG;
     hipStream_t s = as_stream(stream);
     YK_HIP(hipMemcpyAsync(d.seat, agent_seat, sizeof(int32_t) * (size_t)d.E, hipMemcpyHostToDevice, s));
     d.arena = 1;
+    d.arena_agent = agent;
+    d.arena_opp = opponent;
     eng->have_arena = false;
     const int rc = play_batch(eng, seed, env_base, s);
     d.arena = 0;

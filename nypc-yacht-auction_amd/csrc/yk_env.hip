@@ -152,6 +152,16 @@ __global__ void k_hash_prior(const yk_state_t* in, float* pi, float* v, int n) {
 }
 
 // ------------------------------------------------------------------ C ABI
+// GreedyYachtPlayer's heuristic, one wave per state
+__global__ __launch_bounds__(256) void k_greedy(const yk_state_t* in, int32_t* out, int n) {
+    const int lane = threadIdx.x & 63;
+    const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= n) return;
+    const YkS s = load_state(in, i);
+    const int a = greedy_heuristic_wave(s, lane);
+    if (lane == 0) out[i] = a;
+}
+
 extern "C" {
 
 const char* yk_version(void) { return "yacht_hip 0.1 (gfx950)"; }
@@ -247,6 +257,14 @@ int yk_hash_prior(const yk_state_t* in, float* pi, float* v, int n, void* stream
     if (!in || !pi || !v) return YK_ERR_ARG;
     if (n > 65535) return YK_ERR_ARG;
     hipLaunchKernelGGL(k_hash_prior, dim3(4, n), dim3(256), 0, as_stream(stream), in, pi, v, n);
+    YK_LAUNCHED();
+    return YK_OK;
+}
+
+int yk_greedy_action(const yk_state_t* states, int32_t* actions, int n, void* stream) {
+    YK_CHECK_N(n);
+    if (!states || !actions) return YK_ERR_ARG;
+    hipLaunchKernelGGL(k_greedy, dim3((n + 3) / 4), dim3(256), 0, as_stream(stream), states, actions, n);
     YK_LAUNCHED();
     return YK_OK;
 }

@@ -62,7 +62,8 @@ SIGNATURES = {
     "yk_engine_create": [C.POINTER(P), C.POINTER(YkEngineConfig), P],
     "yk_engine_destroy": [P],
     "yk_selfplay": [P, U64, U32, P],
-    "yk_arena": [P, U64, U32, P, P],
+    "yk_arena": [P, U64, U32, P, I, I, P],
+    "yk_greedy_action": [P, P, I, P],
     "yk_arena_results": [P, P, P, P, P, P, P],
     "yk_engine_stats": [P, P],
     "yk_engine_profile": [P, I],

@@ -1,10 +1,12 @@
-"""Arena on the MI355X engine (Arena.py:8-130, YachtPlayers.py:174-183).
+"""Arena on the MI355X engine (Arena.py:8-130, YachtPlayers.py:174-214).
 
 ``Arena(player1, player2, game)`` keeps the reference's sequential host loop for arbitrary
-duck-typed players.  ``MCTSArena(game, nnet, args).playGames(num)`` is the batched form
-of config 4 - the MCTS agent (``np.argmax(getActionProb(x, temp=0))``, Coach.py:124-125)
-against ``RandomYachtPlayer`` - with all ``num`` games played in one lock-step device batch
-(``yk_arena``).  Randomness comes from per-game streams: game k of a playGames call uses
+duck-typed players (``RandomYachtPlayer``, ``GreedyYachtPlayer`` - its heuristic runs on the
+GPU, ``yk_greedy_action`` - or an MCTS lambda).  ``MCTSArena(game, nnet, args).playGames(num)``
+is the batched form of config 4 - by default the MCTS agent
+(``np.argmax(getActionProb(x, temp=0))``, Coach.py:124-125) against ``RandomYachtPlayer``, or
+any pairing of "mcts" / "random" / "greedy" - with all ``num`` games played in one lock-step
+device batch (``yk_arena``).  Randomness comes from per-game streams: game k of a playGames call uses
 ``(game seed, game env_id + k)``; the first num/2 games seat the agent as player 1, the
 rest as player 2 (the reference swaps players after num/2 games, Arena.py:118).
 Every game gets a fresh agent tree (the reference shares one MCTS across the games of a
@@ -29,6 +31,23 @@ class RandomYachtPlayer:
 
     def play(self, board) -> int:
         legal = np.nonzero(self.game.getValidMoves(board, 1))[0]  # canonical player = 1
+        return int(legal[self.game.rng.below(len(legal))]) if len(legal) else 0
+
+
+class GreedyYachtPlayer:
+    """Heuristic bidder + greedy scorer (YachtPlayers.py:186-214) on the canonical board; the
+    heuristic runs on the GPU, a random-legal fallback draws from the game's stream."""
+
+    def __init__(self, game, seed=None):
+        self.game = game  # seed: the reference reseeds the global RNGs; streams are per game here
+
+    def play(self, board) -> int:
+        from . import kernels as K
+        from .state import pack
+        a = int(K.greedy_action(K.states_to_device(pack(board)))[0].item())
+        if a >= 0:
+            return a
+        legal = np.nonzero(self.game.getValidMoves(board, 1))[0]
         return int(legal[self.game.rng.below(len(legal))]) if len(legal) else 0
 
 
@@ -89,24 +108,29 @@ class Arena:
 
 
 class MCTSArena:
-    """Batched Arena.playGames(num) of the MCTS agent (player1) vs RandomYachtPlayer (player2)."""
+    """Batched Arena.playGames(num): `agent` (player1; default the MCTS agent over `nnet`) vs
+    `opponent` (player2; default RandomYachtPlayer), each "mcts", "random" or "greedy"."""
 
-    def __init__(self, game, nnet, args):
+    def __init__(self, game, nnet, args, agent="mcts", opponent="random"):
         self.game, self.nnet, self.args = game, nnet, args
+        self.agent, self.opponent = agent, opponent
         self._games = 0
         self.last = None
 
     def _engine(self, n):
-        prior = "hash" if getattr(self.nnet, "yk_prior", None) == "hash" else "net"
+        uses_net = "mcts" in (self.agent, self.opponent) and self.nnet is not None
+        prior = "hash" if not uses_net or getattr(self.nnet, "yk_prior", None) == "hash" else "net"
         net = None if prior == "hash" else self.nnet.yk_net()
-        return SelfPlayEngine(n, self.args.numMCTSSims, self.args.cpuct, 0, net=net, prior=prior, max_moves=64)
+        sims = self.args.numMCTSSims if "mcts" in (self.agent, self.opponent) else 1
+        return SelfPlayEngine(n, sims, self.args.get("cpuct", 1.0), 0, net=net, prior=prior, max_moves=64)
 
     def play_batch(self, agent_seats) -> dict:
         """One device batch; agent_seats[i] in {1, -1}.  Returns the engine's arena results."""
         seats = np.asarray(agent_seats, dtype=np.int32)
         eng = self._engine(len(seats))
         try:
-            eng.arena(seats, self.game.rng.seed, self.game.rng.env + self._games)
+            eng.arena(seats, self.game.rng.seed, self.game.rng.env + self._games, agent=self.agent,
+                      opponent=self.opponent)
             self._games += len(seats)
             self.last = eng.arena_results()
         finally:

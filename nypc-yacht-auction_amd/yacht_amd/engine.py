@@ -50,14 +50,18 @@ class SelfPlayEngine:
             bits = [n for b, n in self.ERROR_BITS.items() if st["errors"] & b]
             raise YkError(f"yk_selfplay [{', '.join(bits)}; stats {st}]", e.code) from None
 
-    def arena(self, agent_seat, seed: int, env_base: int = 0, stream=None):
-        """Batched Arena.playGame of the MCTS agent (temp 0) vs the uniform-random player
-        (yk_arena): game i uses stream (seed, env_base + i), agent in seat agent_seat[i]."""
+    PLAYERS = {"mcts": 0, "random": 1, "greedy": 2}  # YK_PLAYER_*
+
+    def arena(self, agent_seat, seed: int, env_base: int = 0, stream=None, agent: str = "mcts",
+              opponent: str = "random"):
+        """Batched Arena.playGame (yk_arena): `agent` in seat agent_seat[i] against `opponent`,
+        each "mcts" (temp 0, this engine's net / prior and sims), "random" or "greedy"; game i
+        uses stream (seed, env_base + i)."""
         from ._lib import YkError
         seat = np.ascontiguousarray(np.broadcast_to(np.asarray(agent_seat, dtype=np.int32), (self.n_envs,)))
         try:
             call("yk_arena", self.handle, seed & (2**64 - 1), env_base & (2**32 - 1), seat.ctypes.data,
-                 stream_ptr(stream))
+                 self.PLAYERS[agent], self.PLAYERS[opponent], stream_ptr(stream))
         except YkError as e:
             st = self.stats()
             bits = [n for b, n in self.ERROR_BITS.items() if st["errors"] & b]

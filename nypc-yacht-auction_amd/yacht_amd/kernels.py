@@ -142,3 +142,12 @@ def hash_prior(states):
 
 __all__ = ["states_to_device", "states_to_host", "init_board", "step", "valid_mask", "unpack_mask", "ended",
            "canonical", "score_table", "score_dice", "featurize", "key_hash", "hash_prior", "_lib"]
+
+
+def greedy_action(states):
+    """GreedyYachtPlayer's heuristic on canonical boards: the action, or -1 where the player
+    falls back to a random legal action (YachtPlayers.py:199-214)."""
+    st = _dev(states, torch.int64).reshape(-1, 8)
+    out = torch.empty(st.shape[0], dtype=torch.int32, device="cuda")
+    call("yk_greedy_action", ptr(st), ptr(out), st.shape[0], stream_ptr())
+    return out

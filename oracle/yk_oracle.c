@@ -872,10 +872,11 @@ static int greedy_best(const pl_t* me, const int* dice, int n, int stop_at_first
     return best;
 }
 /* _score_potential_after_bid  YachtPlayers.py:38-87 */
-static int greedy_potential(const st_t* s, const pl_t* me, const int* bundle) {
+static int greedy_potential(const st_t* s, const pl_t* me, const int* bundle, int has_bundle) {
     int dice[15], n = 0;
     for (int i = 0; i < me->n; i++) dice[n++] = me->d[i];
-    for (int i = 0; i < 5; i++) dice[n++] = bundle[i];
+    if (has_bundle) /* an absent roll is an empty list */
+        for (int i = 0; i < 5; i++) dice[n++] = bundle[i];
     if (s->round == 1) {
         int sum = 0, counts[7] = {0}, mx = 0;
         for (int i = 0; i < n; i++) { sum += dice[i]; counts[dice[i]]++; }
@@ -900,7 +901,7 @@ static int total_bb(const pl_t* q) {
 /* _choose_bid  YachtPlayers.py:90-127: the action may encode past index 100 (bids up to 100,000) */
 static int greedy_choose_bid(const st_t* s) {
     const pl_t* me = &s->p[0];
-    const int valA = greedy_potential(s, me, s->A), valB = greedy_potential(s, me, s->B);
+    const int valA = greedy_potential(s, me, s->A, s->hasA), valB = greedy_potential(s, me, s->B, s->hasB);
     int target, gap;
     if (valA >= valB) { target = 0; gap = valA - valB > 0 ? valA - valB : 0; }
     else { target = 1; gap = valB - valA > 0 ? valB - valA : 0; }

@@ -138,3 +138,61 @@ def test_mcts_arena_playgames_and_sequential_arena(Y):
     res = Arena(lambda x: int(np.argmax(mcts.getActionProb(x, temp=0))), RandomYachtPlayer(g2).play,
                 g2).playGame()
     assert res == o["result"][0]
+
+
+def test_greedy_heuristic_kernel_matches_reference(Y, golden):
+    """yk_greedy_action on all 11,403 fixture states against the reference GreedyYachtPlayer's
+    choices (tests/golden/greedy.npz) and the C restatement."""
+    from yacht_amd import kernels as K
+    g = golden("greedy.npz")
+    h = K.greedy_action(K.states_to_device(g["states"])).cpu().numpy()
+    assert np.array_equal(h, O.greedy_heuristic(g["states"]))
+    ok = h >= 0
+    assert np.array_equal(h[ok], g["action"][ok])
+    assert (g["draws"][~ok] > 0).sum() == (g["draws"] > 0).sum()  # every fallback draw is a -1 here
+
+
+@pytest.mark.parametrize("fixture,agent,opponent", [("arena_greedy_random.npz", "greedy", "random"),
+                                                     ("arena_mcts_greedy.npz", "mcts", "greedy")])
+def test_arena_pairings_match_reference_games(Y, golden, fixture, agent, opponent):
+    E, _ = Y
+    g = golden(fixture)
+    env = g["env"]
+    eng = E.SelfPlayEngine(len(env), max(int(g["sims"]), 1), 1.5, 0, prior="hash", max_moves=64)
+    eng.arena(g["seat"], int(g["seed"]), int(env[0]), agent=agent, opponent=opponent)
+    r = eng.arena_results()
+    assert np.array_equal(r["result"], g["result"])
+    assert np.array_equal(r["ctr"], g["ctr_end"].astype(np.uint64))
+    for i, n in enumerate(g["n_moves"]):
+        assert np.array_equal(r["actions"][i, :n], g["actions"][i, :n]), i
+
+
+@pytest.mark.parametrize("agent,opponent,sims,n", [("greedy", "random", 1, 256), ("random", "greedy", 1, 128),
+                                                   ("mcts", "greedy", 4, 64), ("greedy", "mcts", 6, 48),
+                                                   ("greedy", "greedy", 1, 64)])
+def test_arena_pairings_match_oracle(Y, agent, opponent, sims, n):
+    E, _ = Y
+    seed, base = 9100 + sims, 40000
+    seats = np.where(np.arange(n) % 2 == 0, 1, -1).astype(np.int32)
+    eng = E.SelfPlayEngine(n, sims, 1.5, 0, prior="hash", max_moves=64)
+    eng.arena(seats, seed, base, agent=agent, opponent=opponent)
+    r = eng.arena_results()
+    o = O.arena(np.arange(base, base + n), seats, seed, sims, 1.5, agent=agent, opponent=opponent, threads=8)
+    assert o["nerr"] == 0
+    assert np.array_equal(r["result"], o["result"])
+    assert np.array_equal(r["totals"], o["totals"])
+    assert np.array_equal(r["final"], o["final"])
+    assert np.array_equal(r["ctr"], o["stats"][:, 4].astype(np.uint64))
+
+
+def test_sequential_arena_with_greedy_plugin(Y, golden):
+    from yacht_amd.arena import Arena, GreedyYachtPlayer, MCTSArena, RandomYachtPlayer
+    from yacht_amd.game import YachtGame
+    from yacht_amd.utils import dotdict
+    g = golden("arena_greedy_random.npz")
+    game = YachtGame(seed=int(g["seed"]), env_id=int(g["env"][0]))
+    res = Arena(GreedyYachtPlayer(game).play, RandomYachtPlayer(game).play, game).playGame()
+    assert res == g["result"][0] and game.rng.ctr == int(g["ctr_end"][0])
+    one, two, draws = MCTSArena(YachtGame(seed=5, env_id=0), None, dotdict(), agent="greedy",
+                                opponent="random").playGames(200)
+    assert one + two + draws == 200 and one > 180  # the greedy player beats random almost always
