@@ -205,6 +205,46 @@ int yk_mcts_search(yk_engine_t* eng, const yk_state_t* roots, uint64_t seed, con
                    uint64_t* rng_ctr, int sims, int32_t* counts, void* stream);
 int yk_mcts_reset(yk_engine_t* eng);
 
+/* ---------------------------------------------------------------- training
+ * NNetWrapper.train (yacht/NNet.py:118-174): one optimiser step per minibatch of YachtNNet in
+ * float32 - loss = cross_entropy(logits, argmax(pi)) + vloss_weight * mse(v, z) (:143-148),
+ * clip_grad_norm_(max_grad_norm) (:152-153), AdamW(lr, weight_decay) (:109-110).  Dropout masks
+ * come from the Philox stream (seed, layer, step, element), not torch's generator.
+ * Parameters, gradients and Adam moments are flat device buffers in state_dict order. */
+typedef struct {
+    int max_batch;          /* batch_size (rows per step, upper bound) */
+    float lr, weight_decay; /* AdamW */
+    float beta1, beta2, eps;
+    float max_grad_norm;    /* 5.0 in the reference */
+    float vloss_weight;     /* 1.5 in main.py */
+    float dropout;          /* 0.3 in main.py; 0 for deterministic parity tests */
+    uint64_t seed;          /* dropout stream */
+} yk_train_config_t;
+typedef struct yk_trainer yk_trainer_t;
+/* params: HOST float32 arrays in YachtNNet.state_dict() order (as yk_net_create) */
+int yk_trainer_create(yk_trainer_t** t, int hidden, int nblocks, const float* const* params, int nparams,
+                      const yk_train_config_t* cfg);
+int yk_trainer_destroy(yk_trainer_t* t);
+/* device pointers of the flat parameter and gradient buffers (for a DDP all-reduce of grads) */
+int yk_trainer_buffers(yk_trainer_t* t, float** params, float** grads, int64_t* nparams);
+/* forward + backward of one minibatch into the gradient buffer (overwritten).  Example i of the
+ * batch is replay entry batch_idx[i] (device, or NULL for 0..batch-1): states[] packed canonical
+ * boards, targets[] = argmax(pi) (NNet.py:145-146), values[] = v.  Losses: yk_trainer_losses. */
+int yk_trainer_backward(yk_trainer_t* t, const yk_state_t* states, const int32_t* targets, const float* values,
+                        const int32_t* batch_idx, int batch, void* stream);
+/* clip_grad_norm_ + AdamW on the (possibly all-reduced) gradient buffer; advances the step */
+int yk_trainer_apply(yk_trainer_t* t, void* stream);
+/* yk_trainer_backward + yk_trainer_apply */
+int yk_trainer_step(yk_trainer_t* t, const yk_state_t* states, const int32_t* targets, const float* values,
+                    const int32_t* batch_idx, int batch, void* stream);
+/* HOST out[3]: sum over the last batch of cross-entropy, of squared value error; grad sq-norm */
+int yk_trainer_losses(yk_trainer_t* t, double* out);
+/* copy parameters (which 0), gradients (1), exp_avg (2), exp_avg_sq (3) to / from HOST arrays in
+ * state_dict order (NULL entries skipped); set: step >= 0 also sets the optimiser step count */
+int yk_trainer_get(yk_trainer_t* t, int which, float* const* out);
+int yk_trainer_set(yk_trainer_t* t, int which, const float* const* in, int64_t step);
+int64_t yk_trainer_step_count(yk_trainer_t* t);
+
 #ifdef __cplusplus
 }
 #endif

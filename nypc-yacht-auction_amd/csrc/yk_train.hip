@@ -1,0 +1,720 @@
+// yk_train.hip - NNetWrapper.train (yacht/NNet.py:118-174) on MI355X: one optimiser step of
+// YachtNNet (yacht/pytorch/YachtNNet.py:8-70) in float32.
+//
+// Per minibatch: gather (features from packed states, hard targets, values) -> forward with the
+// activations the backward needs -> loss = CE(logits, argmax(pi)) + vloss_weight * MSE(v, z)
+// (NNet.py:143-148) -> backward -> [caller all-reduces the gradient buffer for DDP] ->
+// clip_grad_norm_(5.0) (NNet.py:152-153) -> AdamW (NNet.py:109-110).
+//
+// The dense layers are plain GEMMs and go to rocBLAS (f32).  Everything between them is
+// hand-written and fused per row: bias + SiLU + LayerNorm + dropout + residual forward, the
+// matching backward (LayerNorm input gradient from the saved statistics), the loss and its
+// gradients, column reductions for bias / LayerNorm parameter gradients, the global gradient
+// norm and the AdamW update.  Parameters, gradients and the Adam moments are single flat
+// buffers in torch state_dict order, so the gradient buffer is one RCCL all-reduce.
+#include <rocblas/rocblas.h>
+
+#include <cmath>
+#include <vector>
+
+#include "yk_api.h"
+#include "yk_common.h"
+
+using namespace yk;
+
+namespace {
+
+constexpr int TPB = 256;
+
+__device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
+__device__ __forceinline__ float silu_f(float x) { return x * sigm(x); }
+__device__ __forceinline__ float silu_grad(float x) {  // d/dx x*s(x) = s(x) (1 + x (1 - s(x)))
+    const float s = sigm(x);
+    return s * (1.0f + x * (1.0f - s));
+}
+__device__ __forceinline__ float wsum(float v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ float wmax(float v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+// dropout keep-mask from the Philox stream: element `idx` of layer `layer` at optimiser step `step`
+__device__ __forceinline__ bool keep(uint64_t seed, int layer, uint64_t step, long idx, float p) {
+    if (p <= 0.0f) return true;
+    const uint64_t d = philox_draw(seed, 0x44524F50u + (uint32_t)layer, (step << 32) ^ (uint64_t)idx);
+    return (float)(d >> 40) * (1.0f / 16777216.0f) >= p;
+}
+
+// LayerNorm of one row held VPL-per-lane (biased variance, eps 1e-5); returns x_hat, mean, rstd
+template <int VPL>
+__device__ __forceinline__ void ln_row(float (&x)[VPL], int H, float& mu, float& rs) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPL; i++) s += x[i];
+    mu = wsum(s) / (float)H;
+    float v = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPL; i++) {
+        const float d = x[i] - mu;
+        v += d * d;
+    }
+    rs = 1.0f / sqrtf(wsum(v) / (float)H + 1e-5f);
+#pragma unroll
+    for (int i = 0; i < VPL; i++) x[i] = (x[i] - mu) * rs;
+}
+// LayerNorm backward for one row: dxh = dy * gamma; dx = rs/H (H dxh - sum dxh - xh sum(dxh xh))
+template <int VPL>
+__device__ __forceinline__ void ln_row_bwd(const float (&xh)[VPL], float (&dy)[VPL], const float* g, int c0, int H, float rs) {
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPL; i++) {
+        dy[i] *= g[c0 + i];
+        a += dy[i];
+        b += dy[i] * xh[i];
+    }
+    a = wsum(a);
+    b = wsum(b);
+#pragma unroll
+    for (int i = 0; i < VPL; i++) dy[i] = rs / (float)H * ((float)H * dy[i] - a - xh[i] * b);
+}
+
+// ---------------------------------------------------------------- forward row kernels (one wave per row)
+// inp: Z0 += b; A = LN(Z0) (affine); H0 = dropout(silu(A)).  Saves Z0 (+bias), mu, rs, mask.
+template <int VPL>
+__global__ void k_inp_fwd(float* Z, const float* b, const float* g, const float* be, float* mu_o, float* rs_o,
+                          uint8_t* mask, float* Hout, int B, float p, uint64_t seed, uint64_t step) {
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (row >= B) return;
+    constexpr int H = VPL * 64;
+    const int c0 = lane * VPL;
+    float x[VPL];
+#pragma unroll
+    for (int i = 0; i < VPL; i++) {
+        x[i] = Z[(long)row * H + c0 + i] + b[c0 + i];
+        Z[(long)row * H + c0 + i] = x[i];
+    }
+    float mu, rs;
+    ln_row<VPL>(x, H, mu, rs);
+    if (lane == 0) {
+        mu_o[row] = mu;
+        rs_o[row] = rs;
+    }
+    const float sc = 1.0f / (1.0f - p);
+#pragma unroll
+    for (int i = 0; i < VPL; i++) {
+        const long idx = (long)row * H + c0 + i;
+        const float a = x[i] * g[c0 + i] + be[c0 + i];
+        const bool k = keep(seed, 0, step, idx, p);
+        mask[idx] = k;
+        Hout[idx] = k ? silu_f(a) * (p > 0.f ? sc : 1.0f) : 0.0f;
+    }
+}
+// block half 1: U1 += b1; L1 = LN1(silu(U1)); R1 = dropout(L1).  Saves U1 (+bias), mu, rs, mask, R1.
+// block half 2 (layer < 0 marks it): U2 += b2; L2 = LN2(silu(U2)); Hout = Hin + L2.
+template <int VPL>
+__global__ void k_blk_fwd(float* U, const float* b, const float* g, const float* be, float* mu_o, float* rs_o,
+                          uint8_t* mask, float* out, const float* Hin, int B, float p, uint64_t seed, uint64_t step,
+                          int layer) {
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (row >= B) return;
+    constexpr int H = VPL * 64;
+    const int c0 = lane * VPL;
+    float x[VPL];
+#pragma unroll
+    for (int i = 0; i < VPL; i++) {
+        const float u = U[(long)row * H + c0 + i] + b[c0 + i];
+        U[(long)row * H + c0 + i] = u;
+        x[i] = silu_f(u);
+    }
+    float mu, rs;
+    ln_row<VPL>(x, H, mu, rs);
+    if (lane == 0) {
+        mu_o[row] = mu;
+        rs_o[row] = rs;
+    }
+    const float sc = 1.0f / (1.0f - p);
+#pragma unroll
+    for (int i = 0; i < VPL; i++) {
+        const long idx = (long)row * H + c0 + i;
+        const float l = x[i] * g[c0 + i] + be[c0 + i];
+        if (Hin) {
+            out[idx] = Hin[idx] + l;  // residual
+        } else {
+            const bool k = keep(seed, layer, step, idx, p);
+            mask[idx] = k;
+            out[idx] = k ? l * (p > 0.f ? sc : 1.0f) : 0.0f;
+        }
+    }
+}
+// heads: Tpi = LNpi(h), Api = silu(Tpi); Tv = LNv(h), Av = silu(Tv).  Saves stats of both.
+template <int VPL>
+__global__ void k_heads_fwd(const float* Hh, const float* gp, const float* bp, const float* gv, const float* bv,
+                            float* Api, float* Av, float* mup, float* rsp, float* muv, float* rsv, int B) {
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (row >= B) return;
+    constexpr int H = VPL * 64;
+    const int c0 = lane * VPL;
+    float x[VPL], y[VPL];
+#pragma unroll
+    for (int i = 0; i < VPL; i++) x[i] = y[i] = Hh[(long)row * H + c0 + i];
+    float m1, r1, m2, r2;
+    ln_row<VPL>(x, H, m1, r1);
+    ln_row<VPL>(y, H, m2, r2);
+    if (lane == 0) {
+        mup[row] = m1;
+        rsp[row] = r1;
+        muv[row] = m2;
+        rsv[row] = r2;
+    }
+#pragma unroll
+    for (int i = 0; i < VPL; i++) {
+        Api[(long)row * H + c0 + i] = silu_f(x[i] * gp[c0 + i] + bp[c0 + i]);
+        Av[(long)row * H + c0 + i] = silu_f(y[i] * gv[c0 + i] + bv[c0 + i]);
+    }
+}
+// v head tail + both losses + the output gradients.  One wave per row.
+//   Zv1 += bv1 (saved); v = tanh(silu(Zv1) . wv2 + bv2); mse_i = (v - z)^2
+//   logits += bpi; ce_i = lse - logit[t]; dlogits = (softmax - onehot(t)) / B
+//   dzv2 = vw * 2 (v - z) / B * (1 - v^2); dZv1 = dzv2 wv2 silu'(Zv1)
+__global__ void k_loss(float* logits, const float* bpi, float* Zv1, const float* bv1, const float* wv2, const float* bv2,
+                       const int32_t* tgt, const float* vt, float* dlogits, float* dZv1, float* dzv2, float* vout,
+                       double* loss_acc, int B, int A, float vw) {
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (row >= B) return;
+    float* z = logits + (long)row * A;
+    float m = -INFINITY;
+    for (int a = lane; a < A; a += 64) {
+        const float x = z[a] + bpi[a];
+        z[a] = x;
+        m = fmaxf(m, x);
+    }
+    m = wmax(m);
+    float se = 0.f;
+    for (int a = lane; a < A; a += 64) se += expf(z[a] - m);
+    se = wsum(se);
+    const float lse = m + logf(se);
+    const int t = tgt[row];
+    const float invB = 1.0f / (float)B;
+    for (int a = lane; a < A; a += 64) dlogits[(long)row * A + a] = (expf(z[a] - lse) - (a == t ? 1.0f : 0.0f)) * invB;
+    // value head tail (128 hidden, 2 per lane)
+    float s = 0.f, zz[2];
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        const int c = 2 * lane + k;
+        zz[k] = Zv1[(long)row * 128 + c] + bv1[c];
+        Zv1[(long)row * 128 + c] = zz[k];
+        s += silu_f(zz[k]) * wv2[c];
+    }
+    s = wsum(s) + bv2[0];
+    const float v = tanhf(s);
+    const float e = v - vt[row];
+    const float dv = vw * 2.0f * e * invB * (1.0f - v * v);
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        const int c = 2 * lane + k;
+        dZv1[(long)row * 128 + c] = dv * wv2[c] * silu_grad(zz[k]);
+    }
+    if (lane == 0) {
+        dzv2[row] = dv;
+        vout[row] = v;
+        atomicAdd(&loss_acc[0], (double)(lse - z[t]));
+        atomicAdd(&loss_acc[1], (double)(e * e));
+    }
+}
+
+// ---------------------------------------------------------------- backward row kernels
+// heads backward: dApi, dAv -> dTpi, dTv (silu') -> LN backward of both -> dH (sum); writes
+// the per-row LayerNorm parameter contributions gpi_row = dTpi * xhat, bpi_row = dTpi (same for v)
+template <int VPL>
+__global__ void k_heads_bwd(const float* Hh, const float* gp, const float* bp, const float* gv, const float* bv,
+                            const float* mup, const float* rsp, const float* muv, const float* rsv, const float* dApi,
+                            const float* dAv, float* dH, float* rg_p, float* rb_p, float* rg_v, float* rb_v, int B) {
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (row >= B) return;
+    constexpr int H = VPL * 64;
+    const int c0 = lane * VPL;
+    float xp[VPL], xv[VPL], dp[VPL], dv[VPL];
+    const float m1 = mup[row], r1 = rsp[row], m2 = muv[row], r2 = rsv[row];
+#pragma unroll
+    for (int i = 0; i < VPL; i++) {
+        const long idx = (long)row * H + c0 + i;
+        const float h = Hh[idx];
+        xp[i] = (h - m1) * r1;
+        xv[i] = (h - m2) * r2;
+        dp[i] = dApi[idx] * silu_grad(xp[i] * gp[c0 + i] + bp[c0 + i]);
+        dv[i] = dAv[idx] * silu_grad(xv[i] * gv[c0 + i] + bv[c0 + i]);
+        rg_p[idx] = dp[i] * xp[i];
+        rb_p[idx] = dp[i];
+        rg_v[idx] = dv[i] * xv[i];
+        rb_v[idx] = dv[i];
+    }
+    ln_row_bwd<VPL>(xp, dp, gp, c0, H, r1);
+    ln_row_bwd<VPL>(xv, dv, gv, c0, H, r2);
+#pragma unroll
+    for (int i = 0; i < VPL; i++) dH[(long)row * H + c0 + i] = dp[i] + dv[i];
+}
+// block-half backward through LN(silu(U)) (+ dropout on the way in for half 1):
+//   dL = dIn (* mask / (1-p) when mask); dS = LN backward (S = silu(U) recomputed); dU = dS silu'(U)
+// rg/rb: per-row LayerNorm gamma / beta contributions
+template <int VPL>
+__global__ void k_blk_bwd(const float* dIn, const uint8_t* mask, float p, const float* U, const float* g,
+                          const float* mu, const float* rs, float* dU, float* rg, float* rb, int B) {
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (row >= B) return;
+    constexpr int H = VPL * 64;
+    const int c0 = lane * VPL;
+    const float m = mu[row], r = rs[row];
+    const float sc = p > 0.f ? 1.0f / (1.0f - p) : 1.0f;
+    float xh[VPL], d[VPL], u[VPL];
+#pragma unroll
+    for (int i = 0; i < VPL; i++) {
+        const long idx = (long)row * H + c0 + i;
+        u[i] = U[idx];
+        xh[i] = (silu_f(u[i]) - m) * r;
+        d[i] = dIn[idx];
+        if (mask) d[i] = mask[idx] ? d[i] * sc : 0.0f;
+        rg[idx] = d[i] * xh[i];
+        rb[idx] = d[i];
+    }
+    ln_row_bwd<VPL>(xh, d, g, c0, H, r);
+#pragma unroll
+    for (int i = 0; i < VPL; i++) dU[(long)row * H + c0 + i] = d[i] * silu_grad(u[i]);
+}
+// inp backward: dH0 -> dropout -> silu'(A) -> LN backward (input Z0) -> dZ0
+template <int VPL>
+__global__ void k_inp_bwd(const float* dH0, const uint8_t* mask, float p, const float* Z, const float* g,
+                          const float* be, const float* mu, const float* rs, float* dZ, float* rg, float* rb, int B) {
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (row >= B) return;
+    constexpr int H = VPL * 64;
+    const int c0 = lane * VPL;
+    const float m = mu[row], r = rs[row];
+    const float sc = p > 0.f ? 1.0f / (1.0f - p) : 1.0f;
+    float xh[VPL], d[VPL];
+#pragma unroll
+    for (int i = 0; i < VPL; i++) {
+        const long idx = (long)row * H + c0 + i;
+        xh[i] = (Z[idx] - m) * r;
+        float dy = mask[idx] ? dH0[idx] * sc : 0.0f;
+        dy *= silu_grad(xh[i] * g[c0 + i] + be[c0 + i]);
+        d[i] = dy;
+        rg[idx] = dy * xh[i];
+        rb[idx] = dy;
+    }
+    ln_row_bwd<VPL>(xh, d, g, c0, H, r);
+#pragma unroll
+    for (int i = 0; i < VPL; i++) dZ[(long)row * H + c0 + i] = d[i];
+}
+// out[c] = sum_r in[r * N + c] (column sums), one thread per column
+__global__ void k_colsum(const float* in, float* out, int B, int N) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= N) return;
+    float s = 0.f;
+    for (int r = 0; r < B; r++) s += in[(long)r * N + c];
+    out[c] = s;
+}
+// dwv2[c] = sum_r dzv2[r] * silu(Zv1[r][c]); dbv2 = sum_r dzv2[r]
+__global__ void k_v2_grad(const float* dzv2, const float* Zv1, float* dw, float* db, int B) {
+    const int c = threadIdx.x;  // 128 threads (+1 for the bias)
+    if (c < 128) {
+        float s = 0.f;
+        for (int r = 0; r < B; r++) s += dzv2[r] * silu_f(Zv1[(long)r * 128 + c]);
+        dw[c] = s;
+    } else if (c == 128) {
+        float s = 0.f;
+        for (int r = 0; r < B; r++) s += dzv2[r];
+        db[0] = s;
+    }
+}
+// gather a minibatch: features of states[idx[i]], targets, values
+__global__ void k_gather(const yk_state_t* states, const int32_t* tgt_all, const float* v_all, const int32_t* idx,
+                         float* X, int32_t* tgt, float* vt, int B) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= B * 64) return;
+    const int i = t >> 6, f = t & 63;
+    const int src = idx ? idx[i] : i;
+    if (f < FEAT) {
+        const uint4* q = reinterpret_cast<const uint4*>(states + src);
+        YkS s;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint4 u = q[k];
+            s.w[2 * k] = (uint64_t)u.x | ((uint64_t)u.y << 32);
+            s.w[2 * k + 1] = (uint64_t)u.z | ((uint64_t)u.w << 32);
+        }
+        X[(long)i * FEAT + f] = feature(s, f);
+    }
+    if (f == 0) {
+        tgt[i] = tgt_all[src];
+        vt[i] = v_all[src];
+    }
+}
+// sum of squares of the gradient buffer -> acc (double)
+__global__ void k_sqnorm(const float* g, long n, double* acc) {
+    __shared__ double part[TPB / 64];
+    double s = 0.0;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+        const double x = g[i];
+        s += x * x;
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+        for (int w = 0; w < TPB / 64; w++) t += part[w];
+        atomicAdd(acc, t);
+    }
+}
+// clip_grad_norm_ (coef = min(1, max_norm / (norm + 1e-6)), NNet.py:152-153) + AdamW
+// (torch single-tensor AdamW: decoupled decay, bias-corrected moments)
+__global__ void k_adamw(float* p, float* g, float* m, float* v, long n, const double* sq, float max_norm, float lr,
+                        float wd, float b1, float b2, float eps, float step_size, float bc2_sqrt) {
+    const float norm = (float)sqrt(*sq);
+    float coef = max_norm / (norm + 1e-6f);
+    coef = coef > 1.0f ? 1.0f : coef;
+    const float decay = 1.0f - lr * wd;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+        const float gi = g[i] * coef;
+        g[i] = gi;
+        float pi = p[i] * decay;
+        const float mi = m[i] + (gi - m[i]) * (1.0f - b1);  // exp_avg.lerp_(grad, 1 - beta1)
+        const float vi = v[i] * b2 + (1.0f - b2) * gi * gi;
+        m[i] = mi;
+        v[i] = vi;
+        const float denom = sqrtf(vi) / bc2_sqrt + eps;
+        pi -= step_size * (mi / denom);
+        p[i] = pi;
+    }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- host object
+struct yk_trainer {
+    int H = 0, NB = 0, Bmax = 0;
+    yk_train_config_t cfg{};
+    rocblas_handle blas = nullptr;
+    float *P = nullptr, *G = nullptr, *M = nullptr, *V = nullptr;
+    long nparams = 0;
+    std::vector<long> off;  // tensor offsets, state_dict order
+    std::vector<long> len;
+    uint64_t step = 0;
+    std::vector<void*> allocs;
+    // activations (Bmax rows)
+    float *X = nullptr, *vt = nullptr, *vout = nullptr;
+    int32_t* tgt = nullptr;
+    float *Z0 = nullptr, *mu0 = nullptr, *rs0 = nullptr;
+    uint8_t* mask0 = nullptr;
+    std::vector<float*> Hs, U1, U2, R1, mu1, rs1, mu2, rs2;
+    std::vector<uint8_t*> mask1;
+    float *Api = nullptr, *Av = nullptr, *mup = nullptr, *rsp = nullptr, *muv = nullptr, *rsv = nullptr;
+    float *logits = nullptr, *Zv1 = nullptr, *dlogits = nullptr, *dZv1 = nullptr, *dzv2 = nullptr;
+    float *dA = nullptr, *dAv = nullptr, *dH = nullptr, *dT = nullptr, *dU = nullptr, *rg = nullptr, *rb = nullptr,
+          *rg2 = nullptr, *rb2 = nullptr;
+    double* acc = nullptr;  // [0] ce sum, [1] mse sum, [2] grad sq norm
+    double host_loss[3] = {0, 0, 0};
+};
+
+namespace {
+// tensor indices in state_dict order (YachtNNet.py:30-52)
+enum { T_WIN = 0, T_BIN, T_GIN, T_BEIN };
+inline int t_blk(int b, int k) { return 4 + 8 * b + k; }  // k: 0 fc1.w 1 fc1.b 2 ln1.w 3 ln1.b 4 fc2.w 5 fc2.b 6 ln2.w 7 ln2.b
+inline int t_head(int NB, int k) { return 4 + 8 * NB + k; }  // 0 pi.0.w 1 pi.0.b 2 pi.2.w 3 pi.2.b 4 v.0.w 5 v.0.b 6 v.2.w 7 v.2.b 8 v.4.w 9 v.4.b
+
+template <class T>
+int talloc(yk_trainer* t, T** p, size_t count) {
+    void* q = nullptr;
+    if (hipMalloc(&q, sizeof(T) * (count ? count : 1)) != hipSuccess) {
+        (void)hipGetLastError();
+        return YK_ERR_NOMEM;
+    }
+    t->allocs.push_back(q);
+    *p = static_cast<T*>(q);
+    return YK_OK;
+}
+
+// row-major C[M][N] = op(A)[M][K] . op(B)[K][N] (+ beta C) on rocBLAS's column-major API
+int gemm_rm(yk_trainer* t, bool ta, bool tb, int M, int N, int K, const float* A, int lda, const float* B, int ldb,
+            float* C, int ldc, float beta) {
+    const float one = 1.0f;
+    const rocblas_status st =
+        rocblas_sgemm(t->blas, tb ? rocblas_operation_transpose : rocblas_operation_none,
+                      ta ? rocblas_operation_transpose : rocblas_operation_none, N, M, K, &one, B, ldb, A, lda, &beta, C, ldc);
+    return st == rocblas_status_success ? YK_OK : YK_ERR_HIP;
+}
+
+template <int VPL>
+int step_impl(yk_trainer* t, const yk_state_t* states, const int32_t* targets, const float* values, const int32_t* idx,
+              int B, hipStream_t s) {
+    constexpr int H = VPL * 64;
+    const int NB = t->NB, A = ASIZE;
+    const float p = t->cfg.dropout;
+    const uint64_t seed = t->cfg.seed, step = t->step;
+    auto Pt = [&](int k) { return t->P + t->off[k]; };
+    auto Gt = [&](int k) { return t->G + t->off[k]; };
+    const dim3 rows((B + 3) / 4), wave4(256);
+    int rc;
+    YK_HIP(hipMemsetAsync(t->acc, 0, sizeof(double) * 3, s));
+    hipLaunchKernelGGL(k_gather, dim3((B * 64 + 255) / 256), dim3(256), 0, s, states, targets, values, idx, t->X, t->tgt,
+                       t->vt, B);
+    YK_LAUNCHED();
+    // ---- forward
+    if ((rc = gemm_rm(t, false, true, B, H, FEAT, t->X, FEAT, Pt(T_WIN), FEAT, t->Z0, H, 0.f))) return rc;
+    hipLaunchKernelGGL(k_inp_fwd<VPL>, rows, wave4, 0, s, t->Z0, Pt(T_BIN), Pt(T_GIN), Pt(T_BEIN), t->mu0, t->rs0,
+                       t->mask0, t->Hs[0], B, p, seed, step);
+    YK_LAUNCHED();
+    for (int b = 0; b < NB; b++) {
+        if ((rc = gemm_rm(t, false, true, B, H, H, t->Hs[b], H, Pt(t_blk(b, 0)), H, t->U1[b], H, 0.f))) return rc;
+        hipLaunchKernelGGL(k_blk_fwd<VPL>, rows, wave4, 0, s, t->U1[b], Pt(t_blk(b, 1)), Pt(t_blk(b, 2)), Pt(t_blk(b, 3)),
+                           t->mu1[b], t->rs1[b], t->mask1[b], t->R1[b], (const float*)nullptr, B, p, seed, step, 1 + b);
+        YK_LAUNCHED();
+        if ((rc = gemm_rm(t, false, true, B, H, H, t->R1[b], H, Pt(t_blk(b, 4)), H, t->U2[b], H, 0.f))) return rc;
+        hipLaunchKernelGGL(k_blk_fwd<VPL>, rows, wave4, 0, s, t->U2[b], Pt(t_blk(b, 5)), Pt(t_blk(b, 6)), Pt(t_blk(b, 7)),
+                           t->mu2[b], t->rs2[b], (uint8_t*)nullptr, t->Hs[b + 1], t->Hs[b], B, p, seed, step, -1);
+        YK_LAUNCHED();
+    }
+    const float* Hh = t->Hs[NB];
+    hipLaunchKernelGGL(k_heads_fwd<VPL>, rows, wave4, 0, s, Hh, Pt(t_head(NB, 0)), Pt(t_head(NB, 1)), Pt(t_head(NB, 4)),
+                       Pt(t_head(NB, 5)), t->Api, t->Av, t->mup, t->rsp, t->muv, t->rsv, B);
+    YK_LAUNCHED();
+    if ((rc = gemm_rm(t, false, true, B, A, H, t->Api, H, Pt(t_head(NB, 2)), H, t->logits, A, 0.f))) return rc;
+    if ((rc = gemm_rm(t, false, true, B, 128, H, t->Av, H, Pt(t_head(NB, 6)), H, t->Zv1, 128, 0.f))) return rc;
+    hipLaunchKernelGGL(k_loss, rows, wave4, 0, s, t->logits, Pt(t_head(NB, 3)), t->Zv1, Pt(t_head(NB, 7)), Pt(t_head(NB, 8)),
+                       Pt(t_head(NB, 9)), t->tgt, t->vt, t->dlogits, t->dZv1, t->dzv2, t->vout, t->acc, B, A,
+                       t->cfg.vloss_weight);
+    YK_LAUNCHED();
+    // ---- backward: heads
+    if ((rc = gemm_rm(t, true, false, A, H, B, t->dlogits, A, t->Api, H, Gt(t_head(NB, 2)), H, 0.f))) return rc;
+    hipLaunchKernelGGL(k_colsum, dim3((A + 255) / 256), dim3(256), 0, s, t->dlogits, Gt(t_head(NB, 3)), B, A);
+    YK_LAUNCHED();
+    if ((rc = gemm_rm(t, false, false, B, H, A, t->dlogits, A, Pt(t_head(NB, 2)), H, t->dA, H, 0.f))) return rc;
+    hipLaunchKernelGGL(k_v2_grad, dim3(1), dim3(192), 0, s, t->dzv2, t->Zv1, Gt(t_head(NB, 8)), Gt(t_head(NB, 9)), B);
+    YK_LAUNCHED();
+    if ((rc = gemm_rm(t, true, false, 128, H, B, t->dZv1, 128, t->Av, H, Gt(t_head(NB, 6)), H, 0.f))) return rc;
+    hipLaunchKernelGGL(k_colsum, dim3(1), dim3(128), 0, s, t->dZv1, Gt(t_head(NB, 7)), B, 128);
+    YK_LAUNCHED();
+    if ((rc = gemm_rm(t, false, false, B, H, 128, t->dZv1, 128, Pt(t_head(NB, 6)), H, t->dAv, H, 0.f))) return rc;
+    hipLaunchKernelGGL(k_heads_bwd<VPL>, rows, wave4, 0, s, Hh, Pt(t_head(NB, 0)), Pt(t_head(NB, 1)), Pt(t_head(NB, 4)),
+                       Pt(t_head(NB, 5)), t->mup, t->rsp, t->muv, t->rsv, t->dA, t->dAv, t->dH, t->rg, t->rb, t->rg2,
+                       t->rb2, B);
+    YK_LAUNCHED();
+    const dim3 cs((H + 255) / 256), cb(256);
+    hipLaunchKernelGGL(k_colsum, cs, cb, 0, s, t->rg, Gt(t_head(NB, 0)), B, H);
+    hipLaunchKernelGGL(k_colsum, cs, cb, 0, s, t->rb, Gt(t_head(NB, 1)), B, H);
+    hipLaunchKernelGGL(k_colsum, cs, cb, 0, s, t->rg2, Gt(t_head(NB, 4)), B, H);
+    hipLaunchKernelGGL(k_colsum, cs, cb, 0, s, t->rb2, Gt(t_head(NB, 5)), B, H);
+    YK_LAUNCHED();
+    // ---- blocks, last to first; t->dH holds dL/dH_{b+1}
+    for (int b = NB - 1; b >= 0; b--) {
+        hipLaunchKernelGGL(k_blk_bwd<VPL>, rows, wave4, 0, s, t->dH, (const uint8_t*)nullptr, 0.f, t->U2[b],
+                           Pt(t_blk(b, 6)), t->mu2[b], t->rs2[b], t->dU, t->rg, t->rb, B);
+        YK_LAUNCHED();
+        hipLaunchKernelGGL(k_colsum, cs, cb, 0, s, t->rg, Gt(t_blk(b, 6)), B, H);
+        hipLaunchKernelGGL(k_colsum, cs, cb, 0, s, t->rb, Gt(t_blk(b, 7)), B, H);
+        hipLaunchKernelGGL(k_colsum, cs, cb, 0, s, t->dU, Gt(t_blk(b, 5)), B, H);
+        YK_LAUNCHED();
+        if ((rc = gemm_rm(t, true, false, H, H, B, t->dU, H, t->R1[b], H, Gt(t_blk(b, 4)), H, 0.f))) return rc;
+        if ((rc = gemm_rm(t, false, false, B, H, H, t->dU, H, Pt(t_blk(b, 4)), H, t->dT, H, 0.f))) return rc;  // dR1
+        hipLaunchKernelGGL(k_blk_bwd<VPL>, rows, wave4, 0, s, t->dT, t->mask1[b], p, t->U1[b], Pt(t_blk(b, 2)), t->mu1[b],
+                           t->rs1[b], t->dU, t->rg, t->rb, B);
+        YK_LAUNCHED();
+        hipLaunchKernelGGL(k_colsum, cs, cb, 0, s, t->rg, Gt(t_blk(b, 2)), B, H);
+        hipLaunchKernelGGL(k_colsum, cs, cb, 0, s, t->rb, Gt(t_blk(b, 3)), B, H);
+        hipLaunchKernelGGL(k_colsum, cs, cb, 0, s, t->dU, Gt(t_blk(b, 1)), B, H);
+        YK_LAUNCHED();
+        if ((rc = gemm_rm(t, true, false, H, H, B, t->dU, H, t->Hs[b], H, Gt(t_blk(b, 0)), H, 0.f))) return rc;
+        // dH_b = dH_{b+1} (residual) + dU1 . W1
+        if ((rc = gemm_rm(t, false, false, B, H, H, t->dU, H, Pt(t_blk(b, 0)), H, t->dH, H, 1.f))) return rc;
+    }
+    // ---- input layer
+    hipLaunchKernelGGL(k_inp_bwd<VPL>, rows, wave4, 0, s, t->dH, t->mask0, p, t->Z0, Pt(T_GIN), Pt(T_BEIN), t->mu0,
+                       t->rs0, t->dU, t->rg, t->rb, B);
+    YK_LAUNCHED();
+    hipLaunchKernelGGL(k_colsum, cs, cb, 0, s, t->rg, Gt(T_GIN), B, H);
+    hipLaunchKernelGGL(k_colsum, cs, cb, 0, s, t->rb, Gt(T_BEIN), B, H);
+    hipLaunchKernelGGL(k_colsum, cs, cb, 0, s, t->dU, Gt(T_BIN), B, H);
+    YK_LAUNCHED();
+    if ((rc = gemm_rm(t, true, false, H, FEAT, B, t->dU, H, t->X, FEAT, Gt(T_WIN), FEAT, 0.f))) return rc;
+    return YK_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int yk_trainer_create(yk_trainer_t** out, int H, int NB, const float* const* params, int nparams,
+                      const yk_train_config_t* cfg) {
+    if (!out || !params || !cfg) return YK_ERR_ARG;
+    if (!(H == 64 || H == 128 || H == 256 || H == 512) || NB < 0 || NB > 64) return YK_ERR_ARG;
+    if (nparams != 14 + 8 * NB || cfg->max_batch <= 0) return YK_ERR_ARG;
+    if (!(cfg->dropout >= 0.0f && cfg->dropout < 1.0f)) return YK_ERR_ARG;
+    yk_trainer* t = new yk_trainer();
+    t->H = H;
+    t->NB = NB;
+    t->Bmax = cfg->max_batch;
+    t->cfg = *cfg;
+    // tensor sizes in state_dict order
+    std::vector<long> n = {(long)H * FEAT, H, H, H};
+    for (int b = 0; b < NB; b++)
+        for (long x : {(long)H * H, (long)H, (long)H, (long)H, (long)H * H, (long)H, (long)H, (long)H}) n.push_back(x);
+    for (long x : {(long)H, (long)H, (long)ASIZE * H, (long)ASIZE, (long)H, (long)H, (long)128 * H, 128L, 128L, 1L})
+        n.push_back(x);
+    long o = 0;
+    for (long x : n) {
+        t->off.push_back(o);
+        t->len.push_back(x);
+        o += x;
+    }
+    t->nparams = o;
+    const size_t Bm = (size_t)t->Bmax, HH = (size_t)H;
+    int rc = YK_OK;
+#define TA(p, c) \
+    if (rc == YK_OK) rc = talloc(t, &(p), (c))
+    TA(t->P, o);
+    TA(t->G, o);
+    TA(t->M, o);
+    TA(t->V, o);
+    TA(t->X, Bm * FEAT);
+    TA(t->tgt, Bm);
+    TA(t->vt, Bm);
+    TA(t->vout, Bm);
+    TA(t->Z0, Bm * HH);
+    TA(t->mu0, Bm);
+    TA(t->rs0, Bm);
+    TA(t->mask0, Bm * HH);
+    t->Hs.assign(NB + 1, nullptr);
+    for (int b = 0; b <= NB; b++) TA(t->Hs[b], Bm * HH);
+    t->U1.assign(NB, nullptr); t->U2.assign(NB, nullptr); t->R1.assign(NB, nullptr);
+    t->mu1.assign(NB, nullptr); t->rs1.assign(NB, nullptr); t->mu2.assign(NB, nullptr); t->rs2.assign(NB, nullptr);
+    t->mask1.assign(NB, nullptr);
+    for (int b = 0; b < NB; b++) {
+        TA(t->U1[b], Bm * HH);
+        TA(t->U2[b], Bm * HH);
+        TA(t->R1[b], Bm * HH);
+        TA(t->mu1[b], Bm);
+        TA(t->rs1[b], Bm);
+        TA(t->mu2[b], Bm);
+        TA(t->rs2[b], Bm);
+        TA(t->mask1[b], Bm * HH);
+    }
+    TA(t->Api, Bm * HH);
+    TA(t->Av, Bm * HH);
+    TA(t->mup, Bm); TA(t->rsp, Bm); TA(t->muv, Bm); TA(t->rsv, Bm);
+    TA(t->logits, Bm * ASIZE);
+    TA(t->dlogits, Bm * ASIZE);
+    TA(t->Zv1, Bm * 128);
+    TA(t->dZv1, Bm * 128);
+    TA(t->dzv2, Bm);
+    TA(t->dA, Bm * HH); TA(t->dAv, Bm * HH); TA(t->dH, Bm * HH); TA(t->dT, Bm * HH); TA(t->dU, Bm * HH);
+    TA(t->rg, Bm * HH); TA(t->rb, Bm * HH); TA(t->rg2, Bm * HH); TA(t->rb2, Bm * HH);
+    TA(t->acc, 3);
+#undef TA
+    if (rc == YK_OK && rocblas_create_handle(&t->blas) != rocblas_status_success) rc = YK_ERR_HIP;
+    if (rc != YK_OK) {
+        yk_trainer_destroy(t);
+        return rc;
+    }
+    for (size_t k = 0; k < n.size(); k++)
+        if (hipMemcpy(t->P + t->off[k], params[k], sizeof(float) * t->len[k], hipMemcpyHostToDevice) != hipSuccess) {
+            yk_trainer_destroy(t);
+            return YK_ERR_HIP;
+        }
+    (void)hipMemset(t->M, 0, sizeof(float) * o);
+    (void)hipMemset(t->V, 0, sizeof(float) * o);
+    (void)hipMemset(t->G, 0, sizeof(float) * o);
+    if (hipDeviceSynchronize() != hipSuccess) {
+        yk_trainer_destroy(t);
+        return YK_ERR_HIP;
+    }
+    *out = t;
+    return YK_OK;
+}
+
+int yk_trainer_destroy(yk_trainer_t* t) {
+    if (!t) return YK_OK;
+    if (t->blas) rocblas_destroy_handle(t->blas);
+    for (void* p : t->allocs) (void)hipFree(p);
+    delete t;
+    return YK_OK;
+}
+
+int yk_trainer_buffers(yk_trainer_t* t, float** params, float** grads, int64_t* nparams) {
+    if (!t) return YK_ERR_ARG;
+    if (params) *params = t->P;
+    if (grads) *grads = t->G;
+    if (nparams) *nparams = t->nparams;
+    return YK_OK;
+}
+
+int yk_trainer_backward(yk_trainer_t* t, const yk_state_t* states, const int32_t* targets, const float* values,
+                        const int32_t* batch_idx, int batch, void* stream) {
+    if (!t || !states || !targets || !values) return YK_ERR_ARG;
+    if (batch <= 0 || batch > t->Bmax) return YK_ERR_ARG;
+    hipStream_t s = as_stream(stream);
+    if (rocblas_set_stream(t->blas, s) != rocblas_status_success) return YK_ERR_HIP;
+    switch (t->H) {
+        case 64: return step_impl<1>(t, states, targets, values, batch_idx, batch, s);
+        case 128: return step_impl<2>(t, states, targets, values, batch_idx, batch, s);
+        case 256: return step_impl<4>(t, states, targets, values, batch_idx, batch, s);
+        case 512: return step_impl<8>(t, states, targets, values, batch_idx, batch, s);
+    }
+    return YK_ERR_ARG;
+}
+
+int yk_trainer_apply(yk_trainer_t* t, void* stream) {
+    if (!t) return YK_ERR_ARG;
+    hipStream_t s = as_stream(stream);
+    t->step += 1;
+    const double b1 = t->cfg.beta1, b2 = t->cfg.beta2, st = (double)t->step;
+    const double bc1 = 1.0 - std::pow(b1, st), bc2 = 1.0 - std::pow(b2, st);
+    const float step_size = (float)(t->cfg.lr / bc1), bc2_sqrt = (float)std::sqrt(bc2);
+    hipLaunchKernelGGL(k_sqnorm, dim3(1024), dim3(TPB), 0, s, t->G, t->nparams, t->acc + 2);
+    YK_LAUNCHED();
+    hipLaunchKernelGGL(k_adamw, dim3(2048), dim3(TPB), 0, s, t->P, t->G, t->M, t->V, t->nparams, t->acc + 2,
+                       t->cfg.max_grad_norm, t->cfg.lr, t->cfg.weight_decay, t->cfg.beta1, t->cfg.beta2, t->cfg.eps,
+                       step_size, bc2_sqrt);
+    YK_LAUNCHED();
+    return YK_OK;
+}
+
+int yk_trainer_step(yk_trainer_t* t, const yk_state_t* states, const int32_t* targets, const float* values,
+                    const int32_t* batch_idx, int batch, void* stream) {
+    int rc = yk_trainer_backward(t, states, targets, values, batch_idx, batch, stream);
+    if (rc) return rc;
+    return yk_trainer_apply(t, stream);
+}
+
+int yk_trainer_losses(yk_trainer_t* t, double* out) {
+    if (!t || !out) return YK_ERR_ARG;
+    YK_HIP(hipDeviceSynchronize());
+    YK_HIP(hipMemcpy(out, t->acc, sizeof(double) * 3, hipMemcpyDeviceToHost));
+    return YK_OK;
+}
+
+int yk_trainer_get(yk_trainer_t* t, int which, float* const* out) {
+    if (!t || !out || which < 0 || which > 3) return YK_ERR_ARG;
+    const float* src = which == 0 ? t->P : which == 1 ? t->G : which == 2 ? t->M : t->V;
+    YK_HIP(hipDeviceSynchronize());
+    for (size_t k = 0; k < t->off.size(); k++)
+        if (out[k]) YK_HIP(hipMemcpy(out[k], src + t->off[k], sizeof(float) * t->len[k], hipMemcpyDeviceToHost));
+    return YK_OK;
+}
+
+int yk_trainer_set(yk_trainer_t* t, int which, const float* const* in, int64_t step) {
+    if (!t || !in || which < 0 || which > 3) return YK_ERR_ARG;
+    float* dst = which == 0 ? t->P : which == 1 ? t->G : which == 2 ? t->M : t->V;
+    for (size_t k = 0; k < t->off.size(); k++)
+        if (in[k]) YK_HIP(hipMemcpy(dst + t->off[k], in[k], sizeof(float) * t->len[k], hipMemcpyHostToDevice));
+    if (step >= 0) t->step = (uint64_t)step;
+    YK_HIP(hipDeviceSynchronize());
+    return YK_OK;
+}
+
+int64_t yk_trainer_step_count(yk_trainer_t* t) { return t ? (int64_t)t->step : YK_ERR_ARG; }
+
+}  // extern "C"

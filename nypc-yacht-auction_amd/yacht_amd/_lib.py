@@ -64,6 +64,16 @@ SIGNATURES = {
     "yk_selfplay": [P, U64, U32, P],
     "yk_arena": [P, U64, U32, P, I, I, P],
     "yk_greedy_action": [P, P, I, P],
+    "yk_trainer_create": [P, I, I, P, I, P],
+    "yk_trainer_destroy": [P],
+    "yk_trainer_buffers": [P, P, P, P],
+    "yk_trainer_backward": [P, P, P, P, P, I, P],
+    "yk_trainer_apply": [P, P],
+    "yk_trainer_step": [P, P, P, P, P, I, P],
+    "yk_trainer_losses": [P, P],
+    "yk_trainer_get": [P, I, P],
+    "yk_trainer_set": [P, I, P, C.c_int64],
+    "yk_trainer_step_count": [P],
     "yk_arena_results": [P, P, P, P, P, P, P],
     "yk_engine_stats": [P, P],
     "yk_engine_profile": [P, I],
@@ -75,7 +85,8 @@ SIGNATURES = {
     "yk_mcts_search": [P, P, U64, P, P, I, P, P],
     "yk_mcts_reset": [P],
 }
-_RESTYPE = {"yk_version": C.c_char_p, "yk_rng_draw64": C.c_uint64, "yk_engine_record_bytes": C.c_int64}
+_RESTYPE = {"yk_version": C.c_char_p, "yk_rng_draw64": C.c_uint64, "yk_engine_record_bytes": C.c_int64,
+            "yk_trainer_step_count": C.c_int64}
 
 _lib = None
 

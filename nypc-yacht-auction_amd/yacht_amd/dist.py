@@ -48,6 +48,24 @@ def allgather_records(buf: torch.Tensor) -> torch.Tensor:
     return out
 
 
+def allreduce_grads(trainer) -> None:
+    """DDP gradient averaging for the native trainer: one all-reduce of the flat
+    gradient buffer (state_dict order) between yk_trainer_backward and yk_trainer_apply, so
+    every rank clips and steps on the same mean gradient, as torch DDP does.  RCCL works on the
+    device buffer in place; gloo goes through a host copy."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return
+    g = trainer.grads()
+    w = dist.get_world_size()
+    if dist.get_backend() == "nccl":
+        dist.all_reduce(g)
+        g.div_(w)
+    else:
+        h = g.cpu()
+        dist.all_reduce(h)
+        g.copy_(h.div_(w))
+
+
 def env_base(rank: int, envs_per_rank: int) -> int:
     """Global env id of this rank's first game: results do not depend on the GPU count."""
     return rank * envs_per_rank

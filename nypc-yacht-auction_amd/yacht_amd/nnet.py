@@ -1,9 +1,10 @@
-"""YachtNNet weights (torch) + NNetWrapper.predict on the MI355X f32-MFMA kernels.
+"""YachtNNet weights (torch) + NNetWrapper.predict / train on the MI355X.
 
 ``YachtNNet`` repeats the reference architecture (yacht/pytorch/YachtNNet.py:8-70) so its
 ``state_dict`` names and initialisation match; torch only holds the weights.  Inference
 (``NNetWrapper.predict``, NNet.py:177-195) runs through ``yk_net_predict`` - featurize,
-13 dense layers, both heads and exp(log_softmax) on the GPU.
+13 dense layers, both heads and exp(log_softmax) on the GPU; ``NNetWrapper.train``
+(NNet.py:118-174) through the native trainer (train.py, yk_trainer_*).
 """
 from __future__ import annotations
 
@@ -22,7 +23,7 @@ from .state import ACTION_SIZE, pack
 from .utils import dotdict
 
 DEFAULT_ARGS = dotdict(dict(lr=2e-3, weight_decay=1e-4, epochs=15, batch_size=512, vloss_weight=1.5,
-                            cuda=True, hidden=256, nblocks=6, dropout=0.3))
+                            cuda=True, hidden=256, nblocks=6, dropout=0.3))  # main.py:31-42
 
 
 class ResidualBlock(nn.Module):  # YachtNNet.py:8-21
@@ -134,18 +135,68 @@ class NNetWrapper:
     def predict_batch(self, states: torch.Tensor):
         return self.yk_net().predict_states(states)
 
-    def train(self, examples):
-        raise NotImplementedError("NNetWrapper.train (NNet.py:118-174) is the next row of the build (SURVEY 8f f1)")
+    # ---- training (NNet.py:118-174) on the native trainer (yacht_amd/train.py)
+    def _trainer(self):
+        from .train import Trainer
+        if getattr(self, "_tr", None) is None:
+            a = self.args
+            self._tr = Trainer(self.nnet.state_dict(), a.hidden, a.nblocks, lr=a.lr, weight_decay=a.weight_decay,
+                               max_batch=a.batch_size, vloss_weight=a.get("vloss_weight", 1.0),
+                               dropout=a.dropout, seed=a.get("seed", 0))
+        return self._tr
 
-    def save_checkpoint(self, folder="checkpoint", filename="checkpoint.pth.tar"):  # NNet.py:198-205
+    def train(self, examples, verbose=True):
+        """The reference loop: `epochs` passes over shuffled minibatches of `batch_size`
+        (drop_last False), one CE(argmax pi) + vloss_weight * MSE step each, clip 5.0, AdamW.
+        Shuffles come from a torch generator seeded per call (the reference uses the global
+        torch RNG); dropout masks from the trainer's Philox stream."""
+        from .train import examples_to_device
+        tr = self._trainer()
+        states, targets, values = examples_to_device(examples)
+        n = states.shape[0]
+        bs = self.args.batch_size
+        g = torch.Generator(device="cuda")
+        g.manual_seed(int(self.args.get("seed", 0)) + 1000003 * tr.step_count)
+        for epoch in range(self.args.epochs):
+            perm = torch.randperm(n, generator=g, device="cuda").to(torch.int32)
+            report = verbose and (epoch % 5 == 0 or epoch == self.args.epochs - 1)
+            total, count = 0.0, 0
+            for i in range(0, n, bs):
+                idx = perm[i:i + bs]
+                tr.step(states, targets, values, idx=idx)
+                if report:
+                    ce, se, _ = tr.losses()
+                    b = idx.numel()
+                    total += ce / b + self.args.get("vloss_weight", 1.0) * se / b
+                    count += 1
+            if report:
+                print(f"Epoch {epoch + 1}/{self.args.epochs}, Avg Loss: {total / max(count, 1):.4f}")
+        with torch.no_grad():
+            self.nnet.load_state_dict(tr.state_dict())  # the torch copy feeds checkpoints and predict
+        self._yk = None
+
+    # ---- checkpoints (NNet.py:198-213): the reference's dict, loaded without unpickling code
+    def save_checkpoint(self, folder="checkpoint", filename="checkpoint.pth.tar"):
+        from .train import optimizer_state_dict
         os.makedirs(folder, exist_ok=True)
-        torch.save({"state_dict": self.nnet.state_dict(), "args": dict(self.args)}, os.path.join(folder, filename))
+        if getattr(self, "_tr", None) is not None:
+            opt = optimizer_state_dict(self._tr, self.nnet, self.args.lr, self.args.weight_decay)
+        else:
+            opt = torch.optim.AdamW(self.nnet.parameters(), lr=self.args.lr,
+                                    weight_decay=self.args.weight_decay).state_dict()
+        torch.save({"state_dict": self.nnet.state_dict(), "optimizer": opt, "args": dict(self.args)},
+                   os.path.join(folder, filename))
 
-    def load_checkpoint(self, folder="checkpoint", filename="checkpoint.pth.tar"):  # NNet.py:207-213
+    def load_checkpoint(self, folder="checkpoint", filename="checkpoint.pth.tar", load_optimizer=False):
+        from .train import load_optimizer_state_dict
         ck = torch.load(os.path.join(folder, filename), map_location="cpu", weights_only=True)
         sd = ck["state_dict"] if "state_dict" in ck else ck
         self.nnet.load_state_dict(OrderedDict(sd))
         self._yk = None
+        if getattr(self, "_tr", None) is not None:
+            self._tr.load_params(self.nnet.state_dict())
+        if load_optimizer and "optimizer" in ck:
+            load_optimizer_state_dict(self._trainer(), self.nnet, ck["optimizer"])
 
 
 class HashPriorNet:

@@ -393,6 +393,40 @@ def make_greedy(seed=31):
                 draws=np.array(drew, dtype=np.int32))
 
 
+def make_train(seed=5, n=64, hidden=64, nblocks=1):
+    """The reference NNetWrapper.train (NNet.py:118-174) for one epoch of one batch (dropout 0,
+    CPU float32): closed-form initial weights, n fixture boards, sparse policies (3 entries,
+    ties included), values; records the parameters after the AdamW step."""
+    import torch
+    from utils import dotdict
+    from yacht.NNet import NNetWrapper
+    game = YachtGame()
+    args = dotdict(dict(lr=2e-3, weight_decay=1e-4, epochs=1, batch_size=n, vloss_weight=1.5, cuda=False,
+                        hidden=hidden, nblocks=nblocks, dropout=0.0))
+    w = NNetWrapper(game, args)
+    sd = spec.closed_form_weights(hidden, nblocks)
+    w.nnet.load_state_dict({k: torch.tensor(np.asarray(v, dtype=np.float32)) for k, v in sd.items()})
+    rng = np.random.RandomState(seed)
+    st = np.load(os.path.join(HERE, "states.npz"))["states"]
+    pick = rng.choice(len(st), n, replace=False)
+    pidx = np.stack([rng.choice(3226, 3, replace=False) for _ in range(n)]).astype(np.int32)
+    pval = rng.rand(n, 3).astype(np.float32)
+    pval[::7, 1] = pval[::7, 0]  # ties: argmax takes the first
+    vals = (rng.rand(n) * 2 - 1).astype(np.float32)
+    examples = []
+    for i in range(n):
+        pi = np.zeros(3226, dtype=np.float32)
+        pi[pidx[i]] = pval[i]
+        examples.append((to_ref_state(st[pick[i]]), pi, float(vals[i])))
+    torch.manual_seed(seed)
+    w.train(examples)
+    out = dict(seed=np.int64(seed), hidden=np.int64(hidden), nblocks=np.int64(nblocks), states=st[pick], pidx=pidx,
+               pval=pval, values=vals)
+    for k, v in w.nnet.state_dict().items():
+        out["after/" + k] = v.detach().numpy()
+    return out
+
+
 def make_players():
     np.savez_compressed(os.path.join(HERE, "greedy.npz"), **make_greedy())
     np.savez_compressed(os.path.join(HERE, "arena_greedy_random.npz"),
@@ -433,6 +467,10 @@ def pack_episodes(eps):
 
 def main():
     t0 = time.time()
+    if len(sys.argv) > 1 and sys.argv[1] == "train":
+        np.savez_compressed(os.path.join(HERE, "train_h64_b1.npz"), **make_train())
+        print(f"train fixture in {time.time() - t0:.1f}s")
+        return
     if len(sys.argv) > 1 and sys.argv[1] == "arena":
         np.savez_compressed(os.path.join(HERE, "arena_hash.npz"), **make_arena())
         make_players()
@@ -465,6 +503,7 @@ def main():
     np.savez_compressed(os.path.join(HERE, "episodes_hash.npz"), **pack_episodes(eps))
     np.savez_compressed(os.path.join(HERE, "arena_hash.npz"), **make_arena())
     make_players()
+    np.savez_compressed(os.path.join(HERE, "train_h64_b1.npz"), **make_train())
     print(f"done in {time.time() - t0:.1f}s")
 
 

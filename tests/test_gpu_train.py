@@ -1,0 +1,195 @@
+"""GPU parity of the native trainer (NNetWrapper.train, NNet.py:118-174).
+
+* against the REFERENCE's own train() (tests/golden/train_h64_b1.npz: one AdamW step on one
+  batch, dropout 0, CPU float32);
+* against a plain torch fp32 step of the same architecture at hidden 256 x 6 blocks, over three
+  steps: losses, clipped gradients, parameters and both Adam moments;
+* dropout determinism, the NNetWrapper train / checkpoint round trip, and DDP gradient
+  averaging (2 processes, gloo) equal to one process on the union of the shards.
+Tolerances: f32 reductions in a different order (rocBLAS / torch CPU), amplified on the first
+Adam step only where |grad| ~ eps; stated per test."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import spec
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def T():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from yacht_amd import kernels as K
+    from yacht_amd import nnet, train
+    return K, nnet, train
+
+
+def _sd(hidden, nblocks):
+    return {k: torch.tensor(np.asarray(v, dtype=np.float32)) for k, v in spec.closed_form_weights(hidden, nblocks).items()}
+
+
+def _dense_targets(pidx, pval):
+    n = len(pidx)
+    pi = np.zeros((n, 3226), dtype=np.float32)
+    for i in range(n):
+        pi[i, pidx[i]] = pval[i]
+    return np.argmax(pi, axis=1).astype(np.int32)
+
+
+def test_one_step_matches_reference_train(T, golden):
+    K, N, TR = T
+    g = golden("train_h64_b1.npz")
+    H, NB = int(g["hidden"]), int(g["nblocks"])
+    n = len(g["values"])
+    tr = TR.Trainer(_sd(H, NB), H, NB, lr=2e-3, weight_decay=1e-4, max_batch=n, vloss_weight=1.5, dropout=0.0)
+    S = K.states_to_device(g["states"])
+    t = torch.tensor(_dense_targets(g["pidx"], g["pval"]), device="cuda")
+    v = torch.tensor(g["values"], device="cuda")
+    tr.step(S, t, v)
+    after = tr.state_dict()
+    for k, ref in after.items():
+        np.testing.assert_allclose(ref.numpy(), g["after/" + k], rtol=1e-4, atol=2e-6, err_msg=k)
+
+
+def _torch_step_reference(model, opt, x, t, v, vw=1.5):
+    import torch.nn.functional as F
+    opt.zero_grad(set_to_none=True)
+    out_pi, out_v = model(x)
+    lp = F.cross_entropy(out_pi, t.long())
+    lv = F.mse_loss(out_v, v.reshape(-1, 1))
+    loss = lp + vw * lv
+    loss.backward()
+    torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=5.0)
+    opt.step()
+    return float(lp), float(lv)
+
+
+def test_three_steps_vs_torch_fp32(T, golden):
+    K, N, TR = T
+    H, NB, B = 256, 6, 128
+    torch.manual_seed(3)
+    model = N.YachtNNet(hidden=H, nblocks=NB, dropout=0.0).cuda().float().train()
+    with torch.no_grad():
+        for m in model.modules():
+            if isinstance(m, torch.nn.LayerNorm):
+                m.weight.uniform_(0.5, 1.5)
+                m.bias.uniform_(-0.2, 0.2)
+    sd0 = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
+    opt = torch.optim.AdamW(model.parameters(), lr=2e-3, weight_decay=1e-4)
+    tr = TR.Trainer(sd0, H, NB, lr=2e-3, weight_decay=1e-4, max_batch=B, vloss_weight=1.5, dropout=0.0)
+    W = golden("states.npz")["states"]
+    rng = np.random.RandomState(0)
+    torch.backends.cuda.matmul.allow_tf32 = False
+    S = K.states_to_device(W[:3 * B])
+    X = K.featurize(S)
+    tg = torch.tensor(rng.randint(0, 3226, 3 * B), dtype=torch.int32, device="cuda")
+    vv = torch.tensor(rng.rand(3 * B) * 2 - 1, dtype=torch.float32, device="cuda")
+    for k in range(3):
+        sl = slice(k * B, (k + 1) * B)
+        idx = torch.arange(k * B, (k + 1) * B, dtype=torch.int32, device="cuda")
+        tr.step(S, tg, vv, idx=idx)
+        lp, lv = _torch_step_reference(model, opt, X[sl], tg[sl], vv[sl])
+        ce, se, _ = tr.losses()
+        assert abs(ce / B - lp) <= 1e-5 * abs(lp) + 1e-6 and abs(se / B - lv) <= 1e-5 * abs(lv) + 1e-6
+    grads = tr.gradients()  # clipped, of the last step
+    for name, p in model.named_parameters():
+        np.testing.assert_allclose(grads[name].numpy(), p.grad.detach().cpu().numpy(), rtol=2e-3, atol=2e-7,
+                                   err_msg="grad " + name)
+    params = tr.state_dict()
+    m, v2 = tr.moments()
+    for i, (name, p) in enumerate(model.named_parameters()):
+        np.testing.assert_allclose(params[name].numpy(), p.detach().cpu().numpy(), rtol=1e-4, atol=5e-6,
+                                   err_msg="param " + name)
+        st = opt.state[p]
+        np.testing.assert_allclose(m[name].numpy(), st["exp_avg"].cpu().numpy(), rtol=2e-3, atol=1e-7)
+        np.testing.assert_allclose(v2[name].numpy(), st["exp_avg_sq"].cpu().numpy(), rtol=4e-3, atol=1e-12)
+    assert tr.step_count == 3
+
+
+def test_dropout_masks_are_deterministic_and_active(T, golden):
+    K, N, TR = T
+    H, NB, B = 64, 2, 64
+    sd = _sd(H, NB)
+    W = golden("states.npz")["states"][:B]
+    S = K.states_to_device(W)
+    tg = torch.zeros(B, dtype=torch.int32, device="cuda")
+    vv = torch.zeros(B, dtype=torch.float32, device="cuda")
+    res = []
+    for p, seed in ((0.3, 7), (0.3, 7), (0.3, 8), (0.0, 7)):
+        tr = TR.Trainer(sd, H, NB, max_batch=B, dropout=p, seed=seed)
+        tr.backward(S, tg, vv)
+        res.append(tr.gradients()["inp.0.weight"].numpy())
+    assert np.array_equal(res[0], res[1])
+    assert not np.allclose(res[0], res[2]) and not np.allclose(res[0], res[3])
+
+
+def test_nnetwrapper_train_and_checkpoint(T, tmp_path):
+    K, N, TR = T
+    from yacht_amd.coach import Coach
+    from yacht_amd.game import YachtGame
+    from yacht_amd.nnet import HashPriorNet, NNetWrapper
+    from yacht_amd.utils import dotdict
+    game = YachtGame(seed=1, env_id=0)
+    coach = Coach(game, HashPriorNet(game), dotdict(numMCTSSims=4, cpuct=1.5, tempThreshold=15))
+    examples = [ex for ep in coach.executeEpisodes(4) for ex in ep]
+    args = dotdict(lr=2e-3, weight_decay=1e-4, epochs=2, batch_size=64, vloss_weight=1.5, cuda=True, hidden=64,
+                   nblocks=1, dropout=0.3)
+    w = NNetWrapper(game, args)
+    pi0, _ = w.predict(examples[0][0])
+    w.train(examples, verbose=False)
+    pi1, v1 = w.predict(examples[0][0])
+    assert not np.allclose(pi0, pi1)
+    steps = -(-len(examples) // 64) * 2
+    assert w._trainer().step_count == steps
+    w.save_checkpoint(str(tmp_path), "best.pth.tar")
+    ck = torch.load(os.path.join(tmp_path, "best.pth.tar"), map_location="cpu", weights_only=True)
+    assert set(ck) == {"state_dict", "optimizer", "args"} and len(ck["optimizer"]["state"]) == len(ck["state_dict"])
+    w2 = NNetWrapper(game, args)
+    w2.load_checkpoint(str(tmp_path), "best.pth.tar", load_optimizer=True)
+    pi2, v2 = w2.predict(examples[0][0])
+    assert np.array_equal(pi1, pi2) and v1 == v2
+    m1, s1 = w._trainer().moments()
+    m2, s2 = w2._trainer().moments()
+    assert all(torch.equal(m1[k], m2[k]) and torch.equal(s1[k], s2[k]) for k in m1)
+    assert w2._trainer().step_count == steps
+
+
+def _ddp_worker(rank, world, port, H, NB, B, W, tg, vv, out):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "nypc-yacht-auction_amd"))
+    from yacht_amd import kernels as K
+    from yacht_amd.dist import allreduce_grads
+    from yacht_amd.train import Trainer
+    tr = Trainer(_sd(H, NB), H, NB, max_batch=B, dropout=0.0)
+    sl = slice(rank * B, (rank + 1) * B)
+    S = K.states_to_device(W[sl])
+    tr.backward(S, torch.tensor(tg[sl], device="cuda"), torch.tensor(vv[sl], device="cuda"))
+    allreduce_grads(tr)
+    tr.apply()
+    out[rank] = tr.params().cpu().numpy().copy()
+    dist.destroy_process_group()
+
+
+def test_ddp_gradient_average_equals_union_batch(T, golden):
+    import torch.multiprocessing as mp
+    K, N, TR = T
+    H, NB, B = 64, 1, 32
+    W = golden("states.npz")["states"][:2 * B]
+    rng = np.random.RandomState(1)
+    tg = rng.randint(0, 3226, 2 * B).astype(np.int32)
+    vv = (rng.rand(2 * B) * 2 - 1).astype(np.float32)
+    mgr = mp.get_context("spawn").Manager()
+    out = mgr.dict()
+    mp.start_processes(_ddp_worker, args=(2, 29577, H, NB, B, W, tg, vv, out), nprocs=2, start_method="spawn")
+    ref = TR.Trainer(_sd(H, NB), H, NB, max_batch=2 * B, dropout=0.0)
+    ref.step(K.states_to_device(W), torch.tensor(tg, device="cuda"), torch.tensor(vv, device="cuda"))
+    single = ref.params().cpu().numpy()
+    assert np.array_equal(out[0], out[1])
+    np.testing.assert_allclose(out[0], single, rtol=1e-5, atol=1e-6)
