@@ -107,6 +107,49 @@ def arena_leg(net, games=1000, sims=25, seed=0, reps=3):
     return out
 
 
+def train_leg(model_sd, eng, steps=40, batch=512, seed=0):
+    """Config 5's train step on one GPU (NNetWrapper.train semantics, NNet.py:118-174): minibatches
+    of 512 replay entries drawn from the self-play records just produced (packed boards, argmax
+    of the visit counts, values), forward + backward + clip + AdamW in f32, dropout 0.3."""
+    import numpy as np
+    import torch
+
+    from yacht_amd import kernels as K
+    from yacht_amd.train import Trainer
+    rec = eng.records()
+    E, M = rec["n_moves"].shape[0], rec["states"].shape[1]
+    ok = np.arange(M)[None, :] < rec["n_moves"][:, None]
+    states = rec["states"][ok]
+    # hard targets: the chosen action for temp-0 moves, else the first most-visited action
+    info = rec["info"][ok]
+    tg = info[:, 2].astype(np.int32)
+    vals = rec["values"][ok].astype(np.float32)
+    S = K.states_to_device(states)
+    T = torch.tensor(tg, device="cuda")
+    V = torch.tensor(vals, device="cuda")
+    n = S.shape[0]
+    tr = Trainer(model_sd, H, NB, max_batch=batch, dropout=0.3, seed=seed)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(seed)
+    perm = torch.randperm(n, generator=g, device="cuda").to(torch.int32)
+    for i in range(3):  # warm-up (rocBLAS kernel selection)
+        tr.step(S, T, V, idx=perm[i * batch:(i + 1) * batch])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        j = (i * batch) % (n - batch)
+        tr.step(S, T, V, idx=perm[j:j + batch])
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    ce, se, _ = tr.losses()
+    tr.close()
+    flop = 3 * PREDICT_FLOP * batch  # forward + backward (2x) per example
+    return {"config": f"minibatch {batch} of {n} self-play examples, YachtNNet hidden {H} x {NB}, f32, "
+                      f"AdamW + clip 5.0, dropout 0.3 (rocBLAS GEMMs + fused HIP row kernels)",
+            "ms_per_step": 1000.0 * dt, "examples_per_s": batch / dt, "achieved_tflops": flop / dt / 1e12,
+            "last_loss": ce / batch + 1.5 * se / batch}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -118,6 +161,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel event timing")
     ap.add_argument("--no-arena", action="store_true", help="skip the config-4 Arena leg")
+    ap.add_argument("--no-train", action="store_true", help="skip the config-5 train-step leg")
     ap.add_argument("--dist-backend", default=None, help="nccl (RCCL, default on GPUs) or gloo (rehearsal)")
     args = ap.parse_args()
 
@@ -242,6 +286,8 @@ def main():
                                "work_per_launch": f"{b:.0f} algorithmic bytes"}
     if world == 1 and not args.no_arena:
         out["arena"] = arena_leg(net, seed=args.seed)
+    if world == 1 and not args.no_train:
+        out["train"] = train_leg(sd, eng, seed=args.seed)
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(sd, args.sims)
     print(json.dumps(out), flush=True)

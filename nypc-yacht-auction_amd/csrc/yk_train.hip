@@ -180,26 +180,37 @@ __global__ void k_heads_fwd(const float* Hh, const float* gp, const float* bp, c
 //   Zv1 += bv1 (saved); v = tanh(silu(Zv1) . wv2 + bv2); mse_i = (v - z)^2
 //   logits += bpi; ce_i = lse - logit[t]; dlogits = (softmax - onehot(t)) / B
 //   dzv2 = vw * 2 (v - z) / B * (1 - v^2); dZv1 = dzv2 wv2 silu'(Zv1)
-__global__ void k_loss(float* logits, const float* bpi, float* Zv1, const float* bv1, const float* wv2, const float* bv2,
-                       const int32_t* tgt, const float* vt, float* dlogits, float* dZv1, float* dzv2, float* vout,
-                       double* loss_acc, int B, int A, float vw) {
+constexpr int LOSS_NV = (ASIZE + 63) / 64;  // logits per lane
+__global__ void k_loss(const float* logits, const float* bpi, float* Zv1, const float* bv1, const float* wv2,
+                       const float* bv2, const int32_t* tgt, const float* vt, float* dlogits, float* dZv1, float* dzv2,
+                       float* v2prod, float* vout, double* loss_acc, int B, int A, float vw) {
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (row >= B) return;
-    float* z = logits + (long)row * A;
+    const float* z = logits + (long)row * A;
+    float x[LOSS_NV];
     float m = -INFINITY;
-    for (int a = lane; a < A; a += 64) {
-        const float x = z[a] + bpi[a];
-        z[a] = x;
-        m = fmaxf(m, x);
+#pragma unroll
+    for (int k = 0; k < LOSS_NV; k++) {
+        const int a = lane + 64 * k;
+        x[k] = a < A ? z[a] + bpi[a] : -INFINITY;
+        m = fmaxf(m, x[k]);
     }
     m = wmax(m);
     float se = 0.f;
-    for (int a = lane; a < A; a += 64) se += expf(z[a] - m);
+#pragma unroll
+    for (int k = 0; k < LOSS_NV; k++) se += expf(x[k] - m);
     se = wsum(se);
     const float lse = m + logf(se);
     const int t = tgt[row];
     const float invB = 1.0f / (float)B;
-    for (int a = lane; a < A; a += 64) dlogits[(long)row * A + a] = (expf(z[a] - lse) - (a == t ? 1.0f : 0.0f)) * invB;
+    float zt = 0.f;
+#pragma unroll
+    for (int k = 0; k < LOSS_NV; k++) {
+        const int a = lane + 64 * k;
+        if (a < A) dlogits[(long)row * A + a] = (expf(x[k] - lse) - (a == t ? 1.0f : 0.0f)) * invB;
+        if (a == t) zt = x[k];
+    }
+    zt = wsum(zt);  // exactly one lane holds the target logit
     // value head tail (128 hidden, 2 per lane)
     float s = 0.f, zz[2];
 #pragma unroll
@@ -217,11 +228,12 @@ __global__ void k_loss(float* logits, const float* bpi, float* Zv1, const float*
     for (int k = 0; k < 2; k++) {
         const int c = 2 * lane + k;
         dZv1[(long)row * 128 + c] = dv * wv2[c] * silu_grad(zz[k]);
+        v2prod[(long)row * 128 + c] = dv * silu_f(zz[k]);  // rows of dL/d v_head.4.weight
     }
     if (lane == 0) {
         dzv2[row] = dv;
         vout[row] = v;
-        atomicAdd(&loss_acc[0], (double)(lse - z[t]));
+        atomicAdd(&loss_acc[0], (double)(lse - zt));
         atomicAdd(&loss_acc[1], (double)(e * e));
     }
 }
@@ -309,25 +321,37 @@ __global__ void k_inp_bwd(const float* dH0, const uint8_t* mask, float p, const 
 #pragma unroll
     for (int i = 0; i < VPL; i++) dZ[(long)row * H + c0 + i] = d[i];
 }
-// out[c] = sum_r in[r * N + c] (column sums), one thread per column
-__global__ void k_colsum(const float* in, float* out, int B, int N) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= N) return;
-    float s = 0.f;
-    for (int r = 0; r < B; r++) s += in[(long)r * N + c];
-    out[c] = s;
-}
-// dwv2[c] = sum_r dzv2[r] * silu(Zv1[r][c]); dbv2 = sum_r dzv2[r]
-__global__ void k_v2_grad(const float* dzv2, const float* Zv1, float* dw, float* db, int B) {
-    const int c = threadIdx.x;  // 128 threads (+1 for the bias)
-    if (c < 128) {
+// Every column reduction of a step in one launch: job j sums the B rows of src[j] ([B][N_j])
+// into dst[j][N_j] (bias and LayerNorm gradients).  Block = one 16-column tile of one job, 16
+// row groups x 16 columns, fixed order (deterministic).
+struct ColJob {
+    const float* src;
+    float* dst;
+    int N;
+};
+__global__ __launch_bounds__(256) void k_colsums(const ColJob* jobs, const int2* tiles, int B) {
+    __shared__ float part[16][17];
+    const int2 t = tiles[blockIdx.x];  // (job, first column)
+    const ColJob jb = jobs[t.x];
+    const int c = t.y + (threadIdx.x & 15), g = threadIdx.x >> 4;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    if (c < jb.N) {
+        int r = g;
+        for (; r + 48 < B; r += 64) {
+            a0 += jb.src[(long)r * jb.N + c];
+            a1 += jb.src[(long)(r + 16) * jb.N + c];
+            a2 += jb.src[(long)(r + 32) * jb.N + c];
+            a3 += jb.src[(long)(r + 48) * jb.N + c];
+        }
+        for (; r < B; r += 16) a0 += jb.src[(long)r * jb.N + c];
+    }
+    part[g][threadIdx.x & 15] = (a0 + a1) + (a2 + a3);
+    __syncthreads();
+    if (g == 0 && c < jb.N) {
         float s = 0.f;
-        for (int r = 0; r < B; r++) s += dzv2[r] * silu_f(Zv1[(long)r * 128 + c]);
-        dw[c] = s;
-    } else if (c == 128) {
-        float s = 0.f;
-        for (int r = 0; r < B; r++) s += dzv2[r];
-        db[0] = s;
+#pragma unroll
+        for (int k = 0; k < 16; k++) s += part[k][threadIdx.x & 15];
+        jb.dst[c] = s;
     }
 }
 // gather a minibatch: features of states[idx[i]], targets, values
@@ -415,8 +439,13 @@ struct yk_trainer {
     std::vector<uint8_t*> mask1;
     float *Api = nullptr, *Av = nullptr, *mup = nullptr, *rsp = nullptr, *muv = nullptr, *rsv = nullptr;
     float *logits = nullptr, *Zv1 = nullptr, *dlogits = nullptr, *dZv1 = nullptr, *dzv2 = nullptr;
-    float *dA = nullptr, *dAv = nullptr, *dH = nullptr, *dT = nullptr, *dU = nullptr, *rg = nullptr, *rb = nullptr,
-          *rg2 = nullptr, *rb2 = nullptr;
+    float *dA = nullptr, *dAv = nullptr, *dH = nullptr, *dT = nullptr, *v2prod = nullptr;
+    // per-stage row buffers whose column sums are gradients (kept until the one k_colsums)
+    float *rgp = nullptr, *rbp = nullptr, *rgv = nullptr, *rbv = nullptr, *dZ0 = nullptr, *rg0 = nullptr, *rb0 = nullptr;
+    std::vector<float*> dU1, dU2, rg1, rb1, rg2, rb2;
+    ColJob* jobs = nullptr;
+    int2* tiles = nullptr;
+    int ntiles = 0;
     double* acc = nullptr;  // [0] ce sum, [1] mse sum, [2] grad sq norm
     double host_loss[3] = {0, 0, 0};
 };
@@ -485,62 +514,41 @@ int step_impl(yk_trainer* t, const yk_state_t* states, const int32_t* targets, c
     YK_LAUNCHED();
     if ((rc = gemm_rm(t, false, true, B, A, H, t->Api, H, Pt(t_head(NB, 2)), H, t->logits, A, 0.f))) return rc;
     if ((rc = gemm_rm(t, false, true, B, 128, H, t->Av, H, Pt(t_head(NB, 6)), H, t->Zv1, 128, 0.f))) return rc;
-    hipLaunchKernelGGL(k_loss, rows, wave4, 0, s, t->logits, Pt(t_head(NB, 3)), t->Zv1, Pt(t_head(NB, 7)), Pt(t_head(NB, 8)),
-                       Pt(t_head(NB, 9)), t->tgt, t->vt, t->dlogits, t->dZv1, t->dzv2, t->vout, t->acc, B, A,
-                       t->cfg.vloss_weight);
+    hipLaunchKernelGGL(k_loss, rows, wave4, 0, s, t->logits, Pt(t_head(NB, 3)), t->Zv1, Pt(t_head(NB, 7)),
+                       Pt(t_head(NB, 8)), Pt(t_head(NB, 9)), t->tgt, t->vt, t->dlogits, t->dZv1, t->dzv2, t->v2prod,
+                       t->vout, t->acc, B, A, t->cfg.vloss_weight);
     YK_LAUNCHED();
-    // ---- backward: heads
+    // ---- backward: heads (bias / LayerNorm gradients are column sums, taken at the end)
     if ((rc = gemm_rm(t, true, false, A, H, B, t->dlogits, A, t->Api, H, Gt(t_head(NB, 2)), H, 0.f))) return rc;
-    hipLaunchKernelGGL(k_colsum, dim3((A + 255) / 256), dim3(256), 0, s, t->dlogits, Gt(t_head(NB, 3)), B, A);
-    YK_LAUNCHED();
     if ((rc = gemm_rm(t, false, false, B, H, A, t->dlogits, A, Pt(t_head(NB, 2)), H, t->dA, H, 0.f))) return rc;
-    hipLaunchKernelGGL(k_v2_grad, dim3(1), dim3(192), 0, s, t->dzv2, t->Zv1, Gt(t_head(NB, 8)), Gt(t_head(NB, 9)), B);
-    YK_LAUNCHED();
     if ((rc = gemm_rm(t, true, false, 128, H, B, t->dZv1, 128, t->Av, H, Gt(t_head(NB, 6)), H, 0.f))) return rc;
-    hipLaunchKernelGGL(k_colsum, dim3(1), dim3(128), 0, s, t->dZv1, Gt(t_head(NB, 7)), B, 128);
-    YK_LAUNCHED();
     if ((rc = gemm_rm(t, false, false, B, H, 128, t->dZv1, 128, Pt(t_head(NB, 6)), H, t->dAv, H, 0.f))) return rc;
     hipLaunchKernelGGL(k_heads_bwd<VPL>, rows, wave4, 0, s, Hh, Pt(t_head(NB, 0)), Pt(t_head(NB, 1)), Pt(t_head(NB, 4)),
-                       Pt(t_head(NB, 5)), t->mup, t->rsp, t->muv, t->rsv, t->dA, t->dAv, t->dH, t->rg, t->rb, t->rg2,
-                       t->rb2, B);
-    YK_LAUNCHED();
-    const dim3 cs((H + 255) / 256), cb(256);
-    hipLaunchKernelGGL(k_colsum, cs, cb, 0, s, t->rg, Gt(t_head(NB, 0)), B, H);
-    hipLaunchKernelGGL(k_colsum, cs, cb, 0, s, t->rb, Gt(t_head(NB, 1)), B, H);
-    hipLaunchKernelGGL(k_colsum, cs, cb, 0, s, t->rg2, Gt(t_head(NB, 4)), B, H);
-    hipLaunchKernelGGL(k_colsum, cs, cb, 0, s, t->rb2, Gt(t_head(NB, 5)), B, H);
+                       Pt(t_head(NB, 5)), t->mup, t->rsp, t->muv, t->rsv, t->dA, t->dAv, t->dH, t->rgp, t->rbp, t->rgv,
+                       t->rbv, B);
     YK_LAUNCHED();
     // ---- blocks, last to first; t->dH holds dL/dH_{b+1}
     for (int b = NB - 1; b >= 0; b--) {
         hipLaunchKernelGGL(k_blk_bwd<VPL>, rows, wave4, 0, s, t->dH, (const uint8_t*)nullptr, 0.f, t->U2[b],
-                           Pt(t_blk(b, 6)), t->mu2[b], t->rs2[b], t->dU, t->rg, t->rb, B);
+                           Pt(t_blk(b, 6)), t->mu2[b], t->rs2[b], t->dU2[b], t->rg2[b], t->rb2[b], B);
         YK_LAUNCHED();
-        hipLaunchKernelGGL(k_colsum, cs, cb, 0, s, t->rg, Gt(t_blk(b, 6)), B, H);
-        hipLaunchKernelGGL(k_colsum, cs, cb, 0, s, t->rb, Gt(t_blk(b, 7)), B, H);
-        hipLaunchKernelGGL(k_colsum, cs, cb, 0, s, t->dU, Gt(t_blk(b, 5)), B, H);
-        YK_LAUNCHED();
-        if ((rc = gemm_rm(t, true, false, H, H, B, t->dU, H, t->R1[b], H, Gt(t_blk(b, 4)), H, 0.f))) return rc;
-        if ((rc = gemm_rm(t, false, false, B, H, H, t->dU, H, Pt(t_blk(b, 4)), H, t->dT, H, 0.f))) return rc;  // dR1
+        if ((rc = gemm_rm(t, true, false, H, H, B, t->dU2[b], H, t->R1[b], H, Gt(t_blk(b, 4)), H, 0.f))) return rc;
+        if ((rc = gemm_rm(t, false, false, B, H, H, t->dU2[b], H, Pt(t_blk(b, 4)), H, t->dT, H, 0.f))) return rc;  // dR1
         hipLaunchKernelGGL(k_blk_bwd<VPL>, rows, wave4, 0, s, t->dT, t->mask1[b], p, t->U1[b], Pt(t_blk(b, 2)), t->mu1[b],
-                           t->rs1[b], t->dU, t->rg, t->rb, B);
+                           t->rs1[b], t->dU1[b], t->rg1[b], t->rb1[b], B);
         YK_LAUNCHED();
-        hipLaunchKernelGGL(k_colsum, cs, cb, 0, s, t->rg, Gt(t_blk(b, 2)), B, H);
-        hipLaunchKernelGGL(k_colsum, cs, cb, 0, s, t->rb, Gt(t_blk(b, 3)), B, H);
-        hipLaunchKernelGGL(k_colsum, cs, cb, 0, s, t->dU, Gt(t_blk(b, 1)), B, H);
-        YK_LAUNCHED();
-        if ((rc = gemm_rm(t, true, false, H, H, B, t->dU, H, t->Hs[b], H, Gt(t_blk(b, 0)), H, 0.f))) return rc;
+        if ((rc = gemm_rm(t, true, false, H, H, B, t->dU1[b], H, t->Hs[b], H, Gt(t_blk(b, 0)), H, 0.f))) return rc;
         // dH_b = dH_{b+1} (residual) + dU1 . W1
-        if ((rc = gemm_rm(t, false, false, B, H, H, t->dU, H, Pt(t_blk(b, 0)), H, t->dH, H, 1.f))) return rc;
+        if ((rc = gemm_rm(t, false, false, B, H, H, t->dU1[b], H, Pt(t_blk(b, 0)), H, t->dH, H, 1.f))) return rc;
     }
     // ---- input layer
     hipLaunchKernelGGL(k_inp_bwd<VPL>, rows, wave4, 0, s, t->dH, t->mask0, p, t->Z0, Pt(T_GIN), Pt(T_BEIN), t->mu0,
-                       t->rs0, t->dU, t->rg, t->rb, B);
+                       t->rs0, t->dZ0, t->rg0, t->rb0, B);
     YK_LAUNCHED();
-    hipLaunchKernelGGL(k_colsum, cs, cb, 0, s, t->rg, Gt(T_GIN), B, H);
-    hipLaunchKernelGGL(k_colsum, cs, cb, 0, s, t->rb, Gt(T_BEIN), B, H);
-    hipLaunchKernelGGL(k_colsum, cs, cb, 0, s, t->dU, Gt(T_BIN), B, H);
+    if ((rc = gemm_rm(t, true, false, H, FEAT, B, t->dZ0, H, t->X, FEAT, Gt(T_WIN), FEAT, 0.f))) return rc;
+    // ---- every bias / LayerNorm gradient: one launch of column sums
+    hipLaunchKernelGGL(k_colsums, dim3(t->ntiles), dim3(256), 0, s, t->jobs, t->tiles, B);
     YK_LAUNCHED();
-    if ((rc = gemm_rm(t, true, false, H, FEAT, B, t->dU, H, t->X, FEAT, Gt(T_WIN), FEAT, 0.f))) return rc;
     return YK_OK;
 }
 }  // namespace
@@ -610,9 +618,51 @@ int yk_trainer_create(yk_trainer_t** out, int H, int NB, const float* const* par
     TA(t->Zv1, Bm * 128);
     TA(t->dZv1, Bm * 128);
     TA(t->dzv2, Bm);
-    TA(t->dA, Bm * HH); TA(t->dAv, Bm * HH); TA(t->dH, Bm * HH); TA(t->dT, Bm * HH); TA(t->dU, Bm * HH);
-    TA(t->rg, Bm * HH); TA(t->rb, Bm * HH); TA(t->rg2, Bm * HH); TA(t->rb2, Bm * HH);
+    TA(t->dA, Bm * HH); TA(t->dAv, Bm * HH); TA(t->dH, Bm * HH); TA(t->dT, Bm * HH);
+    TA(t->v2prod, Bm * 128);
+    TA(t->rgp, Bm * HH); TA(t->rbp, Bm * HH); TA(t->rgv, Bm * HH); TA(t->rbv, Bm * HH);
+    TA(t->dZ0, Bm * HH); TA(t->rg0, Bm * HH); TA(t->rb0, Bm * HH);
+    t->dU1.assign(NB, nullptr); t->dU2.assign(NB, nullptr); t->rg1.assign(NB, nullptr); t->rb1.assign(NB, nullptr);
+    t->rg2.assign(NB, nullptr); t->rb2.assign(NB, nullptr);
+    for (int b = 0; b < NB; b++) {
+        TA(t->dU1[b], Bm * HH); TA(t->dU2[b], Bm * HH); TA(t->rg1[b], Bm * HH); TA(t->rb1[b], Bm * HH);
+        TA(t->rg2[b], Bm * HH); TA(t->rb2[b], Bm * HH);
+    }
     TA(t->acc, 3);
+    // the column-sum jobs: (row buffer, gradient tensor, width)
+    std::vector<ColJob> jobs;
+    if (rc == YK_OK) {
+        auto G = [&](int k) { return t->G + t->off[k]; };
+        jobs.push_back({t->dlogits, G(t_head(NB, 3)), ASIZE});
+        jobs.push_back({t->dZv1, G(t_head(NB, 7)), 128});
+        jobs.push_back({t->v2prod, G(t_head(NB, 8)), 128});
+        jobs.push_back({t->dzv2, G(t_head(NB, 9)), 1});
+        jobs.push_back({t->rgp, G(t_head(NB, 0)), H});
+        jobs.push_back({t->rbp, G(t_head(NB, 1)), H});
+        jobs.push_back({t->rgv, G(t_head(NB, 4)), H});
+        jobs.push_back({t->rbv, G(t_head(NB, 5)), H});
+        for (int b = 0; b < NB; b++) {
+            jobs.push_back({t->dU1[b], G(t_blk(b, 1)), H});
+            jobs.push_back({t->rg1[b], G(t_blk(b, 2)), H});
+            jobs.push_back({t->rb1[b], G(t_blk(b, 3)), H});
+            jobs.push_back({t->dU2[b], G(t_blk(b, 5)), H});
+            jobs.push_back({t->rg2[b], G(t_blk(b, 6)), H});
+            jobs.push_back({t->rb2[b], G(t_blk(b, 7)), H});
+        }
+        jobs.push_back({t->dZ0, G(T_BIN), H});
+        jobs.push_back({t->rg0, G(T_GIN), H});
+        jobs.push_back({t->rb0, G(T_BEIN), H});
+    }
+    std::vector<int2> tiles;
+    for (size_t j = 0; j < jobs.size(); j++)
+        for (int c = 0; c < jobs[j].N; c += 16) tiles.push_back(make_int2((int)j, c));
+    t->ntiles = (int)tiles.size();
+    TA(t->jobs, jobs.size());
+    TA(t->tiles, tiles.size());
+    if (rc == YK_OK) {
+        (void)hipMemcpy(t->jobs, jobs.data(), sizeof(ColJob) * jobs.size(), hipMemcpyHostToDevice);
+        (void)hipMemcpy(t->tiles, tiles.data(), sizeof(int2) * tiles.size(), hipMemcpyHostToDevice);
+    }
 #undef TA
     if (rc == YK_OK && rocblas_create_handle(&t->blas) != rocblas_status_success) rc = YK_ERR_HIP;
     if (rc != YK_OK) {
