@@ -19,6 +19,7 @@ class MCTS:
     def __init__(self, game, nnet, args):
         self.game, self.nnet, self.args = game, nnet, args
         self._engine = None
+        self._round = 0  # round of the last root: a lower one starts a new game (fresh tree)
 
     def _eng(self):
         if self._engine is None:
@@ -34,6 +35,11 @@ class MCTS:
         """Run `sims` searches from the root; return the root's visit counts (list)."""
         eng = self._eng()
         rng = self.game.rng
+        if canonicalBoard.round_no < self._round:
+            # a new game (Arena.playGames reuses one MCTS, Coach.py:124-125): the device trees
+            # only keep rounds >= the root's, so the new game starts from a fresh tree
+            call("yk_mcts_reset", eng.handle)
+        self._round = canonicalBoard.round_no
         roots = K.states_to_device(pack(canonicalBoard))
         env = torch.tensor([rng.env], dtype=torch.int32, device="cuda")
         ctr = torch.tensor([rng.ctr], dtype=torch.int64, device="cuda")

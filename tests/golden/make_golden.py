@@ -427,6 +427,31 @@ def make_train(seed=5, n=64, hidden=64, nblocks=1):
     return out
 
 
+def make_examples_pickle(seed=11, env=3, sims=4):
+    """A replay-buffer file exactly as Coach.saveTrainExamples writes it (Coach.py:144-153:
+    Pickler(f).dump(trainExamplesHistory), a list of per-iteration deques of (YachtState, pi, v))
+    from a reference Coach.executeEpisode, plus the expected decoded contents."""
+    from collections import deque
+    from pickle import Pickler
+    from utils import dotdict
+    from Coach import Coach
+    game = YachtGame()
+    set_stream(seed, env)
+    nnet = HashNet(game)
+    coach = Coach(game, nnet, dotdict(dict(numMCTSSims=sims, cpuct=1.5, tempThreshold=15)))
+    ex = coach.executeEpisode()
+    history = [deque(ex[:5], maxlen=200000), deque(ex[20:23], maxlen=200000)]
+    with open(os.path.join(HERE, "examples_ref.pkl"), "wb") as f:
+        Pickler(f).dump(history)
+    flat = [e for it in history for e in it]
+    pis = np.array([np.asarray(e[1], dtype=np.float64) for e in flat])
+    nz = np.nonzero(pis)
+    np.savez_compressed(os.path.join(HERE, "examples_ref_expected.npz"),
+                        states=np.array([words(e[0]) for e in flat], dtype=np.uint64),
+                        sizes=np.array([len(it) for it in history]), pi_rows=nz[0], pi_cols=nz[1], pi_vals=pis[nz],
+                        values=np.array([float(e[2]) for e in flat]))
+
+
 def make_players():
     np.savez_compressed(os.path.join(HERE, "greedy.npz"), **make_greedy())
     np.savez_compressed(os.path.join(HERE, "arena_greedy_random.npz"),
@@ -467,6 +492,10 @@ def pack_episodes(eps):
 
 def main():
     t0 = time.time()
+    if len(sys.argv) > 1 and sys.argv[1] == "examples":
+        make_examples_pickle()
+        print(f"examples fixture in {time.time() - t0:.1f}s")
+        return
     if len(sys.argv) > 1 and sys.argv[1] == "train":
         np.savez_compressed(os.path.join(HERE, "train_h64_b1.npz"), **make_train())
         print(f"train fixture in {time.time() - t0:.1f}s")
@@ -503,6 +532,7 @@ def main():
     np.savez_compressed(os.path.join(HERE, "episodes_hash.npz"), **pack_episodes(eps))
     np.savez_compressed(os.path.join(HERE, "arena_hash.npz"), **make_arena())
     make_players()
+    make_examples_pickle()
     np.savez_compressed(os.path.join(HERE, "train_h64_b1.npz"), **make_train())
     print(f"done in {time.time() - t0:.1f}s")
 

@@ -207,3 +207,32 @@ def test_ddp_gradient_average_equals_union_batch(T, golden):
     # f32 summation order
     assert np.array_equal(out["g0"], out["g1"]) and np.array_equal(out["p0"], out["p1"])
     assert _relnorm(out["g0"], single) < 1e-5
+
+
+def test_coach_learn_iteration_and_resume(T, tmp_path):
+    """Coach.learn (Coach.py:74-139) end to end: batched self-play, examples files, train, the
+    previous-vs-new arena with two MCTS plugins, accept/reject; then loadTrainExamples resumes."""
+    from yacht_amd.coach import Coach
+    from yacht_amd.game import YachtGame
+    from yacht_amd.nnet import NNetWrapper
+    from yacht_amd.utils import dotdict
+    d = str(tmp_path)
+    args = dotdict(numIters=1, numEps=8, tempThreshold=15, updateThreshold=0.55, maxlenOfQueue=200000,
+                   numMCTSSims=4, arenaCompare=2, cpuct=1.5, checkpoint=d, load_folder_file=(d, "checkpoint_0.pth.tar"),
+                   numItersForTrainExamplesHistory=5, lr=2e-3, weight_decay=1e-4, epochs=1, batch_size=64,
+                   vloss_weight=1.5, cuda=True, hidden=64, nblocks=1, dropout=0.3)
+    game = YachtGame(seed=3, env_id=0)
+    c = Coach(game, NNetWrapper(game, args), args)
+    c.learn()
+    assert sum(c.last_pit) == 2
+    for f in ("temp.pth.tar", "checkpoint_0.pth.tar.examples", "checkpoint_0.pth.tar.examples.npz"):
+        assert os.path.exists(os.path.join(d, f)), f
+    assert len(c.trainExamplesHistory) == 1 and len(c.trainExamplesHistory[0]) == 8 * 48
+    c2 = Coach(game, NNetWrapper(game, args), args)
+    c2.loadTrainExamples()
+    assert c2.skipFirstSelfPlay and len(c2.trainExamplesHistory[0]) == 8 * 48
+    os.remove(os.path.join(d, "checkpoint_0.pth.tar.examples.npz"))  # the reference-format file alone
+    c3 = Coach(game, NNetWrapper(game, args), args)
+    c3.loadTrainExamples()
+    a, b = c2.trainExamplesHistory[0][5], c3.trainExamplesHistory[0][5]
+    assert a[0] == b[0] and a[1] == b[1] and a[2] == b[2]
