@@ -117,6 +117,13 @@ int yk_net_create(yk_net_t** net, int hidden, int nblocks, const float* const* p
 int yk_net_predict(yk_net_t* net, const yk_state_t* states, float* pi, float* v, int n, void* stream);
 /* same from explicit feature rows x[i*59 + f] */
 int yk_net_predict_features(yk_net_t* net, const float* x, float* pi, float* v, int n, void* stream);
+/* The submission bot's move (replaces AIPlayer.get_move's network part,
+ * yacht/submission/agent.py:248-280): for canonical states (the mover is p1), the action of
+ * highest softmax probability among the decodable ones (agent.py:150-187, the same set as
+ * getValidMoves), lowest index on equal probability; -1 when none.  probs (optional) gets
+ * that probability.  Device pointers. */
+int yk_net_policy_action(yk_net_t* net, const yk_state_t* states, int32_t* actions, float* probs, int n,
+                         void* stream);
 int yk_net_destroy(yk_net_t* net);
 
 /* ---------------------------------------------------------------- self-play engine

@@ -481,6 +481,44 @@ __global__ void k_softmax(const float* __restrict__ logits, float* __restrict__ 
     for (int a = lane; a < ASIZE; a += 64) pi[(long)row * ASIZE + a] = expf(x[a] - m - lse);
 }
 
+// The submission bot's move (agent.py:248-280): softmax over all 3226 logits in f32, then the
+// most probable *decodable* action (agent.py:150-187 == getValidMoves for the mover p1,
+// YachtGame.py:375-400), the lowest index among equal probabilities (its stable descending
+// sort).  One wavefront per row; -1 when the row has no valid action.
+__global__ void k_policy_pick(const float* __restrict__ logits, const yk_state_t* __restrict__ states,
+                              int32_t* __restrict__ actions, float* __restrict__ probs, int n) {
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (row >= n) return;
+    const float* x = logits + (long)row * PI_LD;
+    YkS s;
+#pragma unroll
+    for (int k = 0; k < 8; k++) s.w[k] = states[row].w[k];
+    float m = -INFINITY;
+    for (int a = lane; a < ASIZE; a += 64) m = fmaxf(m, x[a]);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    float sum = 0.f;
+    for (int a = lane; a < ASIZE; a += 64) sum += expf(x[a] - m);
+    sum = wave_sum(sum);
+    float bp = -1.f;
+    int ba = INT_MAX;
+    for (int a = lane; a < ASIZE; a += 64) {  // ascending per lane: strict > keeps the first
+        if (!action_valid(s, 1, a)) continue;
+        const float p = expf(x[a] - m) / sum;
+        if (p > bp) { bp = p; ba = a; }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const float op = __shfl_xor(bp, o, 64);
+        const int oa = __shfl_xor(ba, o, 64);
+        if (op > bp || (op == bp && oa < ba)) { bp = op; ba = oa; }
+    }
+    if (lane == 0) {
+        actions[row] = ba == INT_MAX ? -1 : ba;
+        if (probs) probs[row] = ba == INT_MAX ? 0.f : bp;
+    }
+}
+
 }  // namespace
 
 namespace yk {
@@ -620,6 +658,27 @@ int yk_net_predict(yk_net_t* net, const yk_state_t* states, float* pi, float* v,
 int yk_net_predict_features(yk_net_t* net, const float* x, float* pi, float* v, int n, void* stream) {
     if (!x) return YK_ERR_ARG;
     return predict_common(net, nullptr, x, pi, v, n, stream);
+}
+
+int yk_net_policy_action(yk_net_t* net, const yk_state_t* states, int32_t* actions, float* probs, int n,
+                         void* stream) {
+    if (!net || !states || !actions || n < 0) return YK_ERR_ARG;
+    if (n == 0) return YK_OK;
+    hipStream_t s = as_stream(stream);
+    float *logits = nullptr, *v = nullptr;
+    YK_HIP(hipMallocAsync((void**)&logits, sizeof(float) * ((size_t)n * PI_LD + n), s));
+    v = logits + (size_t)n * PI_LD;
+    int rc = launch_forward(net->dev, states, nullptr, nullptr, nullptr, n, logits, v, s);
+    if (rc == YK_OK) {
+        hipLaunchKernelGGL(k_policy_pick, dim3((n + 3) / 4), dim3(256), 0, s, logits, states, actions, probs, n);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) {
+            yk::set_hip_error(e);
+            rc = YK_ERR_HIP;
+        }
+    }
+    (void)hipFreeAsync(logits, s);
+    return rc;
 }
 
 }  // extern "C"

@@ -43,7 +43,10 @@ class ResidualBlock(nn.Module):  # YachtNNet.py:8-21
 
 
 class YachtNNet(nn.Module):  # YachtNNet.py:24-70
-    def __init__(self, input_len=59, action_size=ACTION_SIZE, hidden=256, nblocks=6, dropout=0.3):
+    def __init__(self, input_len=59, action_size=ACTION_SIZE, hidden=256, nblocks=6, dropout=0.3,
+                 kaiming_init=True):
+        """kaiming_init=False keeps torch's default Linear init, as the submission bot's copy of
+        the class does (agent.py:30-67)."""
         super().__init__()
         self.input_len, self.action_size = input_len, action_size
         self.inp = nn.Sequential(nn.Linear(input_len, hidden), nn.LayerNorm(hidden), nn.SiLU(), nn.Dropout(dropout))
@@ -51,7 +54,7 @@ class YachtNNet(nn.Module):  # YachtNNet.py:24-70
         self.pi_head = nn.Sequential(nn.LayerNorm(hidden), nn.SiLU(), nn.Linear(hidden, action_size))
         self.v_head = nn.Sequential(nn.LayerNorm(hidden), nn.SiLU(), nn.Linear(hidden, 128), nn.SiLU(),
                                     nn.Linear(128, 1))
-        for m in self.modules():
+        for m in self.modules() if kaiming_init else ():
             if isinstance(m, nn.Linear):
                 nn.init.kaiming_uniform_(m.weight, nonlinearity="relu")
                 nn.init.zeros_(m.bias)
@@ -94,6 +97,16 @@ class YkNet:
         v = torch.empty(n, dtype=torch.float32, device="cuda")
         call("yk_net_predict_features", self.handle, ptr(x), ptr(pi), ptr(v), n, stream_ptr())
         return pi, v
+
+    def policy_action(self, states: torch.Tensor):
+        """states int64[n, 8] canonical (device) -> (actions i32[n], probs f32[n]): the most probable
+        valid action per row, as the submission bot picks it (agent.py:248-280); -1 if none."""
+        n = states.shape[0]
+        actions = torch.empty(n, dtype=torch.int32, device="cuda")
+        probs = torch.empty(n, dtype=torch.float32, device="cuda")
+        call("yk_net_policy_action", self.handle, ptr(states.contiguous()), ptr(actions), ptr(probs), n,
+             stream_ptr())
+        return actions, probs
 
     def __del__(self):
         try:

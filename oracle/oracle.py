@@ -197,6 +197,23 @@ class Net:
             pass
 
 
+def policy_action(net, states):
+    """The submission bot's move (yacht/submission/agent.py:248-280) for canonical states: the
+    valid (== decodable, agent.py:150-187) action of highest softmax probability, the lowest index
+    among equals (its stable descending sort); -1 when none.  Also returns each row's margin to
+    the runner-up as a log-probability (= logit) difference (inf with a single valid action)."""
+    pi, _ = net.predict_states(states)
+    ok, cnt = valid(states, 1)
+    p = np.where(ok.astype(bool), pi, -1.0)
+    a = p.argmax(1).astype(np.int64)  # first maximum
+    top2 = -np.sort(-p, 1)[:, :2]
+    with np.errstate(divide="ignore", invalid="ignore"):
+        margin = np.where(cnt > 1, np.log(top2[:, 0].astype(np.float64)) - np.log(top2[:, 1].astype(np.float64)),
+                          np.inf)
+    a[cnt == 0] = -1
+    return a, margin
+
+
 MODE_HASH, MODE_MLP, MODE_REPLAY = 0, 1, 2
 PLAYERS = {"mcts": 0, "random": 1, "greedy": 2}
 

@@ -460,6 +460,119 @@ def make_players():
                         **make_arena(seed=779, n=8, sims=8, agent_kind="mcts", opp_kind="greedy", env0=700))
 
 
+# ------------------------------------------------------------------ submission bot (f4)
+# The reference agent (yacht/submission/agent.py) is run unmodified as a child process,
+# speaking its stdin/stdout protocol; only its hard-coded model path (AIPlayer default,
+# agent.py:193) is pointed at a checkpoint written here.  A referee in this script plays the
+# two agents against each other under the rules of INSTRUCTION.md and records every line.
+_AGENT_BOOT = ("import sys; sys.path.insert(0, sys.argv[2]); import agent; "
+               "agent.AIPlayer.__init__.__defaults__ = (sys.argv[1],); agent.main()")
+
+
+class _Agent:
+    def __init__(self, ckpt, cwd):
+        import subprocess
+        self.p = subprocess.Popen([sys.executable, "-u", "-c", _AGENT_BOOT, ckpt,
+                                   os.path.join(REF, "yacht", "submission")],
+                                  stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL,
+                                  text=True, cwd=cwd)
+        self.inp, self.out = [], []
+
+    def send(self, line, reply):
+        self.inp.append(line)
+        self.p.stdin.write(line + "\n")
+        self.p.stdin.flush()
+        if reply:
+            r = self.p.stdout.readline().strip()
+            self.out.append(r)
+            return r
+        return None
+
+    def close(self):
+        self.send("FINISH", False)
+        self.p.stdin.close()
+        assert self.p.wait(timeout=60) == 0
+
+
+def _referee_game(ckpts, rng, cwd):
+    """One match under INSTRUCTION.md:10-70 between two reference agents; returns both transcripts."""
+    bots = [_Agent(c, cwd) for c in ckpts]
+    for b in bots:
+        assert b.send("READY", True) == "OK"
+    carry = [[], []]
+    for rnd in range(1, 14):
+        if rnd < 13:
+            A = [int(x) for x in rng.integers(1, 7, 5)]
+            B = [int(x) for x in rng.integers(1, 7, 5)]
+            sa, sb = "".join(map(str, A)), "".join(map(str, B))
+            bids = []
+            for b in bots:
+                cmd, g, x = b.send(f"ROLL {sa} {sb}", True).split()
+                assert cmd == "BID" and g in "AB"
+                bids.append((g, int(x)))
+            (g0, x0), (g1, x1) = bids
+            if g0 != g1:
+                got = [g0, g1]
+            else:
+                win = 0 if x0 > x1 else 1 if x1 > x0 else int(rng.integers(2))
+                other = "B" if g0 == "A" else "A"
+                got = [g0, other] if win == 0 else [other, g1]
+            for i, b in enumerate(bots):
+                b.send(f"GET {got[i]} {bids[1 - i][0]} {bids[1 - i][1]}", False)
+                carry[i] += A if got[i] == "A" else B
+        if rnd >= 2:
+            puts = []
+            for i, b in enumerate(bots):
+                cmd, c, d = b.send("SCORE", True).split()
+                assert cmd == "PUT" and len(d) == 5
+                left = list(carry[i])
+                for v in map(int, d):
+                    left.remove(v)  # the dice must be held
+                carry[i] = left
+                puts.append((c, d))
+            for i, b in enumerate(bots):
+                b.send(f"SET {puts[1 - i][0]} {puts[1 - i][1]}", False)
+    for b in bots:
+        b.close()
+    return [("\n".join(b.inp), "\n".join(b.out)) for b in bots]
+
+
+def make_bot(seed=41, games=3):
+    import tempfile
+    import torch
+    sys.path.insert(0, os.path.join(REF, "yacht", "submission"))
+    import agent as ref_agent
+    out = {}
+    nets = ((64, 1), (256, 6))
+    with tempfile.TemporaryDirectory() as tmp:
+        ckpts = []
+        for k, (hidden, nblocks) in enumerate(nets):
+            torch.manual_seed(seed + k)
+            m = ref_agent.YachtNNet(input_len=59, action_size=3226, hidden=hidden, nblocks=nblocks, dropout=0.0)
+            sd = m.state_dict()
+            path = os.path.join(tmp, f"net{k}.pth.tar")
+            torch.save({"state_dict": sd, "args": {"hidden": hidden, "nblocks": nblocks, "dropout": 0.0}}, path)
+            ckpts.append(path)
+            # the weights are re-created by the tests from the seed (torch.manual_seed + the same
+            # module construction order); the digest pins them
+            import hashlib
+            h = hashlib.sha256(b"".join(t.numpy().astype(np.float32).tobytes() for t in sd.values()))
+            out[f"net{k}_dims"] = np.array([hidden, nblocks, seed + k], dtype=np.int64)
+            out[f"net{k}_sha256"] = np.array(h.hexdigest())
+        rng = np.random.default_rng(seed)
+        pairs = []
+        for g in range(games):
+            order = (0, 1) if g % 2 == 0 else (1, 0)
+            tr = _referee_game([ckpts[i] for i in order], rng, tmp)
+            for seat, (i, (tin, tout)) in enumerate(zip(order, tr)):
+                out[f"g{g}_s{seat}_in"] = np.array(tin)
+                out[f"g{g}_s{seat}_out"] = np.array(tout)
+                pairs.append((g, seat, i))
+                assert tout.count("BID A 0") < 12, "agent fell back to its minimal move (model not loaded?)"
+        out["seats"] = np.array(pairs, dtype=np.int64)  # (game, seat, net index)
+    return out
+
+
 def pack_episodes(eps):
     """Flatten episode dicts into fixed arrays (npz-friendly)."""
     out = {}
@@ -500,6 +613,10 @@ def main():
         np.savez_compressed(os.path.join(HERE, "train_h64_b1.npz"), **make_train())
         print(f"train fixture in {time.time() - t0:.1f}s")
         return
+    if len(sys.argv) > 1 and sys.argv[1] == "bot":
+        np.savez_compressed(os.path.join(HERE, "bot_transcripts.npz"), **make_bot())
+        print(f"bot fixture in {time.time() - t0:.1f}s")
+        return
     if len(sys.argv) > 1 and sys.argv[1] == "arena":
         np.savez_compressed(os.path.join(HERE, "arena_hash.npz"), **make_arena())
         make_players()
@@ -534,6 +651,7 @@ def main():
     make_players()
     make_examples_pickle()
     np.savez_compressed(os.path.join(HERE, "train_h64_b1.npz"), **make_train())
+    np.savez_compressed(os.path.join(HERE, "bot_transcripts.npz"), **make_bot())
     print(f"done in {time.time() - t0:.1f}s")
 
 
