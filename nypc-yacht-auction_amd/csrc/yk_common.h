@@ -431,6 +431,13 @@ __device__ __host__ inline VInfo valid_info(const YkS& s, int player) {
 }
 __device__ __host__ inline int compact_to_action(const VInfo& v, int j) {
     if (v.W == 0) return j;
+    // the two carry sizes of real play need no table and no runtime division: 10 dice -> all
+    // 252 combos valid (ids = ranks); 5 dice -> only combo 0
+    if (v.n >= 10) {
+        const int ci = j / NCOMB, r = j - ci * NCOMB;
+        return NBID + NCOMB * (int)((v.cats >> (4 * ci)) & 0xF) + r;
+    }
+    if (v.n == 5) return NBID + NCOMB * (int)((v.cats >> (4 * j)) & 0xF);
 #ifdef __HIP_DEVICE_COMPILE__
     const Tables& T = c_tab;
 #else

@@ -33,6 +33,9 @@ namespace {
 constexpr int MAXD = 64;          // max search depth (path entries)
 constexpr int LUT_N = 1 << 16;    // f32(sqrt(Ns)), f32(sqrt(Ns + 1e-8)) table size
 constexpr int GAMES_PER_BLOCK = 4;
+#ifndef YK_EXPAND_WPE
+#define YK_EXPAND_WPE 4  // waves per SIMD the expand kernel is register-budgeted for
+#endif
 
 // python value kinds on the search path (MCTS.py:82, 115, 147)
 enum : uint32_t { T_INT = 0, T_F64 = 1, T_F32 = 2 };
@@ -188,9 +191,47 @@ struct ValidQ {
         if (mode == 1) return a < NBID;
         if (mode != 0 || a < NBID) return false;
         const int base = a - NBID, cat = base / NCOMB, ci = base - cat * NCOMB;
-        return !((used >> cat) & 1u) && c_tab.comb_max[ci] < n;
+        if ((used >> cat) & 1u) return false;
+        // the two carry sizes of real play need no table: 10 dice -> every combo, 5 -> combo 0
+        if (n >= 10) return true;
+        if (n == 5) return ci == 0;
+        return c_tab.comb_max[ci] < n;
     }
 };
+// validity over one pairwise leaf [st, st + len), len < 252: runs [.., b1) v0, [b1, b2) v1,
+// [b2, ..) v2 - exact for the bid phase and for 10 carried dice; `generic` otherwise
+struct LeafRuns {
+    int b1, b2;
+    bool v0, v1, v2, generic;
+    __device__ __forceinline__ bool operator()(int a) const { return a < b1 ? v0 : (a < b2 ? v1 : v2); }
+};
+__device__ __forceinline__ LeafRuns leaf_runs(const ValidQ& q, int st) {
+    LeafRuns r{INT_MAX, INT_MAX, false, false, false, false};
+    if (q.mode == 1) {
+        r.b1 = NBID;
+        r.v0 = true;
+    } else if (q.mode == 0) {
+        if (q.n < 10) {
+            r.generic = true;
+            return r;
+        }
+        auto unused = [&](int c) { return c < NCAT && !((q.used >> c) & 1u); };
+        if (st < NBID) {
+            r.b1 = NBID;
+            r.v1 = unused(0);
+            r.b2 = NBID + NCOMB;
+            r.v2 = unused(1);
+        } else {
+            const int c = (st - NBID) / NCOMB;
+            r.v0 = unused(c);
+            r.b1 = NBID + NCOMB * (c + 1);
+            r.v1 = unused(c + 1);
+            r.b2 = r.b1 + NCOMB;
+            r.v2 = unused(c + 2);
+        }
+    }
+    return r;
+}
 __device__ __forceinline__ ValidQ valid_q(const YkS& s) {
     ValidQ q;
     const int round = s_round(s), phase = s_phase(s);
@@ -430,10 +471,10 @@ __global__ __launch_bounds__(256) void k_move_begin(EngDev d, int move, int exte
 // Diagnostic builds only (-DYK_SEL_TIMING, tools/diag_select.py): per-game s_memtime
 // accumulators of the descent's phases.
 #ifdef YK_SEL_TIMING
-__device__ unsigned long long g_sel[16384 * 8];
+__device__ unsigned long long g_sel[16384 * 16];
 #define SEL_T0(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
 #define SEL_ACC(k, t0) \
-    if (lane == 0) g_sel[(long)e * 8 + (k)] += __builtin_amdgcn_s_memtime() - (t0)
+    if (lane == 0) g_sel[(long)e * 16 + (k)] += __builtin_amdgcn_s_memtime() - (t0)
 #else
 #define SEL_T0(v)
 #define SEL_ACC(k, t0)
@@ -572,8 +613,8 @@ __device__ __forceinline__ void select_game(const EngDev& d, int e, int lane, co
         SEL_ACC(2, t_st);
         if (lane == 0) {
 #ifdef YK_SEL_TIMING
-            g_sel[(long)e * 8 + 4] += 1;
-            g_sel[(long)e * 8 + 5] += (unsigned long long)V;
+            g_sel[(long)e * 16 + 4] += 1;
+            g_sel[(long)e * 16 + 5] += (unsigned long long)V;
 #endif
         }
     }
@@ -601,13 +642,19 @@ __global__ __launch_bounds__(256) void k_select(EngDev d, const uint32_t* env_id
 // when do_select - the next simulation's descent for the same game (one kernel boundary per
 // simulation fewer).  One wave per game.
 __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int lane);
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_expand_backup(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(YK_EXPAND_WPE))) void k_expand_backup(
     EngDev d, int do_select, const uint32_t* env_ids, uint64_t* ctr_arr) {
     const int lane = threadIdx.x & 63;
     const int e = blockIdx.x * GAMES_PER_BLOCK + (threadIdx.x >> 6);
     if (e >= d.E) return;
     if (d.done[e]) return;
+#ifdef YK_SEL_TIMING
+    const unsigned long long t_ex = __builtin_amdgcn_s_memtime();
+#endif
     expand_backup_game(d, e, lane);
+#ifdef YK_SEL_TIMING
+    if (lane == 0) g_sel[(long)e * 16 + 6] += __builtin_amdgcn_s_memtime() - t_ex;
+#endif
     if (do_select) {
         wave_sync();  // this wave's backup writes (edges, slots, Ns) precede its descent's reads
         select_game(d, e, lane, env_ids, ctr_arr);
@@ -618,6 +665,7 @@ __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int l
     const int g = d.gen[e];
     PyV res{d.res_v[e], d.res_t[e]};
     if (d.leaf_flag[e]) {
+        SEL_T0(t_x0);
         const YkS s = ld_state(d.leaf_state + e);
         const uint64_t hsh = d.leaf_hash[e];
         const VInfo vi = valid_info(s, 1);
@@ -670,6 +718,7 @@ __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int l
 #pragma unroll
             for (int r = 0; r < PW_TMAX; r++) qt[r] = softmax_p(qt[r], m, lse);
             v = d.vpred[e];
+            SEL_ACC(8, t_x0);
         } else {
 #pragma unroll
             for (int j = 0; j < PW_GMAX; j++) {
@@ -691,20 +740,32 @@ __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int l
                 if (h == 0 && r < R) rpi[st + 8 * G + r] = qt[r];
             if (lane == 0) d.rec_v[(long)e * d.max_exp + pidx] = v;
         }
-        // mask with the valid moves
+        SEL_T0(t_x1);
+        // mask with the valid moves.  With the carry sizes of real play the valid set is a union
+        // of whole runs (the 202 bids, or the 252 actions of each unused category), and a leaf
+        // (<= 106 positions) meets at most three of them: validity is two compares per element.
+        const LeafRuns runs = leaf_runs(valid, st);
+        auto mask_leaf = [&](auto vok) {
 #pragma unroll
-        for (int j = 0; j < PW_GMAX; j++) {
-            const int a = st + 8 * j + 4 * h;
-            if (j < G) {
-                if (!valid(a)) q[j].x = 0.f;
-                if (!valid(a + 1)) q[j].y = 0.f;
-                if (!valid(a + 2)) q[j].z = 0.f;
-                if (!valid(a + 3)) q[j].w = 0.f;
+            for (int j = 0; j < PW_GMAX; j++) {
+                const int a = st + 8 * j + 4 * h;
+                if (j < G) {
+                    if (!vok(a)) q[j].x = 0.f;
+                    if (!vok(a + 1)) q[j].y = 0.f;
+                    if (!vok(a + 2)) q[j].z = 0.f;
+                    if (!vok(a + 3)) q[j].w = 0.f;
+                }
             }
-        }
 #pragma unroll
-        for (int r = 0; r < PW_TMAX; r++)
-            if (h == 0 && r < R && !valid(st + 8 * G + r)) qt[r] = 0.f;
+            for (int r = 0; r < PW_TMAX; r++)
+                if (h == 0 && r < R && !vok(st + 8 * G + r)) qt[r] = 0.f;
+        };
+#ifdef YK_NO_LEAF_RUNS
+        mask_leaf(valid);
+#else
+        if (runs.generic) mask_leaf(valid);  // wave-uniform
+        else mask_leaf(runs);
+#endif
         // numpy pairwise_sum on the leaf: r_k = a[k] + a[8 + k] + ..., then
         // ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)), then the tail one by one
         float4 racc = q[0];
@@ -730,6 +791,8 @@ __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int l
             lsum = (lane & o) ? y + lsum : lsum + y;
         }
         const float sum = lsum;
+        SEL_ACC(9, t_x1);
+        SEL_T0(t_x2);
         // ---- allocate + write P over the compact valid set, zero edge slots
         const int VP = pad4(V);
         const uint32_t off = d.arena_top[e];
@@ -774,6 +837,7 @@ __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int l
                     }
                 }
             }
+            SEL_ACC(10, t_x2);
             if (lane == 0) {
                 NodeRec r;
 #pragma unroll
@@ -799,6 +863,7 @@ __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int l
     }
     // ---- backup (MCTS.py:154-164): the path's nodes are distinct, so every level updates in
     // parallel; level k receives v * (-1)^(depth-1-k) ("return -v" per level).
+    SEL_T0(t_bk);
     const int depth = d.path_len[e];
     if (depth > 0) {
         const uint64_t* path = d.path + (long)e * MAXD;
@@ -839,6 +904,7 @@ __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int l
             if (ne1 > gs[5]) gs[5] = ne1;
         }
     }
+    SEL_ACC(12, t_bk);
 }
 
 // getActionProb tail (MCTS.py:40-54) + Coach sampling/step (Coach.py:59-72).  One wave per game.
@@ -1128,10 +1194,10 @@ int run_sims(yk_engine* eng, int sims, const uint32_t* env_ids, uint64_t* ctr, h
 extern "C" {
 
 #ifdef YK_SEL_TIMING
-int yk_diag_select(uint64_t* out, int n) {  // HOST out[n][8]; resets the accumulators
+int yk_diag_select(uint64_t* out, int n) {  // HOST out[n][16]; resets the accumulators
     YK_HIP(hipDeviceSynchronize());
-    YK_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sel), sizeof(uint64_t) * 8 * (size_t)n));
-    std::vector<uint64_t> z((size_t)8 * n, 0);
+    YK_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sel), sizeof(uint64_t) * 16 * (size_t)n));
+    std::vector<uint64_t> z((size_t)16 * n, 0);
     YK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_sel), z.data(), sizeof(uint64_t) * z.size()));
     return YK_OK;
 }

@@ -24,6 +24,8 @@
 using namespace yk;
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef _Float16 half4 __attribute__((ext_vector_type(4)));
 
 namespace {
 
@@ -43,9 +45,12 @@ constexpr int ROWS = 16;     // rows per workgroup (the MFMA M)
 constexpr int WAVES = 8;     // waves per workgroup
 constexpr int NTHR = 64 * WAVES;
 constexpr int RPW = ROWS / WAVES;  // rows per wave in the row passes
-constexpr int FPAD = 68;     // feature tile row stride (64 + 4)
 constexpr int PCH = 4;       // policy-head tiles per chunk
-constexpr int PW = 8;        // policy-head ring depth (k-blocks)
+#ifndef YK_PW
+#define YK_PW 2
+#endif
+constexpr int PW = YK_PW;    // policy-head ring depth (32-deep slices)
+constexpr float SPLIT = 2048.f, UNSPLIT = 1.f / 2048.f;  // lo plane scale (keeps it out of fp16 subnormals)
 
 // SiLU with the hardware exp / reciprocal (<= 2 ulp each; well inside the 1e-5 contract)
 __device__ __forceinline__ float silu(float x) { return x * __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
@@ -69,59 +74,101 @@ __device__ __forceinline__ float wave_sum(float v) {
 // outstanding global loads (a __syncthreads() would drain vmcnt and the weight stream).
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// fragment (tile nt, k-block kb) of a packed [N][K] matrix with KB k-blocks: 1 KB per wave
-__device__ __forceinline__ float4 ld_frag(const float* __restrict__ P, int KB, int nt, int kb, int lane) {
-    return *reinterpret_cast<const float4*>(P + ((long)(nt * KB + kb) * 64 + lane) * 4);
+// One 16-column x 32-deep weight slice of a packed [N][K] matrix (yk_net.h): the hi and the lo
+// plane, 1 KB each per wave (raw fp16 bits, 8 per lane).
+struct W2 {
+    float4 h, l;
+};
+__device__ __forceinline__ W2 ld_w2(const float* __restrict__ P, int KS, int nt, int ks, int lane) {
+    const float* p = P + ((long)(nt * KS + ks) * 2 * 64 + lane) * 4;
+    return W2{*reinterpret_cast<const float4*>(p), *reinterpret_cast<const float4*>(p + 256)};
 }
 
-__device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+__device__ __forceinline__ floatx4 mfma16(float4 a, float4 b, floatx4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, a), __builtin_bit_cast(half8, b), c, 0, 0, 0);
 }
 
-// acc[t] = A[16 x K] (LDS, row stride lda) x W^T over this wave's NT tiles (nt0 ...), with the
-// fragments taken from the ring; k-block kb lives in slot kb % RW.  After use, the slot is
-// refilled with k-block kb + RW of this layer (cur) or, past its end, of the next layer (nxt,
-// same shape).  Lane l supplies A[l&15][16kb + 4(l>>4) + i] to MFMA i of a k-block.  One tile
-// alternates two accumulators (40-cycle dependent latency vs 32-cycle issue).
-template <int K, int NT, int RW, bool NEXT = true>
-__device__ __forceinline__ void mma_ring(const float* A, int lda, float4 (&ring)[RW][NT], floatx4 (&acc)[NT],
-                                         const float* __restrict__ cur, const float* __restrict__ nxt, int nt0) {
-    constexpr int KB = K / 16;
+// f32-equivalent product of one A slice (hi, lo planes) and one weight slice: three fp16 MFMAs
+// (exact products, f32 accumulation): hi x hi into m, hi x lo and lo x hi into c, which carries
+// the 2^11 scale of the lo planes until combine().
+struct Acc3 {
+    floatx4 m, c;
+};
+__device__ __forceinline__ void acc_zero(Acc3& a) { a.m = a.c = floatx4{0.f, 0.f, 0.f, 0.f}; }
+__device__ __forceinline__ floatx4 combine(const Acc3& a) { return a.m + a.c * UNSPLIT; }
+
+// A fragment of a plane pair in LDS (row stride SA halves): lane l reads row l & 15,
+// k = 32 ks + 8 (l >> 4) .. + 7 of each plane.
+struct APtr {
+    const _Float16* h;
+    const _Float16* l;
+};
+__device__ __forceinline__ APtr a_ptr(const _Float16* planes, int sa) {
     const int lane = threadIdx.x & 63;
-    const float* ap = A + (lane & 15) * lda + 4 * (lane >> 4);
-    floatx4 acc2[NT];
+    const int off = (lane & 15) * sa + 8 * (lane >> 4);
+    return APtr{planes + off, planes + ROWS * sa + off};
+}
+__device__ __forceinline__ float4 ld_a(const _Float16* p, int ks) { return *reinterpret_cast<const float4*>(p + 32 * ks); }
+
+// x -> (hi, lo * 2^11) into row r, column c of a plane pair (row stride sa halves), VPL values
+template <int VPL>
+__device__ __forceinline__ void put_planes(_Float16* planes, int sa, int r, int c, const float (&x)[VPL]) {
+    _Float16 h[VPL], l[VPL];
 #pragma unroll
-    for (int t = 0; t < NT; t++) acc[t] = acc2[t] = floatx4{0.f, 0.f, 0.f, 0.f};
-    float4 a = *reinterpret_cast<const float4*>(ap);
+    for (int i = 0; i < VPL; i++) {
+        h[i] = (_Float16)x[i];
+        l[i] = (_Float16)((x[i] - (float)h[i]) * SPLIT);
+    }
+    _Float16* ph = planes + r * sa + c;
+    _Float16* pl = planes + ROWS * sa + r * sa + c;
+    if constexpr (VPL == 4) {
+        *reinterpret_cast<half4*>(ph) = half4{h[0], h[1], h[2], h[3]};
+        *reinterpret_cast<half4*>(pl) = half4{l[0], l[1], l[2], l[3]};
+    } else {
 #pragma unroll
-    for (int kb = 0; kb < KB; kb++) {
-        const float4 an = *reinterpret_cast<const float4*>(ap + 16 * ((kb + 1) % KB));
-        float4(&w)[NT] = ring[kb % RW];
-        if constexpr (NT == 1) {
-            acc[0] = mfma4(a.x, w[0].x, acc[0]);
-            acc2[0] = mfma4(a.y, w[0].y, acc2[0]);
-            acc[0] = mfma4(a.z, w[0].z, acc[0]);
-            acc2[0] = mfma4(a.w, w[0].w, acc2[0]);
-        } else {
-#pragma unroll
-            for (int t = 0; t < NT; t++) acc[t] = mfma4(a.x, w[t].x, acc[t]);
-#pragma unroll
-            for (int t = 0; t < NT; t++) acc[t] = mfma4(a.y, w[t].y, acc[t]);
-#pragma unroll
-            for (int t = 0; t < NT; t++) acc[t] = mfma4(a.z, w[t].z, acc[t]);
-#pragma unroll
-            for (int t = 0; t < NT; t++) acc[t] = mfma4(a.w, w[t].w, acc[t]);
+        for (int i = 0; i < VPL; i++) {
+            ph[i] = h[i];
+            pl[i] = l[i];
         }
-        const int g = kb + RW;
-        if (g < KB || NEXT) {
+    }
+}
+
+// acc[t] = A[16 x K] (plane pair in LDS) x W^T over this wave's NT tiles (nt0 ...), with the
+// weight slices taken from the ring; slice ks lives in slot ks % RW.  After use, the slot is
+// refilled with slice ks + RW of this layer (cur) or, past its end, of the next layer (nxt,
+// same shape).
+template <int K, int NT, int RW, bool NEXT = true>
+__device__ __forceinline__ void mma_ring(const _Float16* A, int sa, W2 (&ring)[RW][NT], floatx4 (&acc)[NT],
+                                         const float* __restrict__ cur, const float* __restrict__ nxt, int nt0) {
+    constexpr int KS = K / 32;
+    const int lane = threadIdx.x & 63;
+    const APtr ap = a_ptr(A, sa);
+    Acc3 c[NT];
+#pragma unroll
+    for (int t = 0; t < NT; t++) acc_zero(c[t]);
+    float4 ah = ld_a(ap.h, 0), al = ld_a(ap.l, 0);
+#pragma unroll
+    for (int ks = 0; ks < KS; ks++) {
+        const float4 ahn = ld_a(ap.h, (ks + 1) % KS), aln = ld_a(ap.l, (ks + 1) % KS);
+        W2(&w)[NT] = ring[ks % RW];
+#pragma unroll
+        for (int t = 0; t < NT; t++) c[t].m = mfma16(ah, w[t].h, c[t].m);
+#pragma unroll
+        for (int t = 0; t < NT; t++) c[t].c = mfma16(ah, w[t].l, c[t].c);
+#pragma unroll
+        for (int t = 0; t < NT; t++) c[t].c = mfma16(al, w[t].h, c[t].c);
+        const int g = ks + RW;
+        if (g < KS || NEXT) {
 #pragma unroll
             for (int t = 0; t < NT; t++)
-                w[t] = g < KB ? ld_frag(cur, KB, nt0 + t, g, lane) : ld_frag(nxt, KB, nt0 + t, g - KB, lane);
+                w[t] = g < KS ? ld_w2(cur, KS, nt0 + t, g, lane) : ld_w2(nxt, KS, nt0 + t, g - KS, lane);
         }
         __builtin_amdgcn_sched_barrier(0);  // keep the refill here, a ring's depth ahead of its use
-        a = an;
+        ah = ahn;
+        al = aln;
     }
-    if constexpr (NT == 1) acc[0] += acc2[0];
+#pragma unroll
+    for (int t = 0; t < NT; t++) acc[t] = combine(c[t]);
 }
 
 // D[16 x 16] tile t of the wave: lane holds rows 4(l>>4)+j, column 16(nt0 + t) + (l&15).
@@ -158,58 +205,56 @@ __device__ __forceinline__ void layernorm(float (&x)[VPL], const float* g, const
 }
 
 // Policy head chunks: wave w owns tiles w + WAVES j; a chunk holds NTL <= PCH of them
-// (tiles tb, tb + WAVES, ...).  The ring (PW k-blocks of PCH fragments) streams across chunk
-// boundaries: past the last k-block it refills with the next chunk's first k-blocks (NXT
-// tiles, from tb_next).  Tiles >= PI_TILES (the padded last chunk) are computed on a
-// duplicate of tile tb and not stored.
+// (tiles tb, tb + WAVES, ...).  The ring (RD slices of PCH tiles) streams across chunk
+// boundaries: past the last slice it refills with the next chunk's first slices (NXT tiles,
+// from tb_next).  Tiles >= PI_TILES (the padded last chunk) are computed on a duplicate of
+// tile tb and not stored.
 __device__ __forceinline__ int pi_tile(int tb, int t) {  // real tile to load for slot t
     const int x = tb + WAVES * t;
-#ifdef YK_DIAG_L1
-    return x & 1;  // diagnostic: a 2-tile footprint, L1-resident
-#else
     return x < PI_TILES ? x : tb;
-#endif
 }
-template <int KB, int NTL, int NXT, int RD = (PW < KB ? PW : KB)>
-__device__ __forceinline__ void ring_chunk(const float* A, int lda, float4 (&ring)[RD][PCH], floatx4 (&pa)[NTL],
+template <int KS, int NTL, int NXT, int RD = (PW < KS ? PW : KS)>
+__device__ __forceinline__ void ring_chunk(const _Float16* A, int sa, W2 (&ring)[RD][PCH], floatx4 (&pa)[NTL],
                                            const float* __restrict__ W, int tb, const float* __restrict__ Wn,
                                            int tb_next) {
     const int lane = threadIdx.x & 63;
-    const float* ap = A + (lane & 15) * lda + 4 * (lane >> 4);
+    const APtr ap = a_ptr(A, sa);
+    Acc3 c[NTL];
 #pragma unroll
-    for (int t = 0; t < NTL; t++) pa[t] = floatx4{0.f, 0.f, 0.f, 0.f};
-    float4 a = *reinterpret_cast<const float4*>(ap);
+    for (int t = 0; t < NTL; t++) acc_zero(c[t]);
+    float4 ah = ld_a(ap.h, 0), al = ld_a(ap.l, 0);
 #pragma unroll
-    for (int kb = 0; kb < KB; kb++) {
-        const float4 an = *reinterpret_cast<const float4*>(ap + 16 * ((kb + 1) % KB));
-        float4(&w)[PCH] = ring[kb % RD];
+    for (int ks = 0; ks < KS; ks++) {
+        const float4 ahn = ld_a(ap.h, (ks + 1) % KS), aln = ld_a(ap.l, (ks + 1) % KS);
+        W2(&w)[PCH] = ring[ks % RD];
 #pragma unroll
-        for (int t = 0; t < NTL; t++) pa[t] = mfma4(a.x, w[t].x, pa[t]);
+        for (int t = 0; t < NTL; t++) c[t].m = mfma16(ah, w[t].h, c[t].m);
 #pragma unroll
-        for (int t = 0; t < NTL; t++) pa[t] = mfma4(a.y, w[t].y, pa[t]);
+        for (int t = 0; t < NTL; t++) c[t].c = mfma16(ah, w[t].l, c[t].c);
 #pragma unroll
-        for (int t = 0; t < NTL; t++) pa[t] = mfma4(a.z, w[t].z, pa[t]);
+        for (int t = 0; t < NTL; t++) c[t].c = mfma16(al, w[t].h, c[t].c);
+        const int g = ks + RD;
+        if (g < KS) {
 #pragma unroll
-        for (int t = 0; t < NTL; t++) pa[t] = mfma4(a.w, w[t].w, pa[t]);
-        const int g = kb + RD;
-        if (g < KB) {
-#pragma unroll
-            for (int t = 0; t < NTL; t++) w[t] = ld_frag(W, KB, pi_tile(tb, t), g, lane);
+            for (int t = 0; t < NTL; t++) w[t] = ld_w2(W, KS, pi_tile(tb, t), g, lane);
         } else {
 #pragma unroll
-            for (int t = 0; t < NXT; t++) w[t] = ld_frag(Wn, KB, pi_tile(tb_next, t), g - KB, lane);
+            for (int t = 0; t < NXT; t++) w[t] = ld_w2(Wn, KS, pi_tile(tb_next, t), g - KS, lane);
         }
         __builtin_amdgcn_sched_barrier(0);
-        a = an;
+        ah = ahn;
+        al = aln;
     }
+#pragma unroll
+    for (int t = 0; t < NTL; t++) pa[t] = combine(c[t]);
 }
-template <int KB, int NTL, int NXT, int RD = (PW < KB ? PW : KB)>
-__device__ __forceinline__ void pi_chunk(const float* A, int lda, float4 (&ring)[RD][PCH], const float* __restrict__ W,
+template <int KS, int NTL, int NXT, int RD = (PW < KS ? PW : KS)>
+__device__ __forceinline__ void pi_chunk(const _Float16* A, int sa, W2 (&ring)[RD][PCH], const float* __restrict__ W,
                                          int tb, int tb_next, const float* bias, float* __restrict__ logits, int row0,
                                          int n) {
     const int lane = threadIdx.x & 63;
     floatx4 pa[NTL];
-    ring_chunk<KB, NTL, NXT, RD>(A, lda, ring, pa, W, tb, W, tb_next);
+    ring_chunk<KS, NTL, NXT, RD>(A, sa, ring, pa, W, tb, W, tb_next);
     const int rr = lane & 15, q = lane >> 4;
 #pragma unroll
     for (int t = 0; t < NTL; t++) {
@@ -234,16 +279,22 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
                                                  float* __restrict__ logits, float* __restrict__ vout,
                                                  const uint8_t* __restrict__ active) {
     constexpr int LD = (H > 128 ? H : 128) + 4;      // X also holds the 128-wide v_head hidden
+    constexpr int SA = H + 8;                        // plane row stride (halves): conflict-free b128 reads
     constexpr int NT = H >= 16 * WAVES ? H / (16 * WAVES) : 1;  // 16-col tiles per wave, H-wide layers
     constexpr int NACT = H / (16 * NT);              // waves owning columns of the H-wide layers
     constexpr int VPL = H / 64;                      // values per lane in row passes
-    constexpr int KB = H / 16;
-    constexpr int RW = KB * NT <= 32 ? KB : 32 / NT;  // trunk ring depth: <= 32 fragments per lane
+    constexpr int KS = H / 32;                       // 32-deep slices of an H-deep layer
+#ifndef YK_RCAP
+#define YK_RCAP 16
+#endif
+    constexpr int RCAP = H >= 512 ? 8 : YK_RCAP;      // ring slices x tiles held per wave (VGPR budget)
+    constexpr int RW = KS * NT <= RCAP ? KS : RCAP / NT;  // trunk ring depth (slices)
     constexpr int NVS = vstat_size(H), NVB = 6 * H;
+    constexpr int TSZ = ROWS * LD > ROWS * SA ? ROWS * LD : ROWS * SA;  // T, or a_v's plane pair
     static_assert(128 / 16 == WAVES, "v_head.2 maps one 16-column tile to each wave");
     __shared__ __attribute__((aligned(16))) float X[ROWS * LD];
-    __shared__ __attribute__((aligned(16))) float T[ROWS * LD];
-    __shared__ __attribute__((aligned(16))) float F[ROWS * FPAD];
+    __shared__ __attribute__((aligned(16))) float T[TSZ];
+    __shared__ __attribute__((aligned(16))) _Float16 P[2 * ROWS * SA];  // the next GEMM's input planes
     __shared__ __attribute__((aligned(16))) float VS[NVS];  // static vectors (yk_net.h VS_*)
     __shared__ __attribute__((aligned(16))) float VB[NVB];  // this block's b1 g1 be1 b2 g2 be2
 
@@ -272,7 +323,7 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
         for (int k = 0; k < PER; k++)
             if (tid + NTHR * k < NV4) reinterpret_cast<float4*>(VS)[tid + NTHR * k] = v[k];
     }
-    // featurize (state_to_vec, NNet.py:65-86), zero padded to K = 64
+    // featurize (state_to_vec, NNet.py:65-86) straight into the input layer's planes, K = 64
 #pragma unroll
     for (int k = 0; k < ROWS * 64 / NTHR; k++) {
         const int idx = tid + NTHR * k, rr = idx >> 6, f = idx & 63;
@@ -294,21 +345,24 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
                 val = feature(s, f);
             }
         }
-        F[rr * FPAD + f] = val;
+        const float one[1] = {val};
+        put_planes<1>(P, SA, rr, f, one);
     }
-    // weight stream: the input layer, then the trunk ring's first RW k-blocks of fc1 (block 0)
-    float4 w0[4][NT];
-    float4 ring[RW][NT];
-    const float* w_first = net.NB > 0 ? net.w1 : net.w_v1;
+    // weight stream: the input layer, then the trunk ring's first RW slices of fc1 (block 0)
+    W2 w0[2][NT];
+    W2 ring[RW][NT];
+    const float* w_first = net.w1;
     if (gw) {
 #pragma unroll
-        for (int kb = 0; kb < 4; kb++)
+        for (int ks = 0; ks < 2; ks++)
 #pragma unroll
-            for (int t = 0; t < NT; t++) w0[kb][t] = ld_frag(net.w_in, 4, nt0 + t, kb, lane);
+            for (int t = 0; t < NT; t++) w0[ks][t] = ld_w2(net.w_in, 2, nt0 + t, ks, lane);
+    }
+    if (gw && net.NB > 0) {
 #pragma unroll
-        for (int kb = 0; kb < RW; kb++)
+        for (int ks = 0; ks < RW; ks++)
 #pragma unroll
-            for (int t = 0; t < NT; t++) ring[kb][t] = ld_frag(w_first, KB, nt0 + t, kb, lane);
+            for (int t = 0; t < NT; t++) ring[ks][t] = ld_w2(w_first, KS, nt0 + t, ks, lane);
     }
     lds_barrier();
     TSTAMP(1);
@@ -316,26 +370,25 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
     floatx4 acc[NT];
     // inp: Linear -> LayerNorm -> SiLU (-> Dropout, identity in eval)  YachtNNet.py:30-35
     if (gw) {
-        const float* ap = F + (lane & 15) * FPAD + 4 * (lane >> 4);
-        floatx4 acc2[NT];
+        const APtr ap = a_ptr(P, SA);
+        Acc3 c[NT];
 #pragma unroll
-        for (int t = 0; t < NT; t++) acc[t] = acc2[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+        for (int t = 0; t < NT; t++) acc_zero(c[t]);
 #pragma unroll
-        for (int kb = 0; kb < 4; kb++) {
-            const float4 a = *reinterpret_cast<const float4*>(ap + 16 * kb);
+        for (int ks = 0; ks < 2; ks++) {
+            const float4 ah = ld_a(ap.h, ks), al = ld_a(ap.l, ks);
 #pragma unroll
             for (int t = 0; t < NT; t++) {
-                acc[t] = mfma4(a.x, w0[kb][t].x, acc[t]);
-                acc2[t] = mfma4(a.y, w0[kb][t].y, acc2[t]);
-                acc[t] = mfma4(a.z, w0[kb][t].z, acc[t]);
-                acc2[t] = mfma4(a.w, w0[kb][t].w, acc2[t]);
+                c[t].m = mfma16(ah, w0[ks][t].h, c[t].m);
+                c[t].c = mfma16(ah, w0[ks][t].l, c[t].c);
+                c[t].c = mfma16(al, w0[ks][t].h, c[t].c);
             }
         }
 #pragma unroll
-        for (int t = 0; t < NT; t++) acc[t] += acc2[t];
+        for (int t = 0; t < NT; t++) acc[t] = combine(c[t]);
         store_acc<NT>(T, LD, nt0, acc, nullptr);
     }
-    lds_barrier();
+    lds_barrier();  // T complete; every wave is done reading the feature planes
 #pragma unroll
     for (int rr = 0; rr < RPW; rr++) {
         const int r = wave * RPW + rr;
@@ -344,7 +397,11 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
         for (int i = 0; i < VPL; i++) x[i] = T[r * LD + c0 + i] + VS[VS_BIN * H + c0 + i];
         layernorm<VPL>(x, VS + VS_GIN * H, VS + VS_BEIN * H, c0, H);
 #pragma unroll
-        for (int i = 0; i < VPL; i++) X[r * LD + c0 + i] = silu(x[i]);
+        for (int i = 0; i < VPL; i++) {
+            x[i] = silu(x[i]);
+            X[r * LD + c0 + i] = x[i];
+        }
+        put_planes<VPL>(P, SA, r, c0, x);
     }
     lds_barrier();
     TSTAMP(2);
@@ -357,13 +414,13 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
         float4 vb[PB];
 #pragma unroll
         for (int k = 0; k < PB; k++) vb[k] = reinterpret_cast<const float4*>(net.vblk + (long)b * NVB)[min(tid + NTHR * k, NB4 - 1)];
-        if (gw) mma_ring<H, NT, RW>(X, LD, ring, acc, net.w1 + wo, net.w2 + wo, nt0);
+        if (gw) mma_ring<H, NT, RW>(P, SA, ring, acc, net.w1 + wo, net.w2 + wo, nt0);
         if (b == 2) TSTAMP(16);
 #pragma unroll
         for (int k = 0; k < PB; k++)  // the previous block's readers passed a barrier
             if (tid + NTHR * k < NB4) reinterpret_cast<float4*>(VB)[tid + NTHR * k] = vb[k];
         if (gw) store_acc<NT>(T, LD, nt0, acc, nullptr);
-        lds_barrier();
+        lds_barrier();  // T complete; every wave is done reading x's planes
         if (b == 2) TSTAMP(17);
 #pragma unroll
         for (int rr = 0; rr < RPW; rr++) {
@@ -372,20 +429,17 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
 #pragma unroll
             for (int i = 0; i < VPL; i++) x[i] = silu(T[r * LD + c0 + i] + VB[c0 + i]);
             layernorm<VPL>(x, VB + H, VB + 2 * H, c0, H);
-#pragma unroll
-            for (int i = 0; i < VPL; i++) T[r * LD + c0 + i] = x[i];
+            put_planes<VPL>(P, SA, r, c0, x);  // fc2's input
         }
         lds_barrier();
         if (b == 2) TSTAMP(18);
         if (gw) {
-            if (b + 1 < net.NB) mma_ring<H, NT, RW>(T, LD, ring, acc, net.w2 + wo, after, nt0);
-            else mma_ring<H, NT, RW, false>(T, LD, ring, acc, net.w2 + wo, nullptr, nt0);
+            if (b + 1 < net.NB) mma_ring<H, NT, RW>(P, SA, ring, acc, net.w2 + wo, after, nt0);
+            else mma_ring<H, NT, RW, false>(P, SA, ring, acc, net.w2 + wo, nullptr, nt0);
         }
         if (b == 2) TSTAMP(19);
-        lds_barrier();  // every wave is done reading T
-        if (b == 2) TSTAMP(20);
         if (gw) store_acc<NT>(T, LD, nt0, acc, nullptr);
-        lds_barrier();
+        lds_barrier();  // T complete; every wave is done reading h's planes
         if (b == 2) TSTAMP(21);
 #pragma unroll
         for (int rr = 0; rr < RPW; rr++) {
@@ -395,7 +449,11 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
             for (int i = 0; i < VPL; i++) x[i] = silu(T[r * LD + c0 + i] + VB[3 * H + c0 + i]);
             layernorm<VPL>(x, VB + 4 * H, VB + 5 * H, c0, H);
 #pragma unroll
-            for (int i = 0; i < VPL; i++) X[r * LD + c0 + i] += x[i];
+            for (int i = 0; i < VPL; i++) {
+                x[i] += X[r * LD + c0 + i];
+                X[r * LD + c0 + i] = x[i];
+            }
+            if (b + 1 < net.NB) put_planes<VPL>(P, SA, r, c0, x);  // the next fc1's input
         }
         lds_barrier();
         if (b < 6) TSTAMP(3 + b);
@@ -403,11 +461,12 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
 
     // heads: pi_head = LN -> SiLU -> Linear; v_head = LN -> SiLU -> Linear -> SiLU -> Linear -> tanh.
     // One ring streams v_head.2 (one 16-column tile per wave, first) and then the policy head;
-    // its first k-blocks fly under the LayerNorms.
-    constexpr int RD = PW < KB ? PW : KB;  // policy ring depth (k-blocks)
-    float4 pring[RD][PCH];
+    // its first slices fly under the LayerNorms.  a_pi's planes go to P, a_v's to T's storage.
+    constexpr int RD = PW < KS ? PW : KS;  // policy ring depth (slices)
+    _Float16* PV = reinterpret_cast<_Float16*>(T);
+    W2 pring[RD][PCH];
 #pragma unroll
-    for (int kb = 0; kb < RD; kb++) pring[kb][0] = ld_frag(net.w_v1, KB, wave, kb, lane);
+    for (int ks = 0; ks < RD; ks++) pring[ks][0] = ld_w2(net.w_v1, KS, wave, ks, lane);
 #pragma unroll
     for (int rr = 0; rr < RPW; rr++) {
         const int r = wave * RPW + rr;
@@ -418,9 +477,11 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
         layernorm<VPL>(y, VS + VS_GV * H, VS + VS_BEV * H, c0, H);
 #pragma unroll
         for (int i = 0; i < VPL; i++) {
-            X[r * LD + c0 + i] = silu(x[i]);  // a_pi (each wave rewrites only its own rows)
-            T[r * LD + c0 + i] = silu(y[i]);  // a_v
+            x[i] = silu(x[i]);  // a_pi
+            y[i] = silu(y[i]);  // a_v
         }
+        put_planes<VPL>(P, SA, r, c0, x);
+        put_planes<VPL>(PV, SA, r, c0, y);
     }
     lds_barrier();
     TSTAMP(9);
@@ -435,23 +496,21 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
     // the same weight lines at the same moment (each tile's k order, hence the numerics, is fixed)
     const int rot = blockIdx.x % FULL;
     auto chunk_tb = [&](int c) { return wave + WAVES * PCH * ((c + rot) % FULL); };
-    ring_chunk<KB, 1, PCH>(T, LD, pring, av, net.w_v1, wave, net.w_pi, chunk_tb(0));
+    ring_chunk<KS, 1, PCH>(PV, SA, pring, av, net.w_v1, wave, net.w_pi, chunk_tb(0));
 #pragma unroll 1
     for (int c = 0; c + 1 < FULL; c++) {
-        pi_chunk<KB, PCH, PCH>(X, LD, pring, net.w_pi, chunk_tb(c), chunk_tb(c + 1), bpi, logits, row0, n);
+        pi_chunk<KS, PCH, PCH>(P, SA, pring, net.w_pi, chunk_tb(c), chunk_tb(c + 1), bpi, logits, row0, n);
         if (c & 1) TSTAMP(10 + (c >> 1));  // stamps 10, 11 after chunk pairs
     }
     {
         const int tl = wave + WAVES * PCH * FULL;  // the padded last chunk
-        pi_chunk<KB, PCH, LASTN>(X, LD, pring, net.w_pi, chunk_tb(FULL - 1), tl, bpi, logits, row0, n);
+        pi_chunk<KS, PCH, LASTN>(P, SA, pring, net.w_pi, chunk_tb(FULL - 1), tl, bpi, logits, row0, n);
         TSTAMP(12);
-        pi_chunk<KB, LASTN, 0>(X, LD, pring, net.w_pi, tl, 0, bpi, logits, row0, n);
+        pi_chunk<KS, LASTN, 0>(P, SA, pring, net.w_pi, tl, 0, bpi, logits, row0, n);
     }
     TSTAMP(14);
     WSTAMP(24);
-    lds_barrier();  // every wave is done reading a_pi (X)
-    TSTAMP(22);
-    store_acc<1>(X, LD, wave, av, VS + VS_BV1 * H);
+    store_acc<1>(X, LD, wave, av, VS + VS_BV1 * H);  // X (the trunk output) was read by the head LNs only
     lds_barrier();
     TSTAMP(23);
 #pragma unroll
@@ -556,16 +615,22 @@ int yk_net_create(yk_net_t** out, int H, int NB, const float* const* p, int npar
     // host staging of the device layout (every block 256-byte aligned)
     std::vector<float> h;
     auto put = [&](size_t n) { size_t o = h.size(); h.resize(o + ((n + 63) / 64) * 64, 0.f); return o; };
-    // torch [N][K] row-major (K valid columns) -> fragment order, N padded to Np, K to Kp
+    // torch [N][K] row-major (K valid columns) -> fp16 hi / lo planes in MFMA fragment order
+    // (yk_net.h), N padded to Np, K to Kp; same footprint as the f32 matrix
     auto pack = [&](size_t dst, const float* W, int N, int K, int Np, int Kp) {
-        const int KBp = Kp / 16;
+        const int KSp = Kp / 32;
+        _Float16* o = reinterpret_cast<_Float16*>(h.data() + dst);
         for (int nt = 0; nt < Np / 16; nt++)
-            for (int kb = 0; kb < KBp; kb++)
+            for (int ks = 0; ks < KSp; ks++)
                 for (int l = 0; l < 64; l++)
-                    for (int i = 0; i < 4; i++) {
-                        const int nn = 16 * nt + (l & 15), kk = 16 * kb + 4 * (l >> 4) + i;
-                        h[dst + (((size_t)nt * KBp + kb) * 64 + l) * 4 + i] =
-                            (nn < N && kk < K) ? W[(size_t)nn * K + kk] : 0.f;
+                    for (int j = 0; j < 8; j++) {
+                        const int nn = 16 * nt + (l & 15), kk = 32 * ks + 8 * (l >> 4) + j;
+                        const float x = (nn < N && kk < K) ? W[(size_t)nn * K + kk] : 0.f;
+                        const _Float16 hi = (_Float16)x;
+                        const _Float16 lo = (_Float16)((x - (float)hi) * SPLIT);
+                        const size_t base = (((size_t)nt * KSp + ks) * 2 * 64 + l) * 8 + j;
+                        o[base] = hi;
+                        o[base + 64 * 8] = lo;
                     }
     };
     const size_t o_win = put((size_t)H * 64), o_bin = put(H), o_gin = put(H), o_bein = put(H);

@@ -17,7 +17,7 @@ net = YkNet(YachtNNet(hidden=256, nblocks=6).state_dict(), 256, 6)
 eng = SelfPlayEngine(E, sims, 1.5, 15, net=net, max_moves=64)
 L = lib()
 L.yk_diag_select.argtypes = [C.c_void_p, C.c_int]
-out = np.zeros((E, 8), dtype=np.uint64)
+out = np.zeros((E, 16), dtype=np.uint64)
 eng.run(0, 0)
 L.yk_diag_select(out.ctypes.data, E)  # discard the warm-up
 eng.profile(True)
@@ -35,3 +35,10 @@ for k, nm in enumerate(names):
     c = out[:, k].astype(np.float64).sum()
     print(f"  {nm:28s} {c / (E * st['sims']):9.0f} cycles per game-sim  ({100 * c / per:5.1f}% of descent)")
 print(f"  max descent per game-sim    {tot.max() / st['sims']:9.0f}")
+ex = out[:, 6].astype(np.float64).sum()
+print(f"  expand + backup (fused kernel) {ex / (E * st['sims']):9.0f} cycles per game-sim")
+for k, nm in ((8, "expand: logits load, max, sum-exp"), (9, "expand: mask + pairwise sum"),
+              (10, "expand: P / slot write"), (12, "backup")):
+    print(f"    {nm:34s} {out[:, k].astype(np.float64).sum() / (E * st['sims']):9.0f} cycles per game-sim")
+print(f"expand_backup kernel: {kt['expand_backup_select'][0] / kt['expand_backup_select'][1] * 1e3:.1f} us avg")
+print(f"forward kernel: {kt['forward'][0] / kt['forward'][1] * 1e3:.1f} us avg")

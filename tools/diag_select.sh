@@ -4,9 +4,9 @@
 cd "$(dirname "$0")/.." || exit 2
 set -e
 mkdir -p /tmp/yk_diag
-for f in yk_env yk_net yk_engine; do
-  /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -fPIC -std=c++17 -ffp-contract=off -DYK_SEL_TIMING \
+for f in yk_env yk_net yk_engine yk_train; do
+  /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -fPIC -std=c++17 -ffp-contract=off -DYK_SEL_TIMING $YK_EXTRA \
      -Iinclude -Inypc-yacht-auction_amd/csrc -c nypc-yacht-auction_amd/csrc/$f.hip -o /tmp/yk_diag/$f.o
 done
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o /tmp/yk_diag/libyacht_hip.so /tmp/yk_diag/*.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o /tmp/yk_diag/libyacht_hip.so /tmp/yk_diag/*.o -L/opt/rocm/lib -lrocblas -Wl,-rpath,/opt/rocm/lib
 YK_LIB_PATH=/tmp/yk_diag/libyacht_hip.so timeout -k 5 200 python tools/diag_select.py "$@"
