@@ -198,40 +198,6 @@ struct ValidQ {
         return c_tab.comb_max[ci] < n;
     }
 };
-// validity over one pairwise leaf [st, st + len), len < 252: runs [.., b1) v0, [b1, b2) v1,
-// [b2, ..) v2 - exact for the bid phase and for 10 carried dice; `generic` otherwise
-struct LeafRuns {
-    int b1, b2;
-    bool v0, v1, v2, generic;
-    __device__ __forceinline__ bool operator()(int a) const { return a < b1 ? v0 : (a < b2 ? v1 : v2); }
-};
-__device__ __forceinline__ LeafRuns leaf_runs(const ValidQ& q, int st) {
-    LeafRuns r{INT_MAX, INT_MAX, false, false, false, false};
-    if (q.mode == 1) {
-        r.b1 = NBID;
-        r.v0 = true;
-    } else if (q.mode == 0) {
-        if (q.n < 10) {
-            r.generic = true;
-            return r;
-        }
-        auto unused = [&](int c) { return c < NCAT && !((q.used >> c) & 1u); };
-        if (st < NBID) {
-            r.b1 = NBID;
-            r.v1 = unused(0);
-            r.b2 = NBID + NCOMB;
-            r.v2 = unused(1);
-        } else {
-            const int c = (st - NBID) / NCOMB;
-            r.v0 = unused(c);
-            r.b1 = NBID + NCOMB * (c + 1);
-            r.v1 = unused(c + 1);
-            r.b2 = r.b1 + NCOMB;
-            r.v2 = unused(c + 2);
-        }
-    }
-    return r;
-}
 __device__ __forceinline__ ValidQ valid_q(const YkS& s) {
     ValidQ q;
     const int round = s_round(s), phase = s_phase(s);
@@ -741,31 +707,20 @@ __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int l
             if (lane == 0) d.rec_v[(long)e * d.max_exp + pidx] = v;
         }
         SEL_T0(t_x1);
-        // mask with the valid moves.  With the carry sizes of real play the valid set is a union
-        // of whole runs (the 202 bids, or the 252 actions of each unused category), and a leaf
-        // (<= 106 positions) meets at most three of them: validity is two compares per element.
-        const LeafRuns runs = leaf_runs(valid, st);
-        auto mask_leaf = [&](auto vok) {
+        // mask with the valid moves
 #pragma unroll
-            for (int j = 0; j < PW_GMAX; j++) {
-                const int a = st + 8 * j + 4 * h;
-                if (j < G) {
-                    if (!vok(a)) q[j].x = 0.f;
-                    if (!vok(a + 1)) q[j].y = 0.f;
-                    if (!vok(a + 2)) q[j].z = 0.f;
-                    if (!vok(a + 3)) q[j].w = 0.f;
-                }
+        for (int j = 0; j < PW_GMAX; j++) {
+            const int a = st + 8 * j + 4 * h;
+            if (j < G) {
+                if (!valid(a)) q[j].x = 0.f;
+                if (!valid(a + 1)) q[j].y = 0.f;
+                if (!valid(a + 2)) q[j].z = 0.f;
+                if (!valid(a + 3)) q[j].w = 0.f;
             }
+        }
 #pragma unroll
-            for (int r = 0; r < PW_TMAX; r++)
-                if (h == 0 && r < R && !vok(st + 8 * G + r)) qt[r] = 0.f;
-        };
-#ifdef YK_NO_LEAF_RUNS
-        mask_leaf(valid);
-#else
-        if (runs.generic) mask_leaf(valid);  // wave-uniform
-        else mask_leaf(runs);
-#endif
+        for (int r = 0; r < PW_TMAX; r++)
+            if (h == 0 && r < R && !valid(st + 8 * G + r)) qt[r] = 0.f;
         // numpy pairwise_sum on the leaf: r_k = a[k] + a[8 + k] + ..., then
         // ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)), then the tail one by one
         float4 racc = q[0];

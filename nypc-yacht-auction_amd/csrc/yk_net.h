@@ -10,16 +10,18 @@ namespace yk {
 constexpr int PI_LD = 3264;         // logits row stride: 3226 padded to 204 tiles of 16 columns
 constexpr int PI_TILES = PI_LD / 16;
 
-// Dense weights are stored in MFMA fragment order ("packed"): for a [N][K] matrix,
-//   P[nt][kb][lane][i] = W[16 nt + (lane & 15)][16 kb + 4 (lane >> 4) + i]
-// so one wave loads a 16-column x 16-deep slice as one contiguous 1 KB float4 access.
+// Dense weights are stored as two fp16 planes (hi = fp16(w), lo = fp16((w - hi) * 2^11)) in
+// v_mfma_f32_16x16x32_f16 fragment order ("packed"): for a [N][K] matrix,
+//   P[nt][ks][plane][lane][j] = plane(W[16 nt + (lane & 15)][32 ks + 8 (lane >> 4) + j]),  j < 8
+// so one wave loads one plane of a 16-column x 32-deep slice as one contiguous 1 KB access;
+// a packed matrix takes the bytes of the f32 one.
 struct NetDev {
     int H, NB;
-    const float *w_in, *b_in, *g_in, *be_in;  // w_in packed [H/16][4][64][4] (K 59 padded to 64)
-    const float *w1, *b1, *g1, *be1;          // per block: packed [H/16][H/16][64][4], vectors [H]
+    const float *w_in, *b_in, *g_in, *be_in;  // w_in packed [H/16][2][2][64][8 fp16] (K 59 padded to 64)
+    const float *w1, *b1, *g1, *be1;          // per block: packed [H/16][H/32][2][64][8 fp16], vectors [H]
     const float *w2, *b2, *g2, *be2;
-    const float *g_pi, *be_pi, *w_pi, *b_pi;  // w_pi packed [204][H/16][64][4] (rows >= 3226 zero), b_pi [3264]
-    const float *g_v, *be_v, *w_v1, *b_v1, *w_v2, *b_v2;  // w_v1 packed [8][H/16][64][4], w_v2 [128], b_v2 [1]
+    const float *g_pi, *be_pi, *w_pi, *b_pi;  // w_pi packed [204][H/32][2][64][8] (rows >= 3226 zero), b_pi [3264]
+    const float *g_v, *be_v, *w_v1, *b_v1, *w_v2, *b_v2;  // w_v1 packed [8][H/32][2][64][8], w_v2 [128], b_v2 [1]
     const float* vstat;  // copies staged to LDS once: [VS_* x H] + b_v1[128] w_v2[128] + b_pi[3264]
     const float* vblk;   // per block b: b1 g1 be1 b2 g2 be2 ([6][H]), staged to LDS per block
 };

@@ -1,17 +1,22 @@
 // yk_net.hip - NNetWrapper.predict (yacht/NNet.py:177-195) over YachtNNet
-// (yacht/pytorch/YachtNNet.py:8-70), batched over all pending leaves, float32.
+// (yacht/pytorch/YachtNNet.py:8-70), batched over all pending leaves, f32-equivalent.
 //
 // One kernel, k_forward, carries all 3,320,576 FLOP per row (hidden 256, 6 blocks): a
 // 512-thread workgroup (8 waves, 2 per SIMD, up to 256 VGPRs each) owns 16 rows and keeps
 // their activations in LDS through featurize -> Linear/LN/SiLU -> 6 x ResidualBlock -> head
-// LayerNorms -> value head and policy logits (204 x 16 columns).  Every dense layer runs on
-// v_mfma_f32_16x16x4_f32 (exact f32: fmaf chains), so results track torch's float32 CPU path
-// within the north star's 1e-5 (tests/test_gpu_net.py).
+// LayerNorms -> value head and policy logits (204 x 16 columns).  Every dense product is
+// f32-equivalent: weights and GEMM inputs are held as fp16 planes hi = fp16(x) and
+// lo = fp16((x - hi) 2^11), and a 16x16x32 tile is hi*hi + 2^-11 (hi*lo + lo*hi) - three
+// v_mfma_f32_16x16x32_f16 with exact products and f32 accumulation (the dropped lo*lo term
+// is 2^-22 relative).  Results track torch's float32 path within the north star's 1e-5
+// (tests/test_gpu_net.py) at 1/5 of the MFMA cycles of v_mfma_f32_16x16x4_f32.
 //
-// The kernel is latency-bound per workgroup (one per CU), so the weight stream must never
-// stop: weights are pre-packed in MFMA fragment order (yk_net.h), each wave keeps a ring of
-// W k-blocks of its fragments in registers, and as soon as a k-block is consumed its
-// registers are refilled with the fragment W k-blocks ahead - across layer boundaries, so the
+// The kernel is latency-bound per workgroup (one per CU), and on this chip a CU does not
+// overlap MFMA execution with its vector-memory stream (tools/stream_bench.hip), so the weight
+// stream must never stop and the MFMA time must be small: weights are pre-packed in MFMA
+// fragment order (yk_net.h), each wave keeps a ring of W slices of its fragments in registers,
+// and as soon as a slice is consumed its registers are refilled with the slice W ahead - across
+// layer boundaries, so the
 // next layer streams in under the current GEMM and the LayerNorm phase.  Nothing the kernel
 // waits on is ever issued behind that stream (vmcnt retires in order): biases and LayerNorm
 // vectors live in LDS, and the kernel must not spill (scratch also counts in vmcnt).

@@ -2,7 +2,7 @@
 # diagnostic: bench kernel times for expand-kernel build variants (GPU box)
 cd "$(dirname "$0")/.." || exit 2
 set -e
-for v in "" "-DYK_NO_LEAF_RUNS" "-DYK_EXPAND_WPE=3" "-DYK_EXPAND_WPE=3 -DYK_NO_LEAF_RUNS"; do
+for v in "" "-DYK_EXPAND_WPE=3"; do
   make -s -C nypc-yacht-auction_amd clean > /dev/null
   make -s -C nypc-yacht-auction_amd EXTRA="$v" > /dev/null
   echo "[$v]"
