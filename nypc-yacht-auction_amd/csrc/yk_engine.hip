@@ -95,6 +95,7 @@ struct EngDev {
     uint32_t* res_t;
     const float* logits;   // [E][PI_LD]
     const float* vpred;    // [E]
+    const float2* mlse;    // [E] per-row (max, log sum exp) of the logits, from the forward
     const float* lut_sq;
     const float* lut_sqe;
     // records
@@ -649,8 +650,32 @@ __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int l
         const int pidx = (int)d.gstats[(long)e * 8 + 0];
         const bool rec = d.rec_pred && pidx < d.max_exp;
         float* rpi = rec ? d.rec_pi + ((long)e * d.max_exp + pidx) * ASIZE : nullptr;
-        if (d.prior == 0) {
-            // pi = exp(log_softmax(logits))  (NNet.py:193); predict row = game
+        bool masked = false;  // q / qt already hold Ps * valids
+        if (d.prior == 0 && !rec) {
+            // pi = exp(log_softmax(logits)) (NNet.py:193) at the valid actions only: the forward
+            // supplies each row's (max, log sum exp), so the invalid logits are never read
+            const float* x = d.logits + (long)e * PI_LD + st;
+            const float2 ml = d.mlse[e];
+            mx = ml.x;
+            lse = ml.y;
+#pragma unroll
+            for (int j = 0; j < PW_GMAX; j++) {
+                const int a = st + 8 * j + 4 * h;
+                const bool v0 = j < G && valid(a), v1 = j < G && valid(a + 1), v2 = j < G && valid(a + 2),
+                           v3 = j < G && valid(a + 3);
+                float4 x4 = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (v0 || v1 || v2 || v3) x4 = *reinterpret_cast<const float4*>(x + 8 * j + 4 * h);
+                q[j] = make_float4(v0 ? softmax_p(x4.x, mx, lse) : 0.f, v1 ? softmax_p(x4.y, mx, lse) : 0.f,
+                                   v2 ? softmax_p(x4.z, mx, lse) : 0.f, v3 ? softmax_p(x4.w, mx, lse) : 0.f);
+            }
+#pragma unroll
+            for (int r = 0; r < PW_TMAX; r++)
+                qt[r] = (h == 0 && r < R && valid(st + 8 * G + r)) ? softmax_p(x[8 * G + r], mx, lse) : 0.f;
+            v = d.vpred[e];
+            masked = true;
+            SEL_ACC(8, t_x0);
+        } else if (d.prior == 0) {
+            // recording predictions: the whole pi row, max and sum over the 3226 logits here
             const float* x = d.logits + (long)e * PI_LD + st;
             const float NEG = -INFINITY;
 #pragma unroll
@@ -684,7 +709,6 @@ __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int l
 #pragma unroll
             for (int r = 0; r < PW_TMAX; r++) qt[r] = softmax_p(qt[r], m, lse);
             v = d.vpred[e];
-            SEL_ACC(8, t_x0);
         } else {
 #pragma unroll
             for (int j = 0; j < PW_GMAX; j++) {
@@ -711,7 +735,7 @@ __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int l
 #pragma unroll
         for (int j = 0; j < PW_GMAX; j++) {
             const int a = st + 8 * j + 4 * h;
-            if (j < G) {
+            if (j < G && !masked) {
                 if (!valid(a)) q[j].x = 0.f;
                 if (!valid(a + 1)) q[j].y = 0.f;
                 if (!valid(a + 2)) q[j].z = 0.f;
@@ -720,7 +744,7 @@ __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int l
         }
 #pragma unroll
         for (int r = 0; r < PW_TMAX; r++)
-            if (h == 0 && r < R && !valid(st + 8 * G + r)) qt[r] = 0.f;
+            if (h == 0 && r < R && !masked && !valid(st + 8 * G + r)) qt[r] = 0.f;
         // numpy pairwise_sum on the leaf: r_k = a[k] + a[8 + k] + ..., then
         // ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)), then the tail one by one
         float4 racc = q[0];
@@ -1059,6 +1083,7 @@ struct yk_engine {
     std::vector<void*> allocs;
     float* logits = nullptr;
     float* vpred = nullptr;
+    float2* mlse = nullptr;
     float *lut_sq = nullptr, *lut_sqe = nullptr;
     int32_t* done_count = nullptr;
     int32_t* host_done = nullptr;
@@ -1134,7 +1159,7 @@ int run_sims(yk_engine* eng, int sims, const uint32_t* env_ids, uint64_t* ctr, h
             prof_mark(eng, KC_FORWARD, s);
             // predict row = game: no compaction; workgroups without a leaf exit at once
             int rc = launch_forward(eng->net->dev, d.leaf_state, nullptr, nullptr, nullptr, d.E, eng->logits, eng->vpred, s,
-                                    d.leaf_flag);
+                                    d.leaf_flag, eng->mlse);
             if (rc) return rc;
         }
         prof_mark(eng, KC_EXPAND, s);
@@ -1225,6 +1250,7 @@ int yk_engine_create(yk_engine_t** out, const yk_engine_config_t* cfg, yk_net_t*
     A(d.res_v, E);
     A(d.res_t, E);
     A(eng->vpred, E);
+    A(eng->mlse, E);
     A(eng->lut_sq, (size_t)LUT_N);
     A(eng->lut_sqe, (size_t)LUT_N);
     A(d.rec_state, E * d.M);
@@ -1257,6 +1283,7 @@ int yk_engine_create(yk_engine_t** out, const yk_engine_config_t* cfg, yk_net_t*
     }
     d.logits = eng->logits;
     d.vpred = eng->vpred;
+    d.mlse = eng->mlse;
     d.lut_sq = eng->lut_sq;
     d.lut_sqe = eng->lut_sqe;
     hipLaunchKernelGGL(k_lut, dim3(LUT_N / 256), dim3(256), 0, 0, eng->lut_sq, eng->lut_sqe);

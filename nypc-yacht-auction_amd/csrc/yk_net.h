@@ -34,11 +34,13 @@ constexpr int vstat_size(int H) { return vs_bpi(H) + PI_LD; }
 // logits[n][PI_LD] (pi_head before softmax) and v[n] = tanh(v_head).  `rows` (optional) maps
 // output row i to input index rows[i]; `count` (optional, device) overrides n; `active`
 // (optional, device, [n]) lets a workgroup whose 16 rows are all inactive exit at once.
+// `mlse` (optional, device, [n]) gets each row's (max, log sum exp(x - max)) over the 3226
+// logits, so that exp(log_softmax(x))[a] = exp(x[a] - m - l) needs only the logits it is asked for.
 int launch_forward(const NetDev& net, const yk_state_t* states, const float* x, const int32_t* rows,
                    const int32_t* count, int n, float* logits, float* v, hipStream_t stream,
-                   const uint8_t* active = nullptr);
-// pi[n][3226] = exp(log_softmax(logits[:, :3226]))
-int launch_softmax(const float* logits, float* pi, int n, hipStream_t stream);
+                   const uint8_t* active = nullptr, float2* mlse = nullptr);
+// pi[n][3226] = exp(log_softmax(logits[:, :3226])) = exp(logits - m - l), (m, l) = mlse[row]
+int launch_softmax(const float* logits, const float2* mlse, float* pi, int n, hipStream_t stream);
 
 }  // namespace yk
 

@@ -253,26 +253,52 @@ __device__ __forceinline__ void ring_chunk(const _Float16* A, int sa, W2 (&ring)
 #pragma unroll
     for (int t = 0; t < NTL; t++) pa[t] = combine(c[t]);
 }
+// Running softmax statistics of one lane's rows (4 q + j): max and sum exp(x - max) over the
+// columns it has seen (online form); combined over lanes and waves at the end of the head.
+struct SoftStat {
+    float m[4], s[4];
+};
+__device__ __forceinline__ void stat_merge(float& m, float& s, float m2, float s2) {
+    const float mm = fmaxf(m, m2);
+    if (mm == -INFINITY) return;
+    s = s * __expf(m - mm) + s2 * __expf(m2 - mm);
+    m = mm;
+}
 template <int KS, int NTL, int NXT, int RD = (PW < KS ? PW : KS)>
 __device__ __forceinline__ void pi_chunk(const _Float16* A, int sa, W2 (&ring)[RD][PCH], const float* __restrict__ W,
                                          int tb, int tb_next, const float* bias, float* __restrict__ logits, int row0,
-                                         int n) {
+                                         int n, SoftStat& st) {
     const int lane = threadIdx.x & 63;
     floatx4 pa[NTL];
     ring_chunk<KS, NTL, NXT, RD>(A, sa, ring, pa, W, tb, W, tb_next);
     const int rr = lane & 15, q = lane >> 4;
+    bool ok[NTL];
 #pragma unroll
     for (int t = 0; t < NTL; t++) {
         const int tile = tb + WAVES * t;
+        const int col = 16 * tile + rr;
+        ok[t] = tile < PI_TILES && col < ASIZE;  // a real action column
         if (tile < PI_TILES) {
-            const int col = 16 * tile + rr;
             const float b = bias[col];
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 const int row = row0 + 4 * q + j;
-                if (row < n) logits[(long)row * PI_LD + col] = pa[t][j] + b;
+                pa[t][j] += b;
+                if (row < n) logits[(long)row * PI_LD + col] = pa[t][j];
             }
         }
+    }
+    // this chunk's columns into the running (max, sum exp): one rescale per row and chunk
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        float mn = st.m[j];
+#pragma unroll
+        for (int t = 0; t < NTL; t++) mn = ok[t] ? fmaxf(mn, pa[t][j]) : mn;
+        float acc = st.s[j] > 0.f ? st.s[j] * __expf(st.m[j] - mn) : 0.f;
+#pragma unroll
+        for (int t = 0; t < NTL; t++) acc += ok[t] ? __expf(pa[t][j] - mn) : 0.f;
+        st.m[j] = mn;
+        st.s[j] = acc;
     }
 }
 
@@ -282,7 +308,7 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
                                                  const float* __restrict__ xin, const int32_t* __restrict__ rows,
                                                  const int32_t* __restrict__ count, int n,
                                                  float* __restrict__ logits, float* __restrict__ vout,
-                                                 const uint8_t* __restrict__ active) {
+                                                 const uint8_t* __restrict__ active, float2* __restrict__ mlse) {
     constexpr int LD = (H > 128 ? H : 128) + 4;      // X also holds the 128-wide v_head hidden
     constexpr int SA = H + 8;                        // plane row stride (halves): conflict-free b128 reads
     constexpr int NT = H >= 16 * WAVES ? H / (16 * WAVES) : 1;  // 16-col tiles per wave, H-wide layers
@@ -502,21 +528,41 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
     const int rot = blockIdx.x % FULL;
     auto chunk_tb = [&](int c) { return wave + WAVES * PCH * ((c + rot) % FULL); };
     ring_chunk<KS, 1, PCH>(PV, SA, pring, av, net.w_v1, wave, net.w_pi, chunk_tb(0));
+    SoftStat st;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        st.m[j] = -INFINITY;
+        st.s[j] = 0.f;
+    }
 #pragma unroll 1
     for (int c = 0; c + 1 < FULL; c++) {
-        pi_chunk<KS, PCH, PCH>(P, SA, pring, net.w_pi, chunk_tb(c), chunk_tb(c + 1), bpi, logits, row0, n);
+        pi_chunk<KS, PCH, PCH>(P, SA, pring, net.w_pi, chunk_tb(c), chunk_tb(c + 1), bpi, logits, row0, n, st);
         if (c & 1) TSTAMP(10 + (c >> 1));  // stamps 10, 11 after chunk pairs
     }
     {
         const int tl = wave + WAVES * PCH * FULL;  // the padded last chunk
-        pi_chunk<KS, PCH, LASTN>(P, SA, pring, net.w_pi, chunk_tb(FULL - 1), tl, bpi, logits, row0, n);
+        pi_chunk<KS, PCH, LASTN>(P, SA, pring, net.w_pi, chunk_tb(FULL - 1), tl, bpi, logits, row0, n, st);
         TSTAMP(12);
-        pi_chunk<KS, LASTN, 0>(P, SA, pring, net.w_pi, tl, 0, bpi, logits, row0, n);
+        pi_chunk<KS, LASTN, 0>(P, SA, pring, net.w_pi, tl, 0, bpi, logits, row0, n, st);
     }
     TSTAMP(14);
     WSTAMP(24);
     store_acc<1>(X, LD, wave, av, VS + VS_BV1 * H);  // X (the trunk output) was read by the head LNs only
-    lds_barrier();
+    // softmax statistics of the policy logits per row: over the 16 column lanes, then the waves
+    float2* SS = reinterpret_cast<float2*>(T);  // T (a_v's planes) is no longer read
+    if (mlse) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+#pragma unroll
+            for (int o = 1; o < 16; o <<= 1)
+                stat_merge(st.m[j], st.s[j], __shfl_xor(st.m[j], o, 64), __shfl_xor(st.s[j], o, 64));
+        }
+    }
+    lds_barrier();  // every wave is done with v_head.2 (reads of T) and stored its av columns
+    if (mlse && (lane & 15) == 0) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) SS[wave * ROWS + 4 * (lane >> 4) + j] = make_float2(st.m[j], st.s[j]);
+    }
     TSTAMP(23);
 #pragma unroll
     for (int rr = 0; rr < RPW; rr++) {  // SiLU -> Linear(128, 1) -> tanh  YachtNNet.py:49-52,69
@@ -527,22 +573,27 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
         s = wave_sum(s);
         if (lane == 0 && row < n) vout[row] = tanhf(s + net.b_v2[0]);
     }
+    if (mlse) {
+        lds_barrier();
+        if (tid < ROWS && row0 + tid < n) {  // (max, log sum exp(x - max)) of the row: log_softmax = x - m - l
+            float m = -INFINITY, sm = 0.f;
+#pragma unroll
+            for (int w = 0; w < WAVES; w++) stat_merge(m, sm, SS[w * ROWS + tid].x, SS[w * ROWS + tid].y);
+            mlse[row0 + tid] = make_float2(m, __logf(sm));
+        }
+    }
     TSTAMP(15);
 }
 
-// exp(log_softmax(x)) over the first 3226 columns; one wavefront per row
-__global__ void k_softmax(const float* __restrict__ logits, float* __restrict__ pi, int n) {
+// exp(log_softmax(x)) over the first 3226 columns from the forward's per-row (max, log sum
+// exp): one wavefront per row
+__global__ void k_softmax(const float* __restrict__ logits, const float2* __restrict__ mlse, float* __restrict__ pi,
+                          int n) {
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (row >= n) return;
     const float* x = logits + (long)row * PI_LD;
-    float m = -INFINITY;
-    for (int a = lane; a < ASIZE; a += 64) m = fmaxf(m, x[a]);
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-    float s = 0.f;
-    for (int a = lane; a < ASIZE; a += 64) s += expf(x[a] - m);
-    const float lse = logf(wave_sum(s));
-    for (int a = lane; a < ASIZE; a += 64) pi[(long)row * ASIZE + a] = expf(x[a] - m - lse);
+    const float2 ml = mlse[row];
+    for (int a = lane; a < ASIZE; a += 64) pi[(long)row * ASIZE + a] = expf(x[a] - ml.x - ml.y);
 }
 
 // The submission bot's move (agent.py:248-280): softmax over all 3226 logits in f32, then the
@@ -588,23 +639,24 @@ __global__ void k_policy_pick(const float* __restrict__ logits, const yk_state_t
 namespace yk {
 
 int launch_forward(const NetDev& net, const yk_state_t* states, const float* x, const int32_t* rows,
-                   const int32_t* count, int n, float* logits, float* v, hipStream_t stream, const uint8_t* active) {
+                   const int32_t* count, int n, float* logits, float* v, hipStream_t stream, const uint8_t* active,
+                   float2* mlse) {
     if (n <= 0) return YK_OK;
     const dim3 grid((n + ROWS - 1) / ROWS), block(NTHR);
     switch (net.H) {
-        case 64: hipLaunchKernelGGL(k_forward<64>, grid, block, 0, stream, net, states, x, rows, count, n, logits, v, active); break;
-        case 128: hipLaunchKernelGGL(k_forward<128>, grid, block, 0, stream, net, states, x, rows, count, n, logits, v, active); break;
-        case 256: hipLaunchKernelGGL(k_forward<256>, grid, block, 0, stream, net, states, x, rows, count, n, logits, v, active); break;
-        case 512: hipLaunchKernelGGL(k_forward<512>, grid, block, 0, stream, net, states, x, rows, count, n, logits, v, active); break;
+        case 64: hipLaunchKernelGGL(k_forward<64>, grid, block, 0, stream, net, states, x, rows, count, n, logits, v, active, mlse); break;
+        case 128: hipLaunchKernelGGL(k_forward<128>, grid, block, 0, stream, net, states, x, rows, count, n, logits, v, active, mlse); break;
+        case 256: hipLaunchKernelGGL(k_forward<256>, grid, block, 0, stream, net, states, x, rows, count, n, logits, v, active, mlse); break;
+        case 512: hipLaunchKernelGGL(k_forward<512>, grid, block, 0, stream, net, states, x, rows, count, n, logits, v, active, mlse); break;
         default: return YK_ERR_ARG;
     }
     YK_LAUNCHED();
     return YK_OK;
 }
 
-int launch_softmax(const float* logits, float* pi, int n, hipStream_t stream) {
+int launch_softmax(const float* logits, const float2* mlse, float* pi, int n, hipStream_t stream) {
     if (n <= 0) return YK_OK;
-    hipLaunchKernelGGL(k_softmax, dim3((n + 3) / 4), dim3(256), 0, stream, logits, pi, n);
+    hipLaunchKernelGGL(k_softmax, dim3((n + 3) / 4), dim3(256), 0, stream, logits, mlse, pi, n);
     YK_LAUNCHED();
     return YK_OK;
 }
@@ -713,9 +765,10 @@ static int predict_common(yk_net_t* net, const yk_state_t* states, const float* 
     if (n == 0) return YK_OK;
     hipStream_t s = as_stream(stream);
     float* logits = nullptr;
-    YK_HIP(hipMallocAsync((void**)&logits, sizeof(float) * (size_t)n * PI_LD, s));
-    int rc = launch_forward(net->dev, states, x, nullptr, nullptr, n, logits, v, s);
-    if (rc == YK_OK) rc = launch_softmax(logits, pi, n, s);
+    YK_HIP(hipMallocAsync((void**)&logits, sizeof(float) * ((size_t)n * PI_LD + 2 * (size_t)n), s));
+    float2* mlse = reinterpret_cast<float2*>(logits + (size_t)n * PI_LD);
+    int rc = launch_forward(net->dev, states, x, nullptr, nullptr, n, logits, v, s, nullptr, mlse);
+    if (rc == YK_OK) rc = launch_softmax(logits, mlse, pi, n, s);
     (void)hipFreeAsync(logits, s);
     return rc;
 }
