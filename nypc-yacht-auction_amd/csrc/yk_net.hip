@@ -332,10 +332,15 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
     if (count) n = min(n, *count);
     const int row0 = blockIdx.x * ROWS;
     if (row0 >= n) return;
-    if (active) {  // uniform: every wave reads the same 16 flags
+    if (active) {  // uniform: every wave reads the same 16 flags (one scalar load when whole)
         bool any = false;
+        if (row0 + ROWS <= n && (reinterpret_cast<uintptr_t>(active) & 15) == 0) {
+            const uint4 a4 = *reinterpret_cast<const uint4*>(active + row0);
+            any = (a4.x | a4.y | a4.z | a4.w) != 0;
+        } else {
 #pragma unroll
-        for (int i = 0; i < ROWS; i++) any |= row0 + i < n && active[row0 + i];
+            for (int i = 0; i < ROWS; i++) any |= row0 + i < n && active[row0 + i];
+        }
         if (!any) return;
     }
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -344,7 +349,10 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
     const int c0 = lane * VPL;
     TSTAMP(0);
 
-    // static vectors first: their LDS writes must not wait behind the weight stream
+    // loads in the order they are needed: the static vectors first (their LDS writes must not
+    // wait behind the weight stream: vmcnt retires in order), then each wave's two state rows by
+    // scalar loads (wave-uniform addresses: SMEM, lgkmcnt), then the weight stream - the input
+    // layer and the trunk ring's first RW slices of fc1 - and only then the features
     {
         constexpr int NV4 = NVS / 4, PER = (NV4 + NTHR - 1) / NTHR;
         float4 v[PER];
@@ -354,32 +362,20 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
         for (int k = 0; k < PER; k++)
             if (tid + NTHR * k < NV4) reinterpret_cast<float4*>(VS)[tid + NTHR * k] = v[k];
     }
-    // featurize (state_to_vec, NNet.py:65-86) straight into the input layer's planes, K = 64
+    constexpr int FPT = ROWS * 64 / NTHR;  // feature rows per wave (row = wave + WAVES k)
+    static_assert(FPT * WAVES == ROWS, "one feature row per wave and k");
+    YkS fs[FPT];
+    if (!xin) {
 #pragma unroll
-    for (int k = 0; k < ROWS * 64 / NTHR; k++) {
-        const int idx = tid + NTHR * k, rr = idx >> 6, f = idx & 63;
-        const int row = row0 + rr;
-        float val = 0.f;
-        if (row < n && f < FEAT) {
-            const int src = rows ? rows[row] : row;
-            if (xin) {
-                val = xin[(long)src * FEAT + f];
-            } else {
-                const uint4* p = reinterpret_cast<const uint4*>(states + src);
-                YkS s;
+        for (int k = 0; k < FPT; k++) {
+            const int row = row0 + wave + WAVES * k;
+            int src = row < n ? (rows ? rows[row] : row) : 0;
+            src = __builtin_amdgcn_readfirstlane(src);
+            const uint64_t* p = reinterpret_cast<const uint64_t*>(states + src);
 #pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    uint4 u = p[q];
-                    s.w[2 * q] = (uint64_t)u.x | ((uint64_t)u.y << 32);
-                    s.w[2 * q + 1] = (uint64_t)u.z | ((uint64_t)u.w << 32);
-                }
-                val = feature(s, f);
-            }
+            for (int q = 0; q < 8; q++) fs[k].w[q] = p[q];
         }
-        const float one[1] = {val};
-        put_planes<1>(P, SA, rr, f, one);
     }
-    // weight stream: the input layer, then the trunk ring's first RW slices of fc1 (block 0)
     W2 w0[2][NT];
     W2 ring[RW][NT];
     const float* w_first = net.w1;
@@ -394,6 +390,16 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
         for (int ks = 0; ks < RW; ks++)
 #pragma unroll
             for (int t = 0; t < NT; t++) ring[ks][t] = ld_w2(w_first, KS, nt0 + t, ks, lane);
+    }
+    // featurize (state_to_vec, NNet.py:65-86) straight into the input layer's planes, K = 64
+#pragma unroll
+    for (int k = 0; k < FPT; k++) {
+        const int rr = wave + WAVES * k, f = lane;
+        const int row = row0 + rr;
+        float val = 0.f;
+        if (row < n && f < FEAT) val = xin ? xin[(long)(rows ? rows[row] : row) * FEAT + f] : feature(fs[k], f);
+        const float one[1] = {val};
+        put_planes<1>(P, SA, rr, f, one);
     }
     lds_barrier();
     TSTAMP(1);
@@ -494,6 +500,7 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
     // One ring streams v_head.2 (one 16-column tile per wave, first) and then the policy head;
     // its first slices fly under the LayerNorms.  a_pi's planes go to P, a_v's to T's storage.
     constexpr int RD = PW < KS ? PW : KS;  // policy ring depth (slices)
+    static_assert(KS % RD == 0 && KS % RW == 0, "a ring's refills cross into the next chunk / layer slot-aligned");
     _Float16* PV = reinterpret_cast<_Float16*>(T);
     W2 pring[RD][PCH];
 #pragma unroll
