@@ -1159,7 +1159,7 @@ int run_sims(yk_engine* eng, int sims, const uint32_t* env_ids, uint64_t* ctr, h
             prof_mark(eng, KC_FORWARD, s);
             // predict row = game: no compaction; workgroups without a leaf exit at once
             int rc = launch_forward(eng->net->dev, d.leaf_state, nullptr, nullptr, nullptr, d.E, eng->logits, eng->vpred, s,
-                                    d.leaf_flag, eng->mlse);
+                                    d.leaf_flag, eng->mlse, d.rec_pred == 0);
             if (rc) return rc;
         }
         prof_mark(eng, KC_EXPAND, s);

@@ -253,6 +253,31 @@ __device__ __forceinline__ void ring_chunk(const _Float16* A, int sa, W2 (&ring)
 #pragma unroll
     for (int t = 0; t < NTL; t++) pa[t] = combine(c[t]);
 }
+// Which logits of a row are stored (valid_only launches: the engine reads a leaf's logits only
+// at its valid actions, MCTS.py:87-88, so the rest never leave the CU): per row a mode nibble -
+// 0 none (no valid move, or no leaf), 1 the bids (YachtGame.py:379-383), 2 the score actions of
+// unused categories at 10 dice (every combo), 3 the same at 5 dice (combo 0 only; :395-396),
+// 4 every column (any other carry, or a full launch) - and the used-category mask << 4.
+constexpr uint32_t LM_NONE = 0, LM_BID = 1, LM_SCORE10 = 2, LM_SCORE5 = 3, LM_ALL = 4;
+__device__ __forceinline__ uint32_t logit_mode(const YkS& s) {
+    const int round = s_round(s), phase = s_phase(s);
+    if (phase == 0 && round != 13) return LM_BID;
+    if (phase != 1) return LM_NONE;
+    const uint64_t wa = s_pw(s, 0, 0);
+    const int n = wa_n(wa);
+    if (n < 5) return LM_NONE;
+    const uint32_t used = (uint32_t)wa_used(wa) << 4;
+    return n >= 10 ? (LM_SCORE10 | used) : n == 5 ? (LM_SCORE5 | used) : LM_ALL;
+}
+__device__ __forceinline__ bool logit_stored(uint32_t vd, int col) {
+    const uint32_t m = vd & 0xF;
+    if (m == LM_ALL) return true;
+    if (col < NBID) return m == LM_BID;
+    if (m != LM_SCORE10 && m != LM_SCORE5) return false;
+    const int base = col - NBID, cat = base / NCOMB, ci = base - cat * NCOMB;
+    return !((vd >> (4 + cat)) & 1u) && (m == LM_SCORE10 || ci == 0);
+}
+
 // Running softmax statistics of one lane's rows (4 q + j): max and sum exp(x - max) over the
 // columns it has seen (online form); combined over lanes and waves at the end of the head.
 struct SoftStat {
@@ -267,7 +292,7 @@ __device__ __forceinline__ void stat_merge(float& m, float& s, float m2, float s
 template <int KS, int NTL, int NXT, int RD = (PW < KS ? PW : KS)>
 __device__ __forceinline__ void pi_chunk(const _Float16* A, int sa, W2 (&ring)[RD][PCH], const float* __restrict__ W,
                                          int tb, int tb_next, const float* bias, float* __restrict__ logits, int row0,
-                                         int n, SoftStat& st) {
+                                         int n, SoftStat& st, const uint32_t (&vd)[4]) {
     const int lane = threadIdx.x & 63;
     floatx4 pa[NTL];
     ring_chunk<KS, NTL, NXT, RD>(A, sa, ring, pa, W, tb, W, tb_next);
@@ -284,7 +309,7 @@ __device__ __forceinline__ void pi_chunk(const _Float16* A, int sa, W2 (&ring)[R
             for (int j = 0; j < 4; j++) {
                 const int row = row0 + 4 * q + j;
                 pa[t][j] += b;
-                if (row < n) logits[(long)row * PI_LD + col] = pa[t][j];
+                if (row < n && logit_stored(vd[j], col)) logits[(long)row * PI_LD + col] = pa[t][j];
             }
         }
     }
@@ -308,7 +333,8 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
                                                  const float* __restrict__ xin, const int32_t* __restrict__ rows,
                                                  const int32_t* __restrict__ count, int n,
                                                  float* __restrict__ logits, float* __restrict__ vout,
-                                                 const uint8_t* __restrict__ active, float2* __restrict__ mlse) {
+                                                 const uint8_t* __restrict__ active, float2* __restrict__ mlse,
+                                                 int valid_only) {
     constexpr int LD = (H > 128 ? H : 128) + 4;      // X also holds the 128-wide v_head hidden
     constexpr int SA = H + 8;                        // plane row stride (halves): conflict-free b128 reads
     constexpr int NT = H >= 16 * WAVES ? H / (16 * WAVES) : 1;  // 16-col tiles per wave, H-wide layers
@@ -328,20 +354,24 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
     __shared__ __attribute__((aligned(16))) _Float16 P[2 * ROWS * SA];  // the next GEMM's input planes
     __shared__ __attribute__((aligned(16))) float VS[NVS];  // static vectors (yk_net.h VS_*)
     __shared__ __attribute__((aligned(16))) float VB[NVB];  // this block's b1 g1 be1 b2 g2 be2
+    __shared__ uint32_t VD[ROWS];                            // per row: which logits are stored
 
     if (count) n = min(n, *count);
     const int row0 = blockIdx.x * ROWS;
     if (row0 >= n) return;
+    uint32_t amask = 0xFFFFu;  // rows with a leaf (bit r: row row0 + r)
     if (active) {  // uniform: every wave reads the same 16 flags (one scalar load when whole)
-        bool any = false;
+        amask = 0;
         if (row0 + ROWS <= n && (reinterpret_cast<uintptr_t>(active) & 15) == 0) {
             const uint4 a4 = *reinterpret_cast<const uint4*>(active + row0);
-            any = (a4.x | a4.y | a4.z | a4.w) != 0;
+            const uint32_t w4[4] = {a4.x, a4.y, a4.z, a4.w};
+#pragma unroll
+            for (int i = 0; i < ROWS; i++) amask |= (((w4[i >> 2] >> (8 * (i & 3))) & 0xFFu) != 0 ? 1u : 0u) << i;
         } else {
 #pragma unroll
-            for (int i = 0; i < ROWS; i++) any |= row0 + i < n && active[row0 + i];
+            for (int i = 0; i < ROWS; i++) amask |= (row0 + i < n && active[row0 + i] ? 1u : 0u) << i;
         }
-        if (!any) return;
+        if (!amask) return;
     }
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const bool gw = wave < NACT;  // owns columns of the H-wide layers
@@ -400,6 +430,9 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
         if (row < n && f < FEAT) val = xin ? xin[(long)(rows ? rows[row] : row) * FEAT + f] : feature(fs[k], f);
         const float one[1] = {val};
         put_planes<1>(P, SA, rr, f, one);
+        if (lane == 0)
+            VD[rr] = row >= n || !((amask >> rr) & 1u) ? LM_NONE
+                     : (valid_only && !xin) ? logit_mode(fs[k]) : LM_ALL;
     }
     lds_barrier();
     TSTAMP(1);
@@ -536,21 +569,23 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
     auto chunk_tb = [&](int c) { return wave + WAVES * PCH * ((c + rot) % FULL); };
     ring_chunk<KS, 1, PCH>(PV, SA, pring, av, net.w_v1, wave, net.w_pi, chunk_tb(0));
     SoftStat st;
+    uint32_t vd[4];
 #pragma unroll
     for (int j = 0; j < 4; j++) {
         st.m[j] = -INFINITY;
         st.s[j] = 0.f;
+        vd[j] = VD[4 * (lane >> 4) + j];
     }
 #pragma unroll 1
     for (int c = 0; c + 1 < FULL; c++) {
-        pi_chunk<KS, PCH, PCH>(P, SA, pring, net.w_pi, chunk_tb(c), chunk_tb(c + 1), bpi, logits, row0, n, st);
+        pi_chunk<KS, PCH, PCH>(P, SA, pring, net.w_pi, chunk_tb(c), chunk_tb(c + 1), bpi, logits, row0, n, st, vd);
         if (c & 1) TSTAMP(10 + (c >> 1));  // stamps 10, 11 after chunk pairs
     }
     {
         const int tl = wave + WAVES * PCH * FULL;  // the padded last chunk
-        pi_chunk<KS, PCH, LASTN>(P, SA, pring, net.w_pi, chunk_tb(FULL - 1), tl, bpi, logits, row0, n, st);
+        pi_chunk<KS, PCH, LASTN>(P, SA, pring, net.w_pi, chunk_tb(FULL - 1), tl, bpi, logits, row0, n, st, vd);
         TSTAMP(12);
-        pi_chunk<KS, LASTN, 0>(P, SA, pring, net.w_pi, tl, 0, bpi, logits, row0, n, st);
+        pi_chunk<KS, LASTN, 0>(P, SA, pring, net.w_pi, tl, 0, bpi, logits, row0, n, st, vd);
     }
     TSTAMP(14);
     WSTAMP(24);
@@ -647,14 +682,15 @@ namespace yk {
 
 int launch_forward(const NetDev& net, const yk_state_t* states, const float* x, const int32_t* rows,
                    const int32_t* count, int n, float* logits, float* v, hipStream_t stream, const uint8_t* active,
-                   float2* mlse) {
+                   float2* mlse, bool valid_only) {
     if (n <= 0) return YK_OK;
     const dim3 grid((n + ROWS - 1) / ROWS), block(NTHR);
+    const int vo = valid_only ? 1 : 0;
     switch (net.H) {
-        case 64: hipLaunchKernelGGL(k_forward<64>, grid, block, 0, stream, net, states, x, rows, count, n, logits, v, active, mlse); break;
-        case 128: hipLaunchKernelGGL(k_forward<128>, grid, block, 0, stream, net, states, x, rows, count, n, logits, v, active, mlse); break;
-        case 256: hipLaunchKernelGGL(k_forward<256>, grid, block, 0, stream, net, states, x, rows, count, n, logits, v, active, mlse); break;
-        case 512: hipLaunchKernelGGL(k_forward<512>, grid, block, 0, stream, net, states, x, rows, count, n, logits, v, active, mlse); break;
+        case 64: hipLaunchKernelGGL(k_forward<64>, grid, block, 0, stream, net, states, x, rows, count, n, logits, v, active, mlse, vo); break;
+        case 128: hipLaunchKernelGGL(k_forward<128>, grid, block, 0, stream, net, states, x, rows, count, n, logits, v, active, mlse, vo); break;
+        case 256: hipLaunchKernelGGL(k_forward<256>, grid, block, 0, stream, net, states, x, rows, count, n, logits, v, active, mlse, vo); break;
+        case 512: hipLaunchKernelGGL(k_forward<512>, grid, block, 0, stream, net, states, x, rows, count, n, logits, v, active, mlse, vo); break;
         default: return YK_ERR_ARG;
     }
     YK_LAUNCHED();

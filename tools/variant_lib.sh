@@ -1,0 +1,19 @@
+#!/bin/bash
+# diagnostic: builds a variant of libyacht_hip.so with extra defines into /tmp/yk_NAME/
+# (GPU box or here).  usage: tools/variant_lib.sh NAME "-DFOO=1 ..."; then
+# YK_LIB_PATH=/tmp/yk_NAME/libyacht_hip.so python bench.py ...
+# A NAME starting with "base" builds the sources staged under ab_base/csrc (an A/B baseline).
+cd "$(dirname "$0")/.." || exit 2
+set -e
+name=$1; shift
+src=nypc-yacht-auction_amd/csrc
+case $name in base*) src=ab_base/csrc ;; esac
+out=/tmp/yk_$name
+mkdir -p $out
+for f in yk_env yk_net yk_engine yk_train; do
+  /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -fPIC -std=c++17 -ffp-contract=off -w "$@" \
+     -Iinclude -I$src -c $src/$f.hip -o $out/$f.o &
+done
+wait
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $out/libyacht_hip.so $out/yk_*.o -L/opt/rocm/lib -lrocblas -Wl,-rpath,/opt/rocm/lib
+echo "built $out/libyacht_hip.so"
