@@ -24,6 +24,8 @@ struct NetDev {
     const float *g_v, *be_v, *w_v1, *b_v1, *w_v2, *b_v2;  // w_v1 packed [8][H/32][2][64][8], w_v2 [128], b_v2 [1]
     const float* vstat;  // copies staged to LDS once: [VS_* x H] + b_v1[128] w_v2[128] + b_pi[3264]
     const float* vblk;   // per block b: b1 g1 be1 b2 g2 be2 ([6][H]), staged to LDS per block
+    float pi_bspread;    // max - min of pi_head.2's bias over the 3226 actions
+    float pi_wmax;       // max over actions of |pi_head.2 weight row|_2
 };
 // vstat offsets in units of H (b_v1 at VS_BV1*H, w_v2 right after it, b_pi at vs_bpi(H))
 enum { VS_BIN = 0, VS_GIN = 1, VS_BEIN = 2, VS_GPI = 3, VS_BEPI = 4, VS_GV = 5, VS_BEV = 6, VS_BV1 = 7 };

@@ -20,6 +20,8 @@
 // next layer streams in under the current GEMM and the LayerNorm phase.  Nothing the kernel
 // waits on is ever issued behind that stream (vmcnt retires in order): biases and LayerNorm
 // vectors live in LDS, and the kernel must not spill (scratch also counts in vmcnt).
+#include <algorithm>
+#include <cmath>
 #include <vector>
 
 #include "yk_api.h"
@@ -45,6 +47,18 @@ __device__ unsigned long long g_tstamp[4096 * 32];
 #define TSTAMP(i)
 #define WSTAMP(i)
 #endif
+// Diagnostic builds only (-DYK_TILESTAT, tools/diag_tiles.py): policy-head tiles a workgroup
+// would need if it computed only the union of its rows' valid columns.
+#ifdef YK_TILESTAT
+// [0] workgroups, [1] sum of needed tiles, [2] rows, [3] bid-only workgroups, [4] sum over launches
+// of the launch's max, [5] this launch's max, [6] launches, [8 + k] histogram of tiles / 32
+__device__ unsigned long long g_tiles[16];
+__global__ void k_tilestat_flush() {
+    g_tiles[4] += g_tiles[5];
+    g_tiles[5] = 0;
+    g_tiles[6] += 1;
+}
+#endif
 
 constexpr int ROWS = 16;     // rows per workgroup (the MFMA M)
 constexpr int WAVES = 8;     // waves per workgroup
@@ -56,6 +70,8 @@ constexpr int PCH = 4;       // policy-head tiles per chunk
 #endif
 constexpr int PW = YK_PW;    // policy-head ring depth (32-deep slices)
 constexpr float SPLIT = 2048.f, UNSPLIT = 1.f / 2048.f;  // lo plane scale (keeps it out of fp16 subnormals)
+constexpr int REAL_TILES = (ASIZE + 15) / 16;  // policy tiles holding an action column (202 of 204)
+constexpr float FULL_SPREAD = 80.f;  // logit spread bound above which a workgroup takes the full pass
 
 // SiLU with the hardware exp / reciprocal (<= 2 ulp each; well inside the 1e-5 contract)
 __device__ __forceinline__ float silu(float x) { return x * __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
@@ -209,19 +225,15 @@ __device__ __forceinline__ void layernorm(float (&x)[VPL], const float* g, const
     for (int i = 0; i < VPL; i++) x[i] = (x[i] - mean) * rstd * g[c0 + i] + b[c0 + i];
 }
 
-// Policy head chunks: wave w owns tiles w + WAVES j; a chunk holds NTL <= PCH of them
-// (tiles tb, tb + WAVES, ...).  The ring (RD slices of PCH tiles) streams across chunk
-// boundaries: past the last slice it refills with the next chunk's first slices (NXT tiles,
-// from tb_next).  Tiles >= PI_TILES (the padded last chunk) are computed on a duplicate of
-// tile tb and not stored.
-__device__ __forceinline__ int pi_tile(int tb, int t) {  // real tile to load for slot t
-    const int x = tb + WAVES * t;
-    return x < PI_TILES ? x : tb;
-}
+// Policy head chunks.  The workgroup computes the tiles of a list (every real tile, or the union
+// of its rows' valid columns, TL in LDS); wave w owns list entries w + WAVES k, PCH of them per
+// chunk, NTL <= PCH in a wave's last chunk.  The ring (RD slices of PCH tiles) streams across
+// chunk boundaries: past the last slice it refills with the next chunk's first slices (NXT tiles).
+// Chunk shapes are template parameters, so the loop body has no branches.
 template <int KS, int NTL, int NXT, int RD = (PW < KS ? PW : KS)>
 __device__ __forceinline__ void ring_chunk(const _Float16* A, int sa, W2 (&ring)[RD][PCH], floatx4 (&pa)[NTL],
-                                           const float* __restrict__ W, int tb, const float* __restrict__ Wn,
-                                           int tb_next) {
+                                           const float* __restrict__ W, const int (&tile)[PCH],
+                                           const float* __restrict__ Wn, const int (&ntile)[PCH]) {
     const int lane = threadIdx.x & 63;
     const APtr ap = a_ptr(A, sa);
     Acc3 c[NTL];
@@ -241,10 +253,10 @@ __device__ __forceinline__ void ring_chunk(const _Float16* A, int sa, W2 (&ring)
         const int g = ks + RD;
         if (g < KS) {
 #pragma unroll
-            for (int t = 0; t < NTL; t++) w[t] = ld_w2(W, KS, pi_tile(tb, t), g, lane);
+            for (int t = 0; t < NTL; t++) w[t] = ld_w2(W, KS, tile[t], g, lane);
         } else {
 #pragma unroll
-            for (int t = 0; t < NXT; t++) w[t] = ld_w2(Wn, KS, pi_tile(tb_next, t), g - KS, lane);
+            for (int t = 0; t < NXT; t++) w[t] = ld_w2(Wn, KS, ntile[t], g - KS, lane);
         }
         __builtin_amdgcn_sched_barrier(0);
         ah = ahn;
@@ -271,11 +283,43 @@ __device__ __forceinline__ uint32_t logit_mode(const YkS& s) {
 }
 __device__ __forceinline__ bool logit_stored(uint32_t vd, int col) {
     const uint32_t m = vd & 0xF;
-    if (m == LM_ALL) return true;
+    if (m == LM_ALL) return col < ASIZE;
     if (col < NBID) return m == LM_BID;
     if (m != LM_SCORE10 && m != LM_SCORE5) return false;
     const int base = col - NBID, cat = base / NCOMB, ci = base - cat * NCOMB;
     return !((vd >> (4 + cat)) & 1u) && (m == LM_SCORE10 || ci == 0);
+}
+// Tile masks (204 bits = 7 words) of the columns a row keeps: the bids, every real column, each
+// category's 252 combos, each category's combo 0.
+constexpr int TMW = (PI_TILES + 31) / 32;
+struct TileMasks {
+    uint32_t bid[TMW], all[TMW], cat[NCAT][TMW], first[NCAT][TMW];
+};
+constexpr void tm_set(uint32_t (&m)[TMW], int c0, int c1) {  // columns c0 .. c1
+    for (int t = c0 / 16; t <= c1 / 16; t++) m[t / 32] |= 1u << (t % 32);
+}
+constexpr TileMasks make_tile_masks() {
+    TileMasks m{};
+    tm_set(m.bid, 0, NBID - 1);
+    tm_set(m.all, 0, ASIZE - 1);
+    for (int c = 0; c < NCAT; c++) {
+        tm_set(m.cat[c], NBID + NCOMB * c, NBID + NCOMB * c + NCOMB - 1);
+        tm_set(m.first[c], NBID + NCOMB * c, NBID + NCOMB * c);
+    }
+    return m;
+}
+static __constant__ TileMasks c_tm = make_tile_masks();
+// word w of the tile mask of a row with descriptor vd
+__device__ __forceinline__ uint32_t tile_word(uint32_t vd, int w) {
+    const uint32_t m = vd & 0xF;
+    if (m == LM_NONE) return 0u;
+    if (m == LM_ALL) return c_tm.all[w];
+    if (m == LM_BID) return c_tm.bid[w];
+    uint32_t x = 0;
+#pragma unroll
+    for (int c = 0; c < NCAT; c++)
+        if (!((vd >> (4 + c)) & 1u)) x |= m == LM_SCORE10 ? c_tm.cat[c][w] : c_tm.first[c][w];
+    return x;
 }
 
 // Running softmax statistics of one lane's rows (4 q + j): max and sum exp(x - max) over the
@@ -289,41 +333,50 @@ __device__ __forceinline__ void stat_merge(float& m, float& s, float m2, float s
     s = s * __expf(m - mm) + s2 * __expf(m2 - mm);
     m = mm;
 }
+// one chunk of policy tiles: logits (+ bias) stored where the row keeps them, and the columns the
+// row's softmax runs over (`allc`: every action; else the row's stored ones) folded into the
+// running (max, sum exp): one rescale per row and chunk
 template <int KS, int NTL, int NXT, int RD = (PW < KS ? PW : KS)>
 __device__ __forceinline__ void pi_chunk(const _Float16* A, int sa, W2 (&ring)[RD][PCH], const float* __restrict__ W,
-                                         int tb, int tb_next, const float* bias, float* __restrict__ logits, int row0,
-                                         int n, SoftStat& st, const uint32_t (&vd)[4]) {
+                                         const int (&tile)[PCH], const int (&ntile)[PCH], const float* bias,
+                                         float* __restrict__ logits, int row0, int n, SoftStat& st,
+                                         const uint32_t (&vd)[4], const bool (&allc)[4]) {
     const int lane = threadIdx.x & 63;
     floatx4 pa[NTL];
-    ring_chunk<KS, NTL, NXT, RD>(A, sa, ring, pa, W, tb, W, tb_next);
+    ring_chunk<KS, NTL, NXT, RD>(A, sa, ring, pa, W, tile, W, ntile);
     const int rr = lane & 15, q = lane >> 4;
-    bool ok[NTL];
 #pragma unroll
     for (int t = 0; t < NTL; t++) {
-        const int tile = tb + WAVES * t;
-        const int col = 16 * tile + rr;
-        ok[t] = tile < PI_TILES && col < ASIZE;  // a real action column
-        if (tile < PI_TILES) {
-            const float b = bias[col];
+        // the lane's column, classified once for its four rows (logit_stored, unrolled)
+        const int col = 16 * tile[t] + rr;
+        const float b = bias[col];
+        const bool real = col < ASIZE, bid = col < NBID;
+        const int base = bid ? 0 : col - NBID, cat = base / NCOMB;
+        const bool combo0 = base - cat * NCOMB == 0;
+        const uint32_t cbit = 1u << (4 + cat);
 #pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const int row = row0 + 4 * q + j;
-                pa[t][j] += b;
-                if (row < n && logit_stored(vd[j], col)) logits[(long)row * PI_LD + col] = pa[t][j];
-            }
+        for (int j = 0; j < 4; j++) {
+            const int row = row0 + 4 * q + j;
+            const uint32_t md = vd[j] & 0xF;
+            const bool score = !bid && real && !(vd[j] & cbit) && (md == LM_SCORE10 || (md == LM_SCORE5 && combo0));
+            const bool keep = md == LM_ALL ? real : md == LM_BID ? bid : score;
+            pa[t][j] += b;
+            if (row < n && keep) logits[(long)row * PI_LD + col] = pa[t][j];
+            if (!(allc[j] ? real : keep)) pa[t][j] = -INFINITY;  // outside the row's softmax
         }
     }
-    // this chunk's columns into the running (max, sum exp): one rescale per row and chunk
 #pragma unroll
     for (int j = 0; j < 4; j++) {
         float mn = st.m[j];
 #pragma unroll
-        for (int t = 0; t < NTL; t++) mn = ok[t] ? fmaxf(mn, pa[t][j]) : mn;
-        float acc = st.s[j] > 0.f ? st.s[j] * __expf(st.m[j] - mn) : 0.f;
+        for (int t = 0; t < NTL; t++) mn = fmaxf(mn, pa[t][j]);
+        if (mn != -INFINITY) {
+            float acc = st.s[j] > 0.f ? st.s[j] * __expf(st.m[j] - mn) : 0.f;
 #pragma unroll
-        for (int t = 0; t < NTL; t++) acc += ok[t] ? __expf(pa[t][j] - mn) : 0.f;
-        st.m[j] = mn;
-        st.s[j] = acc;
+            for (int t = 0; t < NTL; t++) acc += __expf(pa[t][j] - mn);
+            st.m[j] = mn;
+            st.s[j] = acc;
+        }
     }
 }
 
@@ -355,6 +408,10 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
     __shared__ __attribute__((aligned(16))) float VS[NVS];  // static vectors (yk_net.h VS_*)
     __shared__ __attribute__((aligned(16))) float VB[NVB];  // this block's b1 g1 be1 b2 g2 be2
     __shared__ uint32_t VD[ROWS];                            // per row: which logits are stored
+    __shared__ float HN[ROWS];                               // per row: |a_pi|^2 (policy-head input)
+    __shared__ uint8_t TL[PI_TILES];                         // policy tiles a valid-only pass computes
+    __shared__ int TC;                                       // ... and their count
+    __shared__ uint32_t UM[TMW];                             // the union of the rows' tile masks
 
     if (count) n = min(n, *count);
     const int row0 = blockIdx.x * ROWS;
@@ -373,7 +430,7 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
         }
         if (!amask) return;
     }
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const bool gw = wave < NACT;  // owns columns of the H-wide layers
     const int nt0 = wave * NT;
     const int c0 = lane * VPL;
@@ -422,6 +479,7 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
             for (int t = 0; t < NT; t++) ring[ks][t] = ld_w2(w_first, KS, nt0 + t, ks, lane);
     }
     // featurize (state_to_vec, NNet.py:65-86) straight into the input layer's planes, K = 64
+    uint32_t vdk[FPT];
 #pragma unroll
     for (int k = 0; k < FPT; k++) {
         const int rr = wave + WAVES * k, f = lane;
@@ -430,11 +488,19 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
         if (row < n && f < FEAT) val = xin ? xin[(long)(rows ? rows[row] : row) * FEAT + f] : feature(fs[k], f);
         const float one[1] = {val};
         put_planes<1>(P, SA, rr, f, one);
-        if (lane == 0)
-            VD[rr] = row >= n || !((amask >> rr) & 1u) ? LM_NONE
-                     : (valid_only && !xin) ? logit_mode(fs[k]) : LM_ALL;
+        const uint32_t vdr = row >= n || !((amask >> rr) & 1u) ? LM_NONE
+                             : (valid_only && !xin) ? logit_mode(fs[k]) : LM_ALL;
+        if (lane == 0) VD[rr] = vdr;
+        vdk[k] = vdr;
     }
+    if (tid < TMW) UM[tid] = 0u;
     lds_barrier();
+    if (lane < TMW) {  // this wave's rows into the union (read after the input layer's barrier)
+        uint32_t w = 0;
+#pragma unroll
+        for (int k = 0; k < FPT; k++) w |= tile_word(vdk[k], lane);
+        if (w) atomicOr(&UM[lane], w);
+    }
     TSTAMP(1);
 
     floatx4 acc[NT];
@@ -459,6 +525,18 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
         store_acc<NT>(T, LD, nt0, acc, nullptr);
     }
     lds_barrier();  // T complete; every wave is done reading the feature planes
+    if (wave == 0) {  // the union as an ascending list (read after the trunk's barriers)
+        int base = 0;
+#pragma unroll
+        for (int b = 0; b < (PI_TILES + 63) / 64; b++) {
+            const int t = lane + 64 * b;
+            const bool need = t < PI_TILES && ((UM[t >> 5] >> (t & 31)) & 1u);
+            const uint64_t bal = __ballot(need);
+            if (need) TL[base + __popcll(bal & ((1ull << lane) - 1))] = (uint8_t)t;
+            base += __popcll(bal);
+        }
+        if (lane == 0) TC = base;
+    }
 #pragma unroll
     for (int rr = 0; rr < RPW; rr++) {
         const int r = wave * RPW + rr;
@@ -553,40 +631,131 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
         }
         put_planes<VPL>(P, SA, r, c0, x);
         put_planes<VPL>(PV, SA, r, c0, y);
+        float h2 = 0.f;
+#pragma unroll
+        for (int i = 0; i < VPL; i++) h2 += x[i] * x[i];
+        h2 = wave_sum(h2);
+        if (lane == 0) HN[r] = h2;
     }
     lds_barrier();
     TSTAMP(9);
+#ifdef YK_TILESTAT
+    if (tid == 0 && valid_only) {
+        uint32_t m[7] = {0, 0, 0, 0, 0, 0, 0};  // 204 tile bits
+        auto set = [&](int c0, int c1) {       // columns c0 .. c1 inclusive
+            for (int t = c0 / 16; t <= c1 / 16; t++) m[t >> 5] |= 1u << (t & 31);
+        };
+        int rows_on = 0;
+        bool bid_only = true;
+        for (int r = 0; r < ROWS; r++) {
+            const uint32_t v = VD[r], md = v & 0xF;
+            if (md == LM_NONE) continue;
+            rows_on++;
+            if (md != LM_BID) bid_only = false;
+            if (md == LM_BID) set(0, NBID - 1);
+            else if (md == LM_ALL) set(0, ASIZE - 1);
+            else
+                for (int c = 0; c < NCAT; c++)
+                    if (!((v >> (4 + c)) & 1u)) {
+                        const int a0 = NBID + NCOMB * c;
+                        set(a0, md == LM_SCORE10 ? a0 + NCOMB - 1 : a0);
+                    }
+        }
+        int cnt = 0;
+        for (int i = 0; i < 7; i++) cnt += __popc(m[i]);
+        atomicAdd(&g_tiles[0], 1ull);
+        atomicMax(&g_tiles[5], (unsigned long long)cnt);
+        atomicAdd(&g_tiles[8 + cnt / 32], 1ull);
+        atomicAdd(&g_tiles[1], (unsigned long long)cnt);
+        atomicAdd(&g_tiles[2], (unsigned long long)rows_on);
+        if (bid_only) atomicAdd(&g_tiles[3], 1ull);
+    }
+#endif
+    // The policy head over all real tiles (full) or over the union of the rows' valid columns.
+    // A row's softmax runs over every action (`allc`: the reference's exp(log_softmax), NNet.py:193)
+    // or - engine rows - over its valid actions only: pi_a / sum_valid(pi) (MCTS.py:88-91) is the
+    // same number either way up to rounding, unless every valid pi underflows in the full softmax
+    // (the reference then falls back to uniform, :93-107), which needs a valid logit ~100 below an
+    // invalid one.  |logit_a - b_a| <= |W_a| |a_pi| bounds the spread of a row's logits by
+    // (bmax - bmin) + 2 wmax |a_pi|; a row over FULL_SPREAD keeps the full softmax.  The choice
+    // depends on the row alone, so a row's result does not depend on its workgroup.
+    auto row_allc = [&](int r) {
+        const uint32_t md = VD[r] & 0xF;
+        return md == LM_ALL || (md != LM_NONE && net.pi_bspread + 2.f * net.pi_wmax * sqrtf(HN[r]) > FULL_SPREAD);
+    };
+    bool full = false;
+#pragma unroll
+    for (int r = 0; r < ROWS; r++) full |= row_allc(r);
+    full = __builtin_amdgcn_readfirstlane(full ? 1 : 0) != 0;
+    const int cnt = full ? REAL_TILES : __builtin_amdgcn_readfirstlane(TC);
+    // this wave's list entries k = 0 .. m-1 (list index wave + WAVES k): nf full chunks, in an
+    // order rotated per workgroup (the workgroups of an XCD then do not all read the same weight
+    // lines at the same moment; each tile's k order, hence the numerics, is fixed), then a last
+    // chunk of l entries
+    const int m = cnt > wave ? (cnt - wave + WAVES - 1) / WAVES : 0;
+    const int nf = m / PCH, l = m % PCH, nch = nf + (l ? 1 : 0);
+    const int rot = nf ? (int)(blockIdx.x % (unsigned)nf) : 0;
+    auto chunk_tiles = [&](int c, int (&tl)[PCH]) {
+        const int k0 = c < nf ? PCH * ((c + rot) % nf) : PCH * nf;
+#pragma unroll
+        for (int t = 0; t < PCH; t++) {
+            const int i = wave + WAVES * (k0 + t);
+            tl[t] = c < nch && k0 + t < m ? (full ? i : __builtin_amdgcn_readfirstlane((int)TL[i])) : 0;
+        }
+    };
+    auto chunk_n = [&](int c) { return c < nf ? PCH : c < nch ? l : 0; };
     floatx4 av[1];  // v_head.2: Linear(H, 128), tile `wave`; its refills stream the first policy chunk
-    // policy head (pi_head.2): 204 tiles of 16 columns; wave w owns tiles w + 8 j: FULL chunks
-    // of PCH tiles, then one padded chunk of LASTN, all through one ring
-    constexpr int FULL = PI_TILES / (WAVES * PCH);
-    constexpr int LASTN = (PI_TILES - FULL * WAVES * PCH + WAVES - 1) / WAVES;
-    static_assert(LASTN >= 1 && LASTN <= PCH, "policy-head remainder shape");
     const float* bpi = VS + vs_bpi(H);
-    // the workgroups of an XCD walk the full chunks in rotated orders, so they do not all read
-    // the same weight lines at the same moment (each tile's k order, hence the numerics, is fixed)
-    const int rot = blockIdx.x % FULL;
-    auto chunk_tb = [&](int c) { return wave + WAVES * PCH * ((c + rot) % FULL); };
-    ring_chunk<KS, 1, PCH>(PV, SA, pring, av, net.w_v1, wave, net.w_pi, chunk_tb(0));
+    int tcur[PCH], tnxt[PCH];
+    chunk_tiles(0, tcur);
+    {
+        const int vt[PCH] = {wave, 0, 0, 0};
+        static_assert(PCH == 4, "chunk-shape dispatch below");
+        switch (chunk_n(0)) {
+            case 0: ring_chunk<KS, 1, 0>(PV, SA, pring, av, net.w_v1, vt, net.w_pi, tcur); break;
+            case 1: ring_chunk<KS, 1, 1>(PV, SA, pring, av, net.w_v1, vt, net.w_pi, tcur); break;
+            case 2: ring_chunk<KS, 1, 2>(PV, SA, pring, av, net.w_v1, vt, net.w_pi, tcur); break;
+            case 3: ring_chunk<KS, 1, 3>(PV, SA, pring, av, net.w_v1, vt, net.w_pi, tcur); break;
+            default: ring_chunk<KS, 1, 4>(PV, SA, pring, av, net.w_v1, vt, net.w_pi, tcur); break;
+        }
+    }
     SoftStat st;
     uint32_t vd[4];
+    bool allc[4];
 #pragma unroll
     for (int j = 0; j < 4; j++) {
         st.m[j] = -INFINITY;
         st.s[j] = 0.f;
         vd[j] = VD[4 * (lane >> 4) + j];
+        allc[j] = row_allc(4 * (lane >> 4) + j);
     }
+#define YK_PI_CHUNK(NTL, NXT) \
+    pi_chunk<KS, NTL, NXT>(P, SA, pring, net.w_pi, tcur, tnxt, bpi, logits, row0, n, st, vd, allc)
 #pragma unroll 1
-    for (int c = 0; c + 1 < FULL; c++) {
-        pi_chunk<KS, PCH, PCH>(P, SA, pring, net.w_pi, chunk_tb(c), chunk_tb(c + 1), bpi, logits, row0, n, st, vd);
-        if (c & 1) TSTAMP(10 + (c >> 1));  // stamps 10, 11 after chunk pairs
+    for (int c = 0; c < nch; c++) {
+        chunk_tiles(c + 1, tnxt);
+        const int nx = chunk_n(c + 1);
+        if (c < nf) {
+            switch (nx) {
+                case 0: YK_PI_CHUNK(4, 0); break;
+                case 1: YK_PI_CHUNK(4, 1); break;
+                case 2: YK_PI_CHUNK(4, 2); break;
+                case 3: YK_PI_CHUNK(4, 3); break;
+                default: YK_PI_CHUNK(4, 4); break;
+            }
+        } else {
+            switch (l) {
+                case 1: YK_PI_CHUNK(1, 0); break;
+                case 2: YK_PI_CHUNK(2, 0); break;
+                default: YK_PI_CHUNK(3, 0); break;
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < PCH; t++) tcur[t] = tnxt[t];
+        if (c == 1 || c == 3) TSTAMP(10 + (c >> 1));  // stamps 10, 11 after chunk pairs
+        if (c == 5) TSTAMP(12);
     }
-    {
-        const int tl = wave + WAVES * PCH * FULL;  // the padded last chunk
-        pi_chunk<KS, PCH, LASTN>(P, SA, pring, net.w_pi, chunk_tb(FULL - 1), tl, bpi, logits, row0, n, st, vd);
-        TSTAMP(12);
-        pi_chunk<KS, LASTN, 0>(P, SA, pring, net.w_pi, tl, 0, bpi, logits, row0, n, st, vd);
-    }
+#undef YK_PI_CHUNK
     TSTAMP(14);
     WSTAMP(24);
     store_acc<1>(X, LD, wave, av, VS + VS_BV1 * H);  // X (the trunk output) was read by the head LNs only
@@ -693,6 +862,9 @@ int launch_forward(const NetDev& net, const yk_state_t* states, const float* x, 
         case 512: hipLaunchKernelGGL(k_forward<512>, grid, block, 0, stream, net, states, x, rows, count, n, logits, v, active, mlse, vo); break;
         default: return YK_ERR_ARG;
     }
+#ifdef YK_TILESTAT
+    if (valid_only) hipLaunchKernelGGL(k_tilestat_flush, dim3(1), dim3(1), 0, stream);
+#endif
     YK_LAUNCHED();
     return YK_OK;
 }
@@ -742,6 +914,19 @@ int yk_net_create(yk_net_t** out, int H, int NB, const float* const* p, int npar
     const size_t o_gv = put(H), o_bev = put(H), o_wv1 = put((size_t)128 * H), o_bv1 = put(128), o_wv2 = put(128),
                  o_bv2 = put(1);
     const size_t o_vs = put(vstat_size(H)), o_vb = put((size_t)NB * 6 * H);
+    // pi_head.2 bounds for the valid-only softmax (k_forward): bias spread, largest weight-row norm
+    float pi_bmin = INFINITY, pi_bmax = -INFINITY, pi_wmax = 0.f;
+    {
+        const float* wpi = p[6 + 8 * NB];
+        const float* bpi = p[7 + 8 * NB];
+        for (int a = 0; a < ASIZE; a++) {
+            pi_bmin = std::min(pi_bmin, bpi[a]);
+            pi_bmax = std::max(pi_bmax, bpi[a]);
+            double n2 = 0.0;
+            for (int i = 0; i < H; i++) n2 += (double)wpi[(size_t)a * H + i] * wpi[(size_t)a * H + i];
+            pi_wmax = std::max(pi_wmax, (float)std::sqrt(n2));
+        }
+    }
     int k = 0;
     auto cp = [&](size_t off, size_t n) { std::copy(p[k], p[k] + n, h.begin() + off); k++; };
     pack(o_win, p[k++], H, FEAT, H, 64);
@@ -791,9 +976,23 @@ int yk_net_create(yk_net_t** out, int H, int NB, const float* const* p, int npar
     d.g_pi = B + o_gpi; d.be_pi = B + o_bepi; d.w_pi = B + o_wpi; d.b_pi = B + o_bpi;
     d.g_v = B + o_gv; d.be_v = B + o_bev; d.w_v1 = B + o_wv1; d.b_v1 = B + o_bv1; d.w_v2 = B + o_wv2; d.b_v2 = B + o_bv2;
     d.vstat = B + o_vs; d.vblk = B + o_vb;
+    // rounded up so the device-side bound stays an upper bound (and non-finite weights force the
+    // full softmax)
+    d.pi_bspread = std::isfinite(pi_bmax - pi_bmin) ? (pi_bmax - pi_bmin) * 1.001f + 1e-3f : INFINITY;
+    d.pi_wmax = std::isfinite(pi_wmax) ? pi_wmax * 1.001f + 1e-3f : INFINITY;
     *out = net;
     return YK_OK;
 }
+
+#ifdef YK_TILESTAT
+int yk_diag_tiles(uint64_t* out) {  // HOST out[16]; resets the counters
+    YK_HIP(hipDeviceSynchronize());
+    YK_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tiles), sizeof(uint64_t) * 16));
+    const uint64_t z[16] = {};
+    YK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_tiles), z, sizeof(z)));
+    return YK_OK;
+}
+#endif
 
 int yk_net_destroy(yk_net_t* net) {
     if (!net) return YK_OK;
