@@ -807,6 +807,22 @@ __global__ void k_softmax(const float* __restrict__ logits, const float2* __rest
     for (int a = lane; a < ASIZE; a += 64) pi[(long)row * ASIZE + a] = expf(x[a] - ml.x - ml.y);
 }
 
+// The engine's leaf prior before renormalisation (yk_selfplay's expand, MCTS.py:86-88): at the
+// row's valid actions (player 1 of the canonical state) exp(x - m - l) from the forward's row
+// statistics, 0 elsewhere.  One wavefront per row.
+__global__ void k_leaf_prior(const float* __restrict__ logits, const float2* __restrict__ mlse,
+                             const yk_state_t* __restrict__ states, float* __restrict__ pi, int n) {
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (row >= n) return;
+    YkS s;
+#pragma unroll
+    for (int k = 0; k < 8; k++) s.w[k] = states[row].w[k];
+    const float* x = logits + (long)row * PI_LD;
+    const float2 ml = mlse[row];
+    for (int a = lane; a < ASIZE; a += 64)
+        pi[(long)row * ASIZE + a] = action_valid(s, 1, a) ? expf(x[a] - ml.x - ml.y) : 0.f;
+}
+
 // The submission bot's move (agent.py:248-280): softmax over all 3226 logits in f32, then the
 // most probable *decodable* action (agent.py:150-187 == getValidMoves for the mover p1,
 // YachtGame.py:375-400), the lowest index among equal probabilities (its stable descending
@@ -1023,6 +1039,26 @@ int yk_net_predict(yk_net_t* net, const yk_state_t* states, float* pi, float* v,
 int yk_net_predict_features(yk_net_t* net, const float* x, float* pi, float* v, int n, void* stream) {
     if (!x) return YK_ERR_ARG;
     return predict_common(net, nullptr, x, pi, v, n, stream);
+}
+
+int yk_net_leaf_prior(yk_net_t* net, const yk_state_t* states, float* pi, float* v, int n, void* stream) {
+    if (!net || !states || !pi || !v || n < 0) return YK_ERR_ARG;
+    if (n == 0) return YK_OK;
+    hipStream_t s = as_stream(stream);
+    float* logits = nullptr;
+    YK_HIP(hipMallocAsync((void**)&logits, sizeof(float) * ((size_t)n * PI_LD + 2 * (size_t)n), s));
+    float2* mlse = reinterpret_cast<float2*>(logits + (size_t)n * PI_LD);
+    int rc = launch_forward(net->dev, states, nullptr, nullptr, nullptr, n, logits, v, s, nullptr, mlse, true);
+    if (rc == YK_OK) {
+        hipLaunchKernelGGL(k_leaf_prior, dim3((n + 3) / 4), dim3(256), 0, s, logits, mlse, states, pi, n);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) {
+            yk::set_hip_error(e);
+            rc = YK_ERR_HIP;
+        }
+    }
+    (void)hipFreeAsync(logits, s);
+    return rc;
 }
 
 int yk_net_policy_action(yk_net_t* net, const yk_state_t* states, int32_t* actions, float* probs, int n,

@@ -58,6 +58,7 @@ SIGNATURES = {
     "yk_net_create": [C.POINTER(P), I, I, C.POINTER(P), I],
     "yk_net_predict": [P, P, P, P, I, P],
     "yk_net_predict_features": [P, P, P, P, I, P],
+    "yk_net_leaf_prior": [P, P, P, P, I, P],
     "yk_net_policy_action": [P, P, P, P, I, P],
     "yk_net_destroy": [P],
     "yk_engine_create": [C.POINTER(P), C.POINTER(YkEngineConfig), P],

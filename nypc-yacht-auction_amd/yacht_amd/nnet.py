@@ -90,6 +90,15 @@ class YkNet:
         call("yk_net_predict", self.handle, ptr(states.contiguous()), ptr(pi), ptr(v), n, stream_ptr())
         return pi, v
 
+    def leaf_prior(self, states: torch.Tensor):
+        """The self-play engine's leaf prior before renormalisation (yk_net_leaf_prior): pi at the
+        valid actions of each canonical state (softmax over them), 0 elsewhere, and v."""
+        n = states.shape[0]
+        pi = torch.empty((n, ACTION_SIZE), dtype=torch.float32, device="cuda")
+        v = torch.empty(n, dtype=torch.float32, device="cuda")
+        call("yk_net_leaf_prior", self.handle, ptr(states.contiguous()), ptr(pi), ptr(v), n, stream_ptr())
+        return pi, v
+
     def predict_features(self, x: torch.Tensor):
         x = x.to("cuda", torch.float32).contiguous()
         n = x.shape[0]

@@ -67,3 +67,55 @@ def test_predict_large_batch_vs_oracle(mods, golden):
     np.testing.assert_allclose(pi.cpu().numpy()[pick], opi, rtol=RTOL_PI, atol=ATOL_PI)
     np.testing.assert_allclose(v.cpu().numpy()[pick], ov, rtol=0, atol=ATOL_V)
     assert torch.isfinite(pi).all() and torch.allclose(pi.sum(1), torch.ones(len(W), device="cuda"), atol=1e-4)
+
+
+def _masked_renorm(pi, ok):
+    p = np.where(ok, pi, 0.0).astype(np.float64)
+    s = p.sum(1, keepdims=True)
+    return np.divide(p, s, out=np.zeros_like(p), where=s > 0)
+
+
+def test_leaf_prior_is_the_renormalised_reference_policy(mods, golden):
+    """The engine's valid-only leaf prior (yk_net_leaf_prior, the softmax over the valid actions)
+    renormalised == the masked, renormalised exp(log_softmax) of MCTS.py:86-91: within 1e-5 of the
+    same renormalisation of the GPU's full predict pi (the same logits), and within 3e-5 of the
+    reference's own (pi within 1e-5 per element, test_predict_vs_reference, and the renormalising
+    sum within 1e-5 again)."""
+    K, N = mods
+    g = golden("predict_h256_b6.npz")
+    net = N.YkNet(spec.closed_form_weights(256, 6), 256, 6)
+    S = K.states_to_device(g["states"])
+    pi, v = net.leaf_prior(S)
+    full, _ = net.predict_states(S)
+    ok, cnt = O.valid(g["states"], 1)
+    ok = ok.astype(bool)
+    pi = pi.cpu().numpy()
+    assert not pi[~ok].any()
+    P = _masked_renorm(pi, ok)
+    np.testing.assert_allclose(P, _masked_renorm(full.cpu().numpy(), ok), rtol=RTOL_PI, atol=ATOL_PI)
+    np.testing.assert_allclose(P, _masked_renorm(g["pi"], ok), rtol=3 * RTOL_PI, atol=ATOL_PI)
+    np.testing.assert_allclose(v.cpu().numpy(), g["v"], rtol=0, atol=ATOL_V)
+    has = cnt > 0
+    np.testing.assert_allclose(pi[has].sum(1), 1.0, rtol=0, atol=1e-5)  # a softmax over the valid set
+
+
+def test_leaf_prior_keeps_the_full_softmax_when_underflow_is_possible(mods, golden):
+    """A bias spread past the bound: every row takes the full softmax, so the leaf prior is the
+    predict pi at the valid actions bit for bit (and the reference's uniform fallback stays
+    reachable exactly as in MCTS.py:93-107)."""
+    K, N = mods
+    sd = spec.closed_form_weights(256, 6)
+    b = np.asarray(sd["pi_head.2.bias"], dtype=np.float32).copy()
+    b[202:] += 120.0  # score actions far above the bids
+    sd = dict(sd)
+    sd["pi_head.2.bias"] = b
+    net = N.YkNet(sd, 256, 6)
+    W = golden("states.npz")["states"][:512]
+    S = K.states_to_device(W)
+    lp, _ = net.leaf_prior(S)
+    pp, _ = net.predict_states(S)
+    ok = O.valid(W, 1)[0].astype(bool)
+    lp, pp = lp.cpu().numpy(), pp.cpu().numpy()
+    assert np.array_equal(lp, np.where(ok, pp, 0.0).astype(np.float32))
+    bid = ok[:, :202].any(1)
+    assert bid.any() and (lp[bid].sum(1) < 1e-30).all()  # the bids underflow: uniform fallback
