@@ -119,9 +119,10 @@ int yk_net_predict(yk_net_t* net, const yk_state_t* states, float* pi, float* v,
 int yk_net_predict_features(yk_net_t* net, const float* x, float* pi, float* v, int n, void* stream);
 /* The prior the self-play engine expands a leaf with (MCTS.py:86-88 inside yk_selfplay), before
  * its renormalisation: pi[i*3226 + a] = exp(x_a - m - l) at the valid actions of canonical state
- * i (getValidMoves(s, 1)), 0 elsewhere, with (m, l) the softmax statistics over those valid actions
- * - or over all 3226 logits (then exactly NNetWrapper.predict's pi, masked) when a weight-norm
- * bound cannot rule out that every valid pi underflows in the full softmax. */
+ * i (getValidMoves(s, 1)), 0 elsewhere, with (m, l) the softmax statistics over the actions of the
+ * 16-action tiles holding those valid actions - or over all 3226 logits (NNetWrapper.predict's pi,
+ * masked) when a weight-norm bound cannot rule out that every valid pi underflows in the full
+ * softmax.  Renormalised over the valid actions it is MCTS.py:88-91's P either way. */
 int yk_net_leaf_prior(yk_net_t* net, const yk_state_t* states, float* pi, float* v, int n, void* stream);
 /* The submission bot's move (replaces AIPlayer.get_move's network part,
  * yacht/submission/agent.py:248-280): for canonical states (the mover is p1), the action of

@@ -281,14 +281,6 @@ __device__ __forceinline__ uint32_t logit_mode(const YkS& s) {
     const uint32_t used = (uint32_t)wa_used(wa) << 4;
     return n >= 10 ? (LM_SCORE10 | used) : n == 5 ? (LM_SCORE5 | used) : LM_ALL;
 }
-__device__ __forceinline__ bool logit_stored(uint32_t vd, int col) {
-    const uint32_t m = vd & 0xF;
-    if (m == LM_ALL) return col < ASIZE;
-    if (col < NBID) return m == LM_BID;
-    if (m != LM_SCORE10 && m != LM_SCORE5) return false;
-    const int base = col - NBID, cat = base / NCOMB, ci = base - cat * NCOMB;
-    return !((vd >> (4 + cat)) & 1u) && (m == LM_SCORE10 || ci == 0);
-}
 // Tile masks (204 bits = 7 words) of the columns a row keeps: the bids, every real column, each
 // category's 252 combos, each category's combo 0.
 constexpr int TMW = (PI_TILES + 31) / 32;
@@ -322,60 +314,53 @@ __device__ __forceinline__ uint32_t tile_word(uint32_t vd, int w) {
     return x;
 }
 
-// Running softmax statistics of one lane's rows (4 q + j): max and sum exp(x - max) over the
-// columns it has seen (online form); combined over lanes and waves at the end of the head.
-struct SoftStat {
-    float m[4], s[4];
-};
+// Running softmax statistics (online form: max and sum exp(x - max)), merged over lanes and waves
+// at the end of the head.
 __device__ __forceinline__ void stat_merge(float& m, float& s, float m2, float s2) {
     const float mm = fmaxf(m, m2);
     if (mm == -INFINITY) return;
     s = s * __expf(m - mm) + s2 * __expf(m2 - mm);
     m = mm;
 }
-// one chunk of policy tiles: logits (+ bias) stored where the row keeps them, and the columns the
-// row's softmax runs over (`allc`: every action; else the row's stored ones) folded into the
-// running (max, sum exp): one rescale per row and chunk
+// one chunk of policy tiles: a row's logits (+ bias) in the tiles it keeps a column in (`allc`:
+// every real column) - a set that depends on the row alone - stored and folded into its running
+// (max, sum exp): one rescale per row and chunk.  Lane (q, c) holds rows 4 q + j, column c.
 template <int KS, int NTL, int NXT, int RD = (PW < KS ? PW : KS)>
 __device__ __forceinline__ void pi_chunk(const _Float16* A, int sa, W2 (&ring)[RD][PCH], const float* __restrict__ W,
                                          const int (&tile)[PCH], const int (&ntile)[PCH], const float* bias,
-                                         float* __restrict__ logits, int row0, int n, SoftStat& st,
-                                         const uint32_t (&vd)[4], const bool (&allc)[4]) {
+                                         float* __restrict__ logits, int row0, int n, float (&sm)[4], float (&ss)[4],
+                                         const uint16_t* trb, const bool (&allc)[4]) {
     const int lane = threadIdx.x & 63;
     floatx4 pa[NTL];
     ring_chunk<KS, NTL, NXT, RD>(A, sa, ring, pa, W, tile, W, ntile);
     const int rr = lane & 15, q = lane >> 4;
 #pragma unroll
     for (int t = 0; t < NTL; t++) {
-        // the lane's column, classified once for its four rows (logit_stored, unrolled)
         const int col = 16 * tile[t] + rr;
         const float b = bias[col];
-        const bool real = col < ASIZE, bid = col < NBID;
-        const int base = bid ? 0 : col - NBID, cat = base / NCOMB;
-        const bool combo0 = base - cat * NCOMB == 0;
-        const uint32_t cbit = 1u << (4 + cat);
+        const uint32_t rows = (uint32_t)trb[tile[t]] >> (4 * q);  // this lane's four rows
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             const int row = row0 + 4 * q + j;
-            const uint32_t md = vd[j] & 0xF;
-            const bool score = !bid && real && !(vd[j] & cbit) && (md == LM_SCORE10 || (md == LM_SCORE5 && combo0));
-            const bool keep = md == LM_ALL ? real : md == LM_BID ? bid : score;
+            const bool mine = col < ASIZE && (allc[j] || ((rows >> j) & 1u));
             pa[t][j] += b;
-            if (row < n && keep) logits[(long)row * PI_LD + col] = pa[t][j];
-            if (!(allc[j] ? real : keep)) pa[t][j] = -INFINITY;  // outside the row's softmax
+#ifndef YK_NO_STORE  // diagnostic: the policy head without its logits stores
+            if (row < n && mine) logits[(long)row * PI_LD + col] = pa[t][j];
+#endif
+            if (!mine) pa[t][j] = -INFINITY;  // outside the row's softmax
         }
     }
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-        float mn = st.m[j];
+        float mn = sm[j];
 #pragma unroll
         for (int t = 0; t < NTL; t++) mn = fmaxf(mn, pa[t][j]);
         if (mn != -INFINITY) {
-            float acc = st.s[j] > 0.f ? st.s[j] * __expf(st.m[j] - mn) : 0.f;
+            float acc = ss[j] > 0.f ? ss[j] * __expf(sm[j] - mn) : 0.f;
 #pragma unroll
             for (int t = 0; t < NTL; t++) acc += __expf(pa[t][j] - mn);
-            st.m[j] = mn;
-            st.s[j] = acc;
+            sm[j] = mn;
+            ss[j] = acc;
         }
     }
 }
@@ -412,6 +397,8 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
     __shared__ uint8_t TL[PI_TILES];                         // policy tiles a valid-only pass computes
     __shared__ int TC;                                       // ... and their count
     __shared__ uint32_t UM[TMW];                             // the union of the rows' tile masks
+    __shared__ uint32_t RM[ROWS][TMW];                       // each row's tile mask
+    __shared__ uint16_t TRB[PI_TILES];                       // per tile: the rows that keep a column in it
 
     if (count) n = min(n, *count);
     const int row0 = blockIdx.x * ROWS;
@@ -495,10 +482,14 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
     }
     if (tid < TMW) UM[tid] = 0u;
     lds_barrier();
-    if (lane < TMW) {  // this wave's rows into the union (read after the input layer's barrier)
+    if (lane < TMW) {  // this wave's rows' tile masks, and into the union (read after the input barrier)
         uint32_t w = 0;
 #pragma unroll
-        for (int k = 0; k < FPT; k++) w |= tile_word(vdk[k], lane);
+        for (int k = 0; k < FPT; k++) {
+            const uint32_t x = tile_word(vdk[k], lane);
+            RM[wave + WAVES * k][lane] = x;
+            w |= x;
+        }
         if (w) atomicOr(&UM[lane], w);
     }
     TSTAMP(1);
@@ -525,11 +516,17 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
         store_acc<NT>(T, LD, nt0, acc, nullptr);
     }
     lds_barrier();  // T complete; every wave is done reading the feature planes
-    if (wave == 0) {  // the union as an ascending list (read after the trunk's barriers)
+    if (wave == 0) {  // the union as an ascending list, and each tile's rows (read after the trunk)
         int base = 0;
 #pragma unroll
         for (int b = 0; b < (PI_TILES + 63) / 64; b++) {
             const int t = lane + 64 * b;
+            if (t < PI_TILES) {
+                uint32_t rb = 0;
+#pragma unroll
+                for (int r = 0; r < ROWS; r++) rb |= ((RM[r][t >> 5] >> (t & 31)) & 1u) << r;
+                TRB[t] = (uint16_t)rb;
+            }
             const bool need = t < PI_TILES && ((UM[t >> 5] >> (t & 31)) & 1u);
             const uint64_t bal = __ballot(need);
             if (need) TL[base + __popcll(bal & ((1ull << lane) - 1))] = (uint8_t)t;
@@ -673,8 +670,8 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
 #endif
     // The policy head over all real tiles (full) or over the union of the rows' valid columns.
     // A row's softmax runs over every action (`allc`: the reference's exp(log_softmax), NNet.py:193)
-    // or - engine rows - over its valid actions only: pi_a / sum_valid(pi) (MCTS.py:88-91) is the
-    // same number either way up to rounding, unless every valid pi underflows in the full softmax
+    // or - engine rows - over the tiles holding its valid actions: pi_a / sum_valid(pi) (MCTS.py:88-91)
+    // is the same number either way up to rounding, unless every valid pi underflows in the full softmax
     // (the reference then falls back to uniform, :93-107), which needs a valid logit ~100 below an
     // invalid one.  |logit_a - b_a| <= |W_a| |a_pi| bounds the spread of a row's logits by
     // (bmax - bmin) + 2 wmax |a_pi|; a row over FULL_SPREAD keeps the full softmax.  The choice
@@ -719,18 +716,16 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
             default: ring_chunk<KS, 1, 4>(PV, SA, pring, av, net.w_v1, vt, net.w_pi, tcur); break;
         }
     }
-    SoftStat st;
-    uint32_t vd[4];
+    float sm[4], ss[4];  // running max and sum exp of the lane's rows 4 q + j
     bool allc[4];
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-        st.m[j] = -INFINITY;
-        st.s[j] = 0.f;
-        vd[j] = VD[4 * (lane >> 4) + j];
+        sm[j] = -INFINITY;
+        ss[j] = 0.f;
         allc[j] = row_allc(4 * (lane >> 4) + j);
     }
 #define YK_PI_CHUNK(NTL, NXT) \
-    pi_chunk<KS, NTL, NXT>(P, SA, pring, net.w_pi, tcur, tnxt, bpi, logits, row0, n, st, vd, allc)
+    pi_chunk<KS, NTL, NXT>(P, SA, pring, net.w_pi, tcur, tnxt, bpi, logits, row0, n, sm, ss, TRB, allc)
 #pragma unroll 1
     for (int c = 0; c < nch; c++) {
         chunk_tiles(c + 1, tnxt);
@@ -761,18 +756,17 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
     store_acc<1>(X, LD, wave, av, VS + VS_BV1 * H);  // X (the trunk output) was read by the head LNs only
     // softmax statistics of the policy logits per row: over the 16 column lanes, then the waves
     float2* SS = reinterpret_cast<float2*>(T);  // T (a_v's planes) is no longer read
-    if (mlse) {
+    if (mlse) {  // over the 16 column lanes
 #pragma unroll
         for (int j = 0; j < 4; j++) {
 #pragma unroll
-            for (int o = 1; o < 16; o <<= 1)
-                stat_merge(st.m[j], st.s[j], __shfl_xor(st.m[j], o, 64), __shfl_xor(st.s[j], o, 64));
+            for (int o = 1; o < 16; o <<= 1) stat_merge(sm[j], ss[j], __shfl_xor(sm[j], o, 64), __shfl_xor(ss[j], o, 64));
         }
     }
     lds_barrier();  // every wave is done with v_head.2 (reads of T) and stored its av columns
     if (mlse && (lane & 15) == 0) {
 #pragma unroll
-        for (int j = 0; j < 4; j++) SS[wave * ROWS + 4 * (lane >> 4) + j] = make_float2(st.m[j], st.s[j]);
+        for (int j = 0; j < 4; j++) SS[wave * ROWS + 4 * (lane >> 4) + j] = make_float2(sm[j], ss[j]);
     }
     TSTAMP(23);
 #pragma unroll
@@ -809,7 +803,7 @@ __global__ void k_softmax(const float* __restrict__ logits, const float2* __rest
 
 // The engine's leaf prior before renormalisation (yk_selfplay's expand, MCTS.py:86-88): at the
 // row's valid actions (player 1 of the canonical state) exp(x - m - l) from the forward's row
-// statistics, 0 elsewhere.  One wavefront per row.
+// statistics, with the expand's hardware exp, 0 elsewhere.  One wavefront per row.
 __global__ void k_leaf_prior(const float* __restrict__ logits, const float2* __restrict__ mlse,
                              const yk_state_t* __restrict__ states, float* __restrict__ pi, int n) {
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -820,7 +814,7 @@ __global__ void k_leaf_prior(const float* __restrict__ logits, const float2* __r
     const float* x = logits + (long)row * PI_LD;
     const float2 ml = mlse[row];
     for (int a = lane; a < ASIZE; a += 64)
-        pi[(long)row * ASIZE + a] = action_valid(s, 1, a) ? expf(x[a] - ml.x - ml.y) : 0.f;
+        pi[(long)row * ASIZE + a] = action_valid(s, 1, a) ? __expf(x[a] - ml.x - ml.y) : 0.f;  // the expand's exp
 }
 
 // The submission bot's move (agent.py:248-280): softmax over all 3226 logits in f32, then the
