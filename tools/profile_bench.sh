@@ -1,6 +1,6 @@
 #!/bin/bash
 # rocprofv3 evidence for bench.py (GPU box): kernel-trace stats of the bench command, then the
-# HBM counters of k_forward in separate --pmc passes (FETCH_SIZE and WRITE_SIZE cannot share a
+# HBM counters of k_forward and k_expand_backup in separate --pmc passes (FETCH_SIZE and WRITE_SIZE cannot share a
 # pass on gfx950).  usage: tools/profile_bench.sh TAG   -> gpurun_out/prof_TAG/
 cd "$(dirname "$0")/.." || exit 2
 set -e
@@ -11,7 +11,7 @@ mkdir -p $out
 args="--steps 1 --warmup 1 --no-cpu-baseline --no-arena"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/trace -o bench --output-format csv -- python3 bench.py $args > $out/bench_trace.json
 for c in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 400 rocprofv3 --kernel-include-regex k_forward --pmc $c -d $out/$c -o $c --output-format csv -- python3 bench.py $args --no-profile > $out/bench_$c.json
+  timeout -k 10 400 rocprofv3 --kernel-include-regex 'k_forward|k_expand_backup' --pmc $c -d $out/$c -o $c --output-format csv -- python3 bench.py $args --no-profile > $out/bench_$c.json
 done
 python3 tools/summarize_prof.py $out > $out/summary.json
 cat $out/summary.json

@@ -1,5 +1,5 @@
 """Summarise a tools/profile_bench.sh directory: per-kernel average duration (kernel trace) and
-the k_forward HBM bytes per launch from the PMC passes (FETCH_SIZE doubled on gfx950 and
+the k_forward / k_expand_backup HBM bytes per launch from the PMC passes (FETCH_SIZE doubled on gfx950 and
 WRITE_SIZE as read; both counters in KiB, MI355X_MICROARCH.md 'HBM')."""
 import csv
 import glob
