@@ -16,7 +16,7 @@ def declared_functions():
 def test_header_declares_the_boundary():
     names = declared_functions()
     for required in ("yk_step", "yk_valid_mask", "yk_ended", "yk_canonical", "yk_score_table", "yk_featurize",
-                     "yk_net_predict", "yk_selfplay", "yk_mcts_search", "yk_engine_pack_records", "yk_arena", "yk_greedy_action",
+                     "yk_net_predict", "yk_net_leaf_prior", "yk_selfplay", "yk_mcts_search", "yk_engine_pack_records", "yk_arena", "yk_greedy_action",
                      "yk_arena_results"):
         assert required in names
 
@@ -46,4 +46,6 @@ def test_null_arguments_are_rejected_without_a_gpu():
     assert lib.yk_arena(None, 0, 0, None, 0, 1, None) == -1
     assert lib.yk_greedy_action(None, None, 1, None) == -1
     assert lib.yk_arena_results(None, None, None, None, None, None, None) == -1
+    for f in ("yk_net_predict", "yk_net_predict_features", "yk_net_leaf_prior"):
+        assert getattr(lib, f)(None, None, None, None, 1, None) == -1
     assert lib.yk_step(None, None, None, 0, None, None, None, None, None, 0, None) == 0  # empty batch
