@@ -75,15 +75,16 @@ def _masked_renorm(pi, ok):
     return np.divide(p, s, out=np.zeros_like(p), where=s > 0)
 
 
-def test_leaf_prior_is_the_renormalised_reference_policy(mods, golden):
+@pytest.mark.parametrize("hidden,nblocks", [(256, 6), (64, 1)])
+def test_leaf_prior_is_the_renormalised_reference_policy(mods, golden, hidden, nblocks):
     """The engine's valid-only leaf prior (yk_net_leaf_prior, the softmax over the valid actions)
     renormalised == the masked, renormalised exp(log_softmax) of MCTS.py:86-91: within 1e-5 of the
     same renormalisation of the GPU's full predict pi (the same logits), and within 3e-5 of the
     reference's own (pi within 1e-5 per element, test_predict_vs_reference, and the renormalising
     sum within 1e-5 again)."""
     K, N = mods
-    g = golden("predict_h256_b6.npz")
-    net = N.YkNet(spec.closed_form_weights(256, 6), 256, 6)
+    g = golden(f"predict_h{hidden}_b{nblocks}.npz")
+    net = N.YkNet(spec.closed_form_weights(hidden, nblocks), hidden, nblocks)
     S = K.states_to_device(g["states"])
     pi, v = net.leaf_prior(S)
     full, _ = net.predict_states(S)
