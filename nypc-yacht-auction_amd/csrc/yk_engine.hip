@@ -75,6 +75,7 @@ struct EngDev {
     uint32_t* arena_top;   // [E]
     uint8_t* gen;          // [E]
     uint8_t* cur_round;    // [E]
+    uint32_t* root_nid;    // [E] the move's root node id + 1 once a descent found it (0: not yet)
     // game state
     yk_state_t* board;
     int32_t* cur;
@@ -356,6 +357,7 @@ __global__ __launch_bounds__(256) void k_move_begin(EngDev d, int move, int exte
     const int lane = threadIdx.x & 63;
     const int e = blockIdx.x * GAMES_PER_BLOCK + (threadIdx.x >> 6);
     if (e >= d.E) return;
+    if (lane == 0) d.root_nid[e] = 0;  // node ids move at a compaction; the root is looked up afresh
     if (!external_root) {
         if (d.done[e]) return;
         const YkS b = ld_state(d.board + e);
@@ -477,8 +479,12 @@ __device__ __forceinline__ void select_game(const EngDev& d, int e, int lane, co
             res = PyV{-es, T_F64};
             break;
         }
-        const uint64_t hsh = key_hash(s);
-        const int nid = lookup(d, g, e, s, hsh);
+        // the root (depth 0) is the same node for every simulation of a move: its id is kept after
+        // the first lookup, which saves the hash and the index probe
+        const uint32_t rc = depth == 0 ? d.root_nid[e] : 0u;
+        const uint64_t hsh = rc ? 0ull : key_hash(s);
+        const int nid = rc ? (int)rc - 1 : lookup(d, g, e, s, hsh);
+        if (depth == 0 && !rc && nid >= 0 && lane == 0) d.root_nid[e] = (uint32_t)nid + 1;
         SEL_ACC(0, t_lv);
         if (nid < 0) {  // leaf: predict (MCTS.py:84-115)
             leaf = 1;
@@ -1235,6 +1241,7 @@ int yk_engine_create(yk_engine_t** out, const yk_engine_config_t* cfg, yk_net_t*
     A(d.arena_top, E);
     A(d.gen, E);
     A(d.cur_round, E);
+    A(d.root_nid, E);
     A(d.board, E);
     A(d.cur, E);
     A(d.ctr, E);
