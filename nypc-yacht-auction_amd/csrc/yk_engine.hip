@@ -75,7 +75,8 @@ struct EngDev {
     uint32_t* arena_top;   // [E]
     uint8_t* gen;          // [E]
     uint8_t* cur_round;    // [E]
-    uint32_t* root_nid;    // [E] the move's root node id + 1 once a descent found it (0: not yet)
+    uint4* root_c;         // [E][2] the move's root once a descent found it: {id + 1 (0: not yet), p_off,
+                           //        nvalid, -}, {vinfo lo, hi, -, -}
     // game state
     yk_state_t* board;
     int32_t* cur;
@@ -357,7 +358,7 @@ __global__ __launch_bounds__(256) void k_move_begin(EngDev d, int move, int exte
     const int lane = threadIdx.x & 63;
     const int e = blockIdx.x * GAMES_PER_BLOCK + (threadIdx.x >> 6);
     if (e >= d.E) return;
-    if (lane == 0) d.root_nid[e] = 0;  // node ids move at a compaction; the root is looked up afresh
+    if (lane == 0) d.root_c[2 * e] = make_uint4(0, 0, 0, 0);  // ids move at a compaction: look the root up afresh
     if (!external_root) {
         if (d.done[e]) return;
         const YkS b = ld_state(d.board + e);
@@ -479,12 +480,17 @@ __device__ __forceinline__ void select_game(const EngDev& d, int e, int lane, co
             res = PyV{-es, T_F64};
             break;
         }
-        // the root (depth 0) is the same node for every simulation of a move: its id is kept after
-        // the first lookup, which saves the hash and the index probe
-        const uint32_t rc = depth == 0 ? d.root_nid[e] : 0u;
-        const uint64_t hsh = rc ? 0ull : key_hash(s);
-        const int nid = rc ? (int)rc - 1 : lookup(d, g, e, s, hsh);
-        if (depth == 0 && !rc && nid >= 0 && lane == 0) d.root_nid[e] = (uint32_t)nid + 1;
+        // the root (depth 0) is the same node for every simulation of a move: its id and the
+        // record's fixed fields are kept after the first lookup, which saves the hash, the index
+        // probe and the record's round trip before the prior / slot loads
+        uint4 rc0 = make_uint4(0, 0, 0, 0), rc1 = rc0;
+        if (depth == 0) {
+            rc0 = d.root_c[2 * e];
+            rc1 = d.root_c[2 * e + 1];
+        }
+        const bool cached = rc0.x != 0;
+        const uint64_t hsh = cached ? 0ull : key_hash(s);
+        const int nid = cached ? (int)rc0.x - 1 : lookup(d, g, e, s, hsh);
         SEL_ACC(0, t_lv);
         if (nid < 0) {  // leaf: predict (MCTS.py:84-115)
             leaf = 1;
@@ -495,7 +501,13 @@ __device__ __forceinline__ void select_game(const EngDev& d, int e, int lane, co
             break;
         }
         const NodeRec& nd = nodes[nid];
-        const int V = (int)nd.nvalid;
+        const uint32_t p_off = cached ? rc0.y : nd.p_off;
+        const int V = cached ? (int)rc0.z : (int)nd.nvalid;
+        const uint64_t vinfo = cached ? ((uint64_t)rc1.x | ((uint64_t)rc1.y << 32)) : nd.vinfo;
+        if (depth == 0 && !cached && lane == 0) {
+            d.root_c[2 * e] = make_uint4((uint32_t)nid + 1, p_off, (uint32_t)V, 0);
+            d.root_c[2 * e + 1] = make_uint4((uint32_t)vinfo, (uint32_t)(vinfo >> 32), 0, 0);
+        }
         if (V == 0) {  // no valid action: MCTS.py:141-147 returns 0 (python int)
             res = PyV{0.0, T_INT};
             break;
@@ -511,8 +523,8 @@ __device__ __forceinline__ void select_game(const EngDev& d, int e, int lane, co
             sqe = (float)sqrt((double)Ns + 1e-8);
         }
         SEL_T0(t_sc);
-        const float* P = Pbase + nd.p_off;
-        const uint16_t* S = Sbase + nd.p_off;
+        const float* P = Pbase + p_off;
+        const uint16_t* S = Sbase + p_off;
         float best = -INFINITY;
         int bj = 0x7FFFFFFF;
         // software-pipelined scan: iteration it+1's P / slot loads fly while iteration it's
@@ -571,9 +583,9 @@ __device__ __forceinline__ void select_game(const EngDev& d, int e, int lane, co
             res = PyV{0.0, T_INT};
             break;
         }
-        if (lane == 0) path[depth] = ((uint64_t)(nd.p_off + (uint32_t)j) << 32) | (uint32_t)nid;
+        if (lane == 0) path[depth] = ((uint64_t)(p_off + (uint32_t)j) << 32) | (uint32_t)nid;
         depth++;
-        const VInfo vi = unpack_vinfo(nd.vinfo, nd.nvalid);
+        const VInfo vi = unpack_vinfo(vinfo, (uint32_t)V);
         const int a = compact_to_action(vi, j);
         int np = 1;
         const int st = step_state<true>(s, 1, a, rs, np);  // MCTS.py:149 (all lanes: wave-parallel dice)
@@ -1241,7 +1253,7 @@ int yk_engine_create(yk_engine_t** out, const yk_engine_config_t* cfg, yk_net_t*
     A(d.arena_top, E);
     A(d.gen, E);
     A(d.cur_round, E);
-    A(d.root_nid, E);
+    A(d.root_c, 2 * E);
     A(d.board, E);
     A(d.cur, E);
     A(d.ctr, E);
