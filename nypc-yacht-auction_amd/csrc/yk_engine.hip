@@ -249,6 +249,25 @@ __device__ __forceinline__ VInfo unpack_vinfo(uint64_t x, uint32_t V) {
 }
 __device__ __forceinline__ int pad4(int v) { return (v + 3) & ~3; }
 
+// The transposition index's hash of a packed state: 32-bit multiply-rotate over the 16 words
+// (the index only needs spread; a key compare settles every probe).  key_hash (yk_common.h, the
+// spec's) is computed only where the hash prior needs it.
+__device__ __forceinline__ uint64_t index_hash(const YkS& s) {
+    uint32_t a = 0x9E3779B9u, b = 0x85EBCA6Bu;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        a = (a ^ (uint32_t)s.w[i]) * 0xCC9E2D51u;
+        a = (a << 15) | (a >> 17);
+        b = (b ^ (uint32_t)(s.w[i] >> 32)) * 0x1B873593u;
+        b = (b << 13) | (b >> 19);
+    }
+    a ^= b * 0x85EBCA6Bu;
+    a ^= a >> 16;
+    a *= 0xC2B2AE35u;
+    a ^= a >> 13;
+    return ((uint64_t)b << 32) | a;
+}
+
 // open-addressing lookup; returns node id or -1.  Uniform across the wave.
 __device__ __forceinline__ int lookup(const EngDev& d, int g, int e, const YkS& s, uint64_t h) {
     const uint32_t* hx = d.hidx[g] + (long)e * d.HCAP;
@@ -489,7 +508,7 @@ __device__ __forceinline__ void select_game(const EngDev& d, int e, int lane, co
             rc1 = d.root_c[2 * e + 1];
         }
         const bool cached = rc0.x != 0;
-        const uint64_t hsh = cached ? 0ull : key_hash(s);
+        const uint64_t hsh = cached ? 0ull : index_hash(s);
         const int nid = cached ? (int)rc0.x - 1 : lookup(d, g, e, s, hsh);
         SEL_ACC(0, t_lv);
         if (nid < 0) {  // leaf: predict (MCTS.py:84-115)
@@ -652,7 +671,8 @@ __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int l
     if (d.leaf_flag[e]) {
         SEL_T0(t_x0);
         const YkS s = ld_state(d.leaf_state + e);
-        const uint64_t hsh = d.leaf_hash[e];
+        const uint64_t ihsh = d.leaf_hash[e];                  // the index's hash
+        const uint64_t hsh = d.prior == 1 ? key_hash(s) : 0ull;  // the hash prior's (spec) hash
         const VInfo vi = valid_info(s, 1);
         const ValidQ valid = valid_q(s);
         const int V = vi.V;
@@ -839,14 +859,14 @@ __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int l
                 NodeRec r;
 #pragma unroll
                 for (int i = 0; i < 8; i++) r.key[i] = s.w[i];
-                r.hash = hsh;
+                r.hash = ihsh;
                 r.vinfo = pack_vinfo(vi);
                 r.p_off = off;
                 r.nvalid = (uint32_t)V;
                 r.Ns = 0;
                 r.pad = 0;
                 d.nodes[g][(long)e * d.NCAP + nid] = r;
-                if (!insert_index(d, g, e, hsh, nid)) atomicOr(d.err, ERR_HASH);
+                if (!insert_index(d, g, e, ihsh, nid)) atomicOr(d.err, ERR_HASH);
                 d.node_count[g * d.E + e] = nid + 1;
                 d.arena_top[e] = off + (uint32_t)VP;
                 uint64_t* gs = d.gstats + (long)e * 8;
@@ -915,7 +935,7 @@ __global__ __launch_bounds__(256) void k_move_end(EngDev d, int move) {
     const int g = d.gen[e];
     const YkS r = ld_state(d.root + e);
     const bool idle = d.idle[e] != 0;
-    const int nid = idle ? -1 : lookup(d, g, e, r, key_hash(r));
+    const int nid = idle ? -1 : lookup(d, g, e, r, index_hash(r));
     int nvis = 0;
     uint32_t root_ns = 0xFFFFFFFFu;
     if (idle) {
@@ -1070,7 +1090,7 @@ __global__ void k_root_counts(EngDev d, int32_t* counts) {
     wave_sync();
     const int g = d.gen[e];
     const YkS r = ld_state(d.root + e);
-    const int nid = lookup(d, g, e, r, key_hash(r));
+    const int nid = lookup(d, g, e, r, index_hash(r));
     if (nid < 0) return;
     const NodeRec& nd = d.nodes[g][(long)e * d.NCAP + nid];
     const VInfo vi = unpack_vinfo(nd.vinfo, nd.nvalid);
