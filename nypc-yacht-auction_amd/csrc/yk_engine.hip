@@ -696,11 +696,26 @@ __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int l
             const float2 ml = d.mlse[e];
             mx = ml.x;
             lse = ml.y;
+            // score actions at 10 dice (most leaves): a group a .. a + 3 (a = 0 mod 4) holds at
+            // most two categories, a's and a + 2's (category starts are 202 + 252 c = 2 mod 4)
+            static_assert(NBID % 4 == 2 && NCOMB % 4 == 0, "category starts are 2 mod 4");
+            const bool score10 = valid.mode == 0 && valid.n >= 10;
 #pragma unroll
             for (int j = 0; j < PW_GMAX; j++) {
                 const int a = st + 8 * j + 4 * h;
-                const bool v0 = j < G && valid(a), v1 = j < G && valid(a + 1), v2 = j < G && valid(a + 2),
-                           v3 = j < G && valid(a + 3);
+                bool v0, v1, v2, v3;
+                if (score10) {
+                    const int b0 = a - NBID, b2 = a + 2 - NBID;
+                    const bool lo = j < G && b0 >= 0 && !((valid.used >> ((unsigned)b0 / NCOMB)) & 1u);
+                    const bool hi = j < G && b2 >= 0 && !((valid.used >> ((unsigned)b2 / NCOMB)) & 1u);
+                    v0 = v1 = lo;
+                    v2 = v3 = hi;
+                } else {
+                    v0 = j < G && valid(a);
+                    v1 = j < G && valid(a + 1);
+                    v2 = j < G && valid(a + 2);
+                    v3 = j < G && valid(a + 3);
+                }
                 float4 x4 = make_float4(0.f, 0.f, 0.f, 0.f);
                 if (v0 || v1 || v2 || v3) x4 = *reinterpret_cast<const float4*>(x + 8 * j + 4 * h);
                 q[j] = make_float4(v0 ? softmax_p(x4.x, mx, lse) : 0.f, v1 ? softmax_p(x4.y, mx, lse) : 0.f,
