@@ -144,9 +144,11 @@ typedef struct {
     int temp_threshold;     /* tempThreshold */
     int max_moves;          /* record capacity per game (every real game has 48 moves) */
     int prior;              /* 0 = yk_net (MLP), 1 = hash prior (test) */
-    int record_predictions; /* test: keep every expansion's (pi, v) per game */
+    int record_predictions; /* test: keep every expansion's (Ps * valids, v, leaf) of sampled games */
     int max_expansions;     /* capacity of that record per game (record_predictions only) */
     int64_t arena_entries;  /* per game per generation P/edge-slot entries; 0 = default */
+    int record_stride;      /* record_predictions samples games e with e % record_stride == 0 (0 = 1:
+                               every game); recording never changes the search path */
 } yk_engine_config_t;
 
 typedef struct yk_engine yk_engine_t;
@@ -178,8 +180,12 @@ int yk_engine_stats(yk_engine_t* eng, int64_t* out);
 int yk_engine_records(yk_engine_t* eng, uint64_t* states, int32_t* info, uint64_t* ctr, double* values,
                       uint64_t* final_states, int32_t* n_moves, int64_t* visits_off, int32_t* visits,
                       int64_t* n_visits);
-/* record_predictions: HOST pi[n][max_expansions][3226], v[n][max_expansions], count[n] */
-int yk_engine_predictions(yk_engine_t* eng, float* pi, float* v, int32_t* count);
+/* record_predictions, for the R = ceil(n_envs / record_stride) sampled games (game r * record_stride):
+ * HOST pi[R][max_expansions][3226] = the prior each expansion was made with, masked (MCTS.py:86-88:
+ * Ps * valids, before the renormalisation, the production valid-only softmax of yk_net_leaf_prior),
+ * v[R][max_expansions], leaves[R][max_expansions] the expanded canonical states, count[R] the
+ * expansions of each game (> max_expansions: the record was truncated).  Any may be NULL. */
+int yk_engine_predictions(yk_engine_t* eng, float* pi, float* v, yk_state_t* leaves, int32_t* count);
 /* Fixed-size trajectory records of the last batch for the multi-GPU all-gather:
  * yk_engine_record_bytes = size of the packed image; yk_engine_pack_records copies it
  * (device to device, async on `stream`) into dst (device, >= that many bytes).  Image:

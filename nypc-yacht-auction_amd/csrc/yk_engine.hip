@@ -61,7 +61,7 @@ struct EngDev {
     int sims, temp_threshold;
     float c32;
     int prior;  // 0 net, 1 hash
-    int rec_pred, max_exp;
+    int rec_pred, max_exp, rec_stride;  // record_predictions: games e % rec_stride == 0, slot e / rec_stride
     int arena;             // 1 while yk_arena runs
     int arena_agent, arena_opp;  // YK_PLAYER_* of the seat-agent_seat player and of the other seat
     uint64_t seed;
@@ -110,8 +110,9 @@ struct EngDev {
     double* final_r;       // [E]
     int32_t* final_cur;    // [E]
     int32_t* final_tot;    // [E][2] score totals with bonus (getGameEnded, YachtGame.py:408-428)
-    float* rec_pi;         // [E][max_exp][3226]  (record_predictions)
-    float* rec_v;          // [E][max_exp]
+    float* rec_pi;         // [R][max_exp][3226]  (record_predictions; R = ceil(E / rec_stride))
+    float* rec_v;          // [R][max_exp]
+    yk_state_t* rec_leaf;  // [R][max_exp] the expanded leaf (canonical state)
     // stats
     uint64_t* gstats;      // [E][8]: expansions, scanned, path edges, vnew, max nodes, max edges, max arena, sims
     uint32_t* err;         // [1] error bits
@@ -686,10 +687,12 @@ __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int l
         float qt[PW_TMAX];
         float v, mx = 0.f, lse = 0.f;
         const int pidx = (int)d.gstats[(long)e * 8 + 0];
-        const bool rec = d.rec_pred && pidx < d.max_exp;
-        float* rpi = rec ? d.rec_pi + ((long)e * d.max_exp + pidx) * ASIZE : nullptr;
+        // record_predictions samples games without changing the path: the production prior
+        // below is what gets recorded (after masking, i.e. exactly what np.sum / P see)
+        const bool rec = d.rec_pred && (e % d.rec_stride) == 0 && pidx < d.max_exp;
+        const long rslot = rec ? (long)(e / d.rec_stride) * d.max_exp + pidx : 0;
         bool masked = false;  // q / qt already hold Ps * valids
-        if (d.prior == 0 && !rec) {
+        if (d.prior == 0) {
             // pi = exp(log_softmax(logits)) (NNet.py:193) at the valid actions only: the forward
             // supplies each row's (max, log sum exp), so the invalid logits are never read
             const float* x = d.logits + (long)e * PI_LD + st;
@@ -727,41 +730,6 @@ __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int l
             v = d.vpred[e];
             masked = true;
             SEL_ACC(8, t_x0);
-        } else if (d.prior == 0) {
-            // recording predictions: the whole pi row, max and sum over the 3226 logits here
-            const float* x = d.logits + (long)e * PI_LD + st;
-            const float NEG = -INFINITY;
-#pragma unroll
-            for (int j = 0; j < PW_GMAX; j++)
-                q[j] = j < G ? *reinterpret_cast<const float4*>(x + 8 * j + 4 * h) : make_float4(NEG, NEG, NEG, NEG);
-#pragma unroll
-            for (int r = 0; r < PW_TMAX; r++) qt[r] = (h == 0 && r < R) ? x[8 * G + r] : NEG;
-            float m = NEG;
-#pragma unroll
-            for (int j = 0; j < PW_GMAX; j++) m = fmaxf(fmaxf(m, fmaxf(q[j].x, q[j].y)), fmaxf(q[j].z, q[j].w));
-#pragma unroll
-            for (int r = 0; r < PW_TMAX; r++) m = fmaxf(m, qt[r]);
-            m = wave_max(m);
-            // hardware exp (<= 2 ulp; the 1e-5 contract holds, tests/test_gpu_selfplay.py); the
-            // same softmax_p() produces the recorded prior, the pairwise sum and P below
-            float se = 0.f;
-#pragma unroll
-            for (int j = 0; j < PW_GMAX; j++)
-                se += (__expf(q[j].x - m) + __expf(q[j].y - m)) + (__expf(q[j].z - m) + __expf(q[j].w - m));
-#pragma unroll
-            for (int r = 0; r < PW_TMAX; r++) se += __expf(qt[r] - m);
-            lse = __logf(wave_sumf(se));
-            mx = m;
-#pragma unroll
-            for (int j = 0; j < PW_GMAX; j++) {
-                q[j].x = softmax_p(q[j].x, m, lse);
-                q[j].y = softmax_p(q[j].y, m, lse);
-                q[j].z = softmax_p(q[j].z, m, lse);
-                q[j].w = softmax_p(q[j].w, m, lse);
-            }
-#pragma unroll
-            for (int r = 0; r < PW_TMAX; r++) qt[r] = softmax_p(qt[r], m, lse);
-            v = d.vpred[e];
         } else {
 #pragma unroll
             for (int j = 0; j < PW_GMAX; j++) {
@@ -773,15 +741,6 @@ __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int l
 #pragma unroll
             for (int r = 0; r < PW_TMAX; r++) qt[r] = (h == 0 && r < R) ? hash_prior_pi(hsh, st + 8 * G + r) : 0.f;
             v = hash_prior_v(hsh);
-        }
-        if (rec) {
-#pragma unroll
-            for (int j = 0; j < PW_GMAX; j++)
-                if (j < G) *reinterpret_cast<float4*>(rpi + st + 8 * j + 4 * h) = q[j];
-#pragma unroll
-            for (int r = 0; r < PW_TMAX; r++)
-                if (h == 0 && r < R) rpi[st + 8 * G + r] = qt[r];
-            if (lane == 0) d.rec_v[(long)e * d.max_exp + pidx] = v;
         }
         SEL_T0(t_x1);
         // mask with the valid moves
@@ -798,6 +757,19 @@ __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int l
 #pragma unroll
         for (int r = 0; r < PW_TMAX; r++)
             if (h == 0 && r < R && !masked && !valid(st + 8 * G + r)) qt[r] = 0.f;
+        if (rec) {  // Ps * valids (MCTS.py:88) of this expansion, the leaf and v
+            float* rpi = d.rec_pi + rslot * ASIZE;
+#pragma unroll
+            for (int j = 0; j < PW_GMAX; j++)
+                if (j < G) *reinterpret_cast<float4*>(rpi + st + 8 * j + 4 * h) = q[j];
+#pragma unroll
+            for (int r = 0; r < PW_TMAX; r++)
+                if (h == 0 && r < R) rpi[st + 8 * G + r] = qt[r];
+            if (lane == 0) {
+                d.rec_v[rslot] = v;
+                st_state(d.rec_leaf + rslot, s);
+            }
+        }
         // numpy pairwise_sum on the leaf: r_k = a[k] + a[8 + k] + ..., then
         // ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)), then the tail one by one
         float4 racc = q[0];
@@ -1212,7 +1184,7 @@ int run_sims(yk_engine* eng, int sims, const uint32_t* env_ids, uint64_t* ctr, h
             prof_mark(eng, KC_FORWARD, s);
             // predict row = game: no compaction; workgroups without a leaf exit at once
             int rc = launch_forward(eng->net->dev, d.leaf_state, nullptr, nullptr, nullptr, d.E, eng->logits, eng->vpred, s,
-                                    d.leaf_flag, eng->mlse, d.rec_pred == 0);
+                                    d.leaf_flag, eng->mlse, true);
             if (rc) return rc;
         }
         prof_mark(eng, KC_EXPAND, s);
@@ -1272,6 +1244,8 @@ int yk_engine_create(yk_engine_t** out, const yk_engine_config_t* cfg, yk_net_t*
     d.VCAP = 2 * cfg->max_moves * std::max(cfg->sims, 32);
     d.rec_pred = cfg->record_predictions ? 1 : 0;
     d.max_exp = cfg->record_predictions ? std::max(cfg->max_expansions, 1) : 0;
+    d.rec_stride = std::max(cfg->record_stride, 1);
+    const size_t R = ((size_t)cfg->n_envs + d.rec_stride - 1) / d.rec_stride;
     const size_t E = (size_t)d.E;
     int rc = YK_OK;
 #define A(p, n) \
@@ -1326,8 +1300,9 @@ int yk_engine_create(yk_engine_t** out, const yk_engine_config_t* cfg, yk_net_t*
         A(eng->logits, E * (size_t)PI_LD);
     }
     if (d.rec_pred) {
-        A(d.rec_pi, E * (size_t)d.max_exp * ASIZE);
-        A(d.rec_v, E * (size_t)d.max_exp);
+        A(d.rec_pi, R * (size_t)d.max_exp * ASIZE);
+        A(d.rec_v, R * (size_t)d.max_exp);
+        A(d.rec_leaf, R * (size_t)d.max_exp);
     }
 #undef A
     if (rc == YK_OK && hipHostMalloc((void**)&eng->host_done, sizeof(int32_t)) != hipSuccess) rc = YK_ERR_NOMEM;
@@ -1556,16 +1531,18 @@ int yk_engine_records(yk_engine_t* eng, uint64_t* states, int32_t* info, uint64_
     return YK_OK;
 }
 
-int yk_engine_predictions(yk_engine_t* eng, float* pi, float* v, int32_t* count) {
+int yk_engine_predictions(yk_engine_t* eng, float* pi, float* v, yk_state_t* leaves, int32_t* count) {
     if (!eng || !eng->d.rec_pred) return YK_ERR_ARG;
     EngDev& d = eng->d;
+    const size_t R = ((size_t)d.E + d.rec_stride - 1) / d.rec_stride, X = (size_t)d.max_exp;
     YK_HIP(hipDeviceSynchronize());
-    if (pi) YK_HIP(hipMemcpy(pi, d.rec_pi, sizeof(float) * (size_t)d.E * d.max_exp * ASIZE, hipMemcpyDeviceToHost));
-    if (v) YK_HIP(hipMemcpy(v, d.rec_v, sizeof(float) * (size_t)d.E * d.max_exp, hipMemcpyDeviceToHost));
+    if (pi) YK_HIP(hipMemcpy(pi, d.rec_pi, sizeof(float) * R * X * ASIZE, hipMemcpyDeviceToHost));
+    if (v) YK_HIP(hipMemcpy(v, d.rec_v, sizeof(float) * R * X, hipMemcpyDeviceToHost));
+    if (leaves) YK_HIP(hipMemcpy(leaves, d.rec_leaf, sizeof(yk_state_t) * R * X, hipMemcpyDeviceToHost));
     if (count) {
         std::vector<uint64_t> gs((size_t)d.E * 8);
         YK_HIP(hipMemcpy(gs.data(), d.gstats, sizeof(uint64_t) * gs.size(), hipMemcpyDeviceToHost));
-        for (int e = 0; e < d.E; e++) count[e] = (int32_t)gs[(size_t)e * 8];
+        for (size_t r = 0; r < R; r++) count[r] = (int32_t)gs[r * d.rec_stride * 8];  // > max_expansions: truncated
     }
     return YK_OK;
 }

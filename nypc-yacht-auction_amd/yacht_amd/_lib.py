@@ -33,7 +33,7 @@ class YkError(RuntimeError):
 class YkEngineConfig(C.Structure):
     _fields_ = [("n_envs", C.c_int), ("sims", C.c_int), ("cpuct", C.c_double), ("temp_threshold", C.c_int),
                 ("max_moves", C.c_int), ("prior", C.c_int), ("record_predictions", C.c_int),
-                ("max_expansions", C.c_int), ("arena_entries", C.c_int64)]
+                ("max_expansions", C.c_int), ("arena_entries", C.c_int64), ("record_stride", C.c_int)]
 
 
 # name -> argtypes (restype int unless listed in _RESTYPE)
@@ -81,7 +81,7 @@ SIGNATURES = {
     "yk_engine_profile": [P, I],
     "yk_engine_kernel_times": [P, P, P],
     "yk_engine_records": [P, P, P, P, P, P, P, P, P, P],
-    "yk_engine_predictions": [P, P, P, P],
+    "yk_engine_predictions": [P, P, P, P, P],
     "yk_engine_record_bytes": [P],
     "yk_engine_pack_records": [P, P, C.c_int64, P],
     "yk_mcts_search": [P, P, U64, P, P, I, P, P],

@@ -21,7 +21,7 @@ ACTION_SIZE = 3226
 class SelfPlayEngine:
     def __init__(self, n_envs: int, sims: int, cpuct: float = 1.5, temp_threshold: int = 15, net=None,
                  prior: str = "net", max_moves: int = 64, record_predictions: bool = False,
-                 max_expansions: int = 0, arena_entries: int = 0):
+                 max_expansions: int = 0, arena_entries: int = 0, record_stride: int = 1):
         if prior not in ("net", "hash"):
             raise ValueError("prior is 'net' (YachtNNet on MFMA) or 'hash' (deterministic test prior)")
         if prior == "net" and net is None:
@@ -30,7 +30,7 @@ class SelfPlayEngine:
                                   max_moves=max_moves, prior=0 if prior == "net" else 1,
                                   record_predictions=int(record_predictions),
                                   max_expansions=max_expansions or (max_moves * sims + 8),
-                                  arena_entries=arena_entries)
+                                  arena_entries=arena_entries, record_stride=max(int(record_stride), 1))
         self.net = net  # keep the weights alive
         h = C.c_void_p()
         call("yk_engine_create", C.byref(h), C.byref(self.cfg), C.c_void_p(net.handle if net is not None else None))
@@ -117,13 +117,21 @@ class SelfPlayEngine:
         return dict(states=states, info=info, ctr=ctr, values=values, final=final, n_moves=nm,
                     visits_off=voff.reshape(-1)[:E * M + 1], visits=visits[:int(nv[0])])
 
-    def predictions(self):
-        E, X = self.n_envs, self.cfg.max_expansions
-        pi = np.zeros((E, X, ACTION_SIZE), dtype=np.float32)
-        v = np.zeros((E, X), dtype=np.float32)
-        cnt = np.zeros(E, dtype=np.int32)
-        call("yk_engine_predictions", self.handle, pi.ctypes.data, v.ctypes.data, cnt.ctypes.data)
-        return pi, v, cnt
+    def predictions(self, leaves: bool = False):
+        """(pi, v, count[, leaves]) of the recorded games (every record_stride-th): pi[r, k] is
+        Ps * valids of game r * record_stride's k-th expansion (MCTS.py:86-88, before the
+        renormalisation), exactly what the search used; count[r] its expansions."""
+        R = (self.n_envs + self.cfg.record_stride - 1) // self.cfg.record_stride
+        X = self.cfg.max_expansions
+        pi = np.zeros((R, X, ACTION_SIZE), dtype=np.float32)
+        v = np.zeros((R, X), dtype=np.float32)
+        lv = np.zeros((R, X, 8), dtype=np.uint64) if leaves else None
+        cnt = np.zeros(R, dtype=np.int32)
+        call("yk_engine_predictions", self.handle, pi.ctypes.data, v.ctypes.data,
+             lv.ctypes.data if leaves else None, cnt.ctypes.data)
+        if (cnt > X).any():
+            raise RuntimeError(f"prediction record truncated: {int(cnt.max())} expansions > max_expansions {X}")
+        return (pi, v, cnt, lv) if leaves else (pi, v, cnt)
 
     def record_bytes(self) -> int:
         n = int(lib().yk_engine_record_bytes(self.handle))

@@ -214,6 +214,24 @@ def policy_action(net, states):
     return a, margin
 
 
+def mcts_prior(pi, states):
+    """MCTS.py:86-111 for given predict outputs: P = Ps * valids / np.sum (numpy's float32
+    pairwise sum of the masked 3226-vector), the uniform-over-valid fallback when that sum is 0,
+    action 0 when nothing is valid.  pi f32[n, 3226], canonical states [n, 8] -> f32[n, 3226]."""
+    ok, cnt = valid(states, 1)
+    p = np.asarray(pi, dtype=np.float32) * ok.astype(np.float32)
+    out = np.zeros_like(p)
+    for i in range(len(p)):
+        s = pairwise_sum(p[i])
+        if s > 0:
+            out[i] = p[i] / s
+        elif cnt[i] > 0:
+            out[i] = ok[i].astype(np.float32) / np.float32(cnt[i])
+        else:
+            out[i, 0] = 1.0
+    return out
+
+
 MODE_HASH, MODE_MLP, MODE_REPLAY = 0, 1, 2
 PLAYERS = {"mcts": 0, "random": 1, "greedy": 2}
 

@@ -1125,6 +1125,7 @@ void or_hash_prior(const uint64_t* w, float* pi, float* v, int n) {
     for (int i = 0; i < n; i++) hash_prior(w + 8 * i, pi + (size_t)ASIZE * i, v + i);
 }
 void or_net_predict(void* net, const uint64_t* w, float* pi, float* v, int n) {
+#pragma omp parallel for schedule(dynamic, 16)
     for (int i = 0; i < n; i++) {
         st_t s;
         float x[FEAT];

@@ -1,0 +1,84 @@
+"""Shared parity checks for the GPU tests (test infrastructure: uses the oracle as the checker)."""
+import numpy as np
+
+from oracle import oracle as O
+
+# The north star's tolerance is on predict's policy tensor (pi within 1e-5, as test_gpu_net; x3 here
+# for the prior and its renormalising sum, as test_gpu_net's leaf-prior test) and value (1e-5).  The
+# checker is a float64 forward of the same weights (torch on the CPU): the engine's f32-equivalent
+# products and the reference's own f32 CPU path each sit a few 1e-6 off it, so two f32 paths can
+# differ by twice that (measured: v 1.1e-5 engine vs oracle; tools/diag_prior.py,
+# profiles/r02_diag_prior.log).  After MCTS.py:88-91's renormalisation over a few valid actions of
+# small total mass, P inherits the logits' absolute error as a RELATIVE error (measured vs float64:
+# engine 6.3e-5, the reference's torch fp32 4.8e-5, the oracle 5.9e-5), so P is checked in predict
+# space (P x the valid mass, i.e. the pi that renormalises to it) at the north-star tolerance, and
+# directly against the reference's own f32 forward: P's worst relative error (entries > 1e-3) may be
+# at most REF_FACTOR times that of torch fp32 on the CPU over the same rows.  The engine's products
+# carry 22-bit operands (fp16 hi + lo planes) and drop lo*lo, so its tails sit about 2x torch fp32's
+# (measured 1.30e-4 vs 6.3e-5 over 14,628 arena leaves); the check prints both.
+RTOL_PI, ATOL_PI, ATOL_V = 3e-5, 1e-7, 1e-5
+REF_FACTOR = 3.0
+_NETS = {}
+
+
+def torch_predict(sd, hidden, nblocks, states, dtype, chunk=4096):
+    """YachtNNet.forward (yacht/pytorch/YachtNNet.py) on the CPU in `dtype`, eval mode, over
+    state_to_vec of the states (the oracle's featurize, pinned to the reference): (pi, v) as
+    NNetWrapper.predict returns them (exp(log_softmax), NNet.py:193)."""
+    import torch
+    from yacht_amd.nnet import YachtNNet
+    key = (id(sd), hidden, nblocks, dtype)
+    if key not in _NETS:
+        m = YachtNNet(hidden=hidden, nblocks=nblocks).to(dtype)
+        m.load_state_dict({k: torch.as_tensor(np.asarray(t)).to(dtype) for k, t in sd.items()})
+        _NETS[key] = m.eval()
+    m = _NETS[key]
+    x = torch.from_numpy(O.featurize(states)).to(dtype)
+    pis, vs = [], []
+    with torch.no_grad():
+        for i in range(0, len(x), chunk):
+            lg, v = m(x[i:i + chunk])
+            pis.append(torch.exp(torch.log_softmax(lg, 1)).double().numpy())
+            vs.append(v.double().numpy().reshape(-1))
+    return np.concatenate(pis), np.concatenate(vs)
+
+
+def renorm64(pi, ok):
+    p = np.where(ok, np.asarray(pi, dtype=np.float64), 0.0)
+    s = p.sum(1, keepdims=True)
+    return np.divide(p, s, out=np.zeros_like(p), where=s > 0), s
+
+
+def check_recorded_priors(pi, v, cnt, leaves, sd, hidden=256, nblocks=6, every=1):
+    """The recorded priors (the production valid-only forward inside the engine, Ps * valids)
+    renormalised as MCTS.py:88-91 does vs a float64 forward put through the same lines: zero
+    outside the valid set; within the north-star tolerance in predict space; P and v no further
+    from exact than REF_FACTOR x the reference's own f32 forward (v: or within 1e-5)."""
+    rs = np.concatenate([np.full(len(range(0, int(c), every)), r) for r, c in enumerate(cnt)])
+    ks = np.concatenate([np.arange(0, int(c), every) for c in cnt])
+    S = leaves[rs, ks]
+    P = pi[rs, ks]
+    ok, _ = O.valid(S, 1)
+    ok = ok.astype(bool)
+    assert not P[~ok].any()
+    import torch
+    tpi, tv = torch_predict(sd, hidden, nblocks, S, torch.float64)
+    Pt, mass = renorm64(tpi, ok)
+    none = ~ok.any(1)
+    Pt[none, 0] = 1.0  # no valid action: P is one-hot on action 0 (MCTS.py:108-111)
+    Pe = O.mcts_prior(P, S).astype(np.float64)  # exactly as the reference renormalises (f32, pairwise)
+    np.testing.assert_allclose(Pe * mass, Pt * mass, rtol=RTOL_PI, atol=ATOL_PI)
+    # v within 1e-5 of exact, or no worse than the reference's own f32 CPU forward (x REF_FACTOR);
+    # P no worse than that forward, relative to exact arithmetic
+    rpi, rv = torch_predict(sd, hidden, nblocks, S, torch.float32)
+    verr_e, verr_r = float(np.abs(v[rs, ks] - tv).max()), float(np.abs(rv - tv).max())
+    assert verr_e <= max(ATOL_V, REF_FACTOR * verr_r), (verr_e, verr_r)
+    Pr, _ = renorm64(rpi, ok)
+    Pr[none, 0] = 1.0
+    big = Pt > 1e-3
+    err_e = float((np.abs(Pe - Pt)[big] / Pt[big]).max())
+    err_r = float((np.abs(Pr - Pt)[big] / Pt[big]).max())
+    print(f"priors of {len(rs)} leaves: max rel err of P vs float64 {err_e:.2e} (torch fp32 {err_r:.2e}), "
+          f"max |v err| {verr_e:.2e} (torch fp32 {verr_r:.2e})")
+    assert err_e <= REF_FACTOR * err_r, (err_e, err_r)
+    return len(rs)

@@ -13,6 +13,7 @@ import pytest
 
 from oracle import oracle as O
 from oracle import spec
+from helpers import check_recorded_priors
 
 pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
@@ -99,6 +100,55 @@ def test_arena_net_prior_replayed_by_oracle(Y):
     assert np.array_equal(r["totals"], o["totals"])
     assert np.array_equal(r["final"], o["final"])
     assert np.array_equal(r["ctr"], o["stats"][:, 4].astype(np.uint64))
+
+
+def _compare_arena(r, o, n):
+    assert o["nerr"] == 0
+    assert np.array_equal(r["result"], o["result"])
+    assert np.array_equal(r["totals"], o["totals"])
+    assert np.array_equal(r["final"], o["final"])
+    assert np.array_equal(r["n_moves"], o["stats"][:, 0].astype(np.int32))
+    assert np.array_equal(r["ctr"], o["stats"][:, 4].astype(np.uint64))
+    for i in range(n):
+        m = int(r["n_moves"][i])
+        assert np.array_equal(r["actions"][i, :m], o["actions"][i, :m]), i
+
+
+def test_arena_1000_games_hash_prior_vs_oracle(Y):
+    """Config 4's shape: Arena.playGames(1000) (Arena.py:95-130: half the games in each seat),
+    MCTS temp 0 at 25 sims vs RandomYachtPlayer, every result, both totals, every action and
+    final board bit-exact against the oracle's own independent run."""
+    E, _ = Y
+    n, sims, seed, base = 1000, 25, 31337, 0
+    seats = np.where(np.arange(n) < n // 2, 1, -1).astype(np.int32)
+    eng = E.SelfPlayEngine(n, sims, 1.5, 0, prior="hash", max_moves=48)
+    eng.arena(seats, seed, base)
+    r = eng.arena_results()
+    o = O.arena(np.arange(base, base + n), seats, seed, sims, 1.5, max_moves=48, threads=16)
+    _compare_arena(r, o, n)
+    ended, tot = O.ended(r["final"], np.ones(n, dtype=np.int32))
+    assert np.array_equal(tot, r["totals"]) and np.array_equal(ended, r["result"])
+
+
+def test_arena_1000_games_net_prior_replayed_by_oracle(Y):
+    """Config 4 as bench.py runs it (1000 games, 25 sims, random-init YachtNNet 256 x 6 on the
+    production valid-only forward): every game's predictions recorded, the oracle replays them
+    and ends all 1000 games identically; the recorded priors match the oracle net."""
+    E, N = Y
+    n, sims, seed, base = 1000, 25, 4711, 100000
+    sd = spec.closed_form_weights(256, 6)
+    seats = np.where(np.arange(n) < n // 2, 1, -1).astype(np.int32)
+    eng = E.SelfPlayEngine(n, sims, 1.5, 0, net=N.YkNet(sd, 256, 6), max_moves=48, record_predictions=True,
+                           max_expansions=24 * sims + 16)
+    eng.arena(seats, seed, base)
+    r = eng.arena_results()
+    pi, v, cnt, leaves = eng.predictions(leaves=True)
+    replay = [(pi[e, :cnt[e]], v[e, :cnt[e]]) for e in range(n)]
+    o = O.arena(np.arange(base, base + n), seats, seed, sims, 1.5, O.MODE_REPLAY, replay=replay, max_moves=48,
+                threads=16)
+    assert np.array_equal(o["stats"][:, 1], cnt)
+    _compare_arena(r, o, n)
+    assert check_recorded_priors(pi, v, cnt, leaves, sd, every=40) > 10000
 
 
 def test_arena_after_selfplay_and_back(Y):

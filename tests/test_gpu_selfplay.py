@@ -4,16 +4,20 @@ MCTS.search) and of the plugin classes.
 * hash prior: the engine reproduces, bit for bit, whole episodes that the REFERENCE's own
   Coach/MCTS/YachtGame produced (tests/golden/episodes_hash.npz), and the C oracle on
   further games;
-* YachtNNet prior: the engine records every expansion's (pi, v); the oracle replays the
-  same predictions through its restatement of MCTS and must produce identical visit
-  counts, actions, RNG counters and values (search and env are exact; predict is checked
-  separately to 1e-5 in test_gpu_net.py).
+* YachtNNet prior: the engine records the prior every expansion of the sampled games was
+  made with (the production valid-only forward, Ps * valids) with its leaf and v; the oracle
+  replays those predictions through its restatement of MCTS and must produce identical visit
+  counts, actions, RNG counters and values, and each recorded prior, renormalised as
+  MCTS.py:86-111, is within 3e-5 of the oracle net's (search and env are exact; predict
+  itself is checked to 1e-5 in test_gpu_net.py);
+* both at the bench configuration (4096 games x 100 sims) on sampled games.
 """
 import numpy as np
 import pytest
 
 from oracle import oracle as O
 from oracle import spec
+from helpers import check_recorded_priors
 
 pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
@@ -101,21 +105,73 @@ def test_selfplay_net_prior_replayed_by_oracle(Y):
     eng.run(seed, base)
     assert eng.stats()["errors"] == 0
     rec = eng.records()
-    pi, v, cnt = eng.predictions()
+    pi, v, cnt, leaves = eng.predictions(leaves=True)
     replay = [(pi[e, :cnt[e]], v[e, :cnt[e]]) for e in range(n)]
     orc = O.selfplay(np.arange(base, base + n), seed, sims, 1.5, 15, O.MODE_REPLAY, replay=replay)
     assert orc["nerr"] == 0
     assert np.array_equal(orc["stats"][:, 1], cnt)  # every recorded prediction consumed
     _compare_to_oracle(rec, orc, n)
-    # the recorded predictions themselves are the f32 MLP within tolerance
-    onet = O.Net(sd, 256, 6)
-    pick = [(e, k) for e in range(n) for k in (0, int(cnt[e]) // 2, int(cnt[e]) - 1)]
-    # states of those expansions are not recorded; check the root predictions instead
-    roots = rec["states"][:, 0]
-    opi, ov = onet.predict_states(roots)
-    np.testing.assert_allclose(pi[:, 0], opi, rtol=1e-5, atol=1e-7)
-    np.testing.assert_allclose(v[:, 0], ov, atol=1e-5)
-    assert len(pick) == 3 * n
+    # every recorded prediction (root and non-root expansions) is the f32 MLP within tolerance
+    assert np.array_equal(leaves[:, 0], rec["states"][:, 0])  # the first expansion is the root
+    assert check_recorded_priors(pi, v, cnt, leaves, sd) == int(cnt.sum())
+
+
+def test_selfplay_net_prior_at_bench_size(Y):
+    """Config 2 (4096 games x 100 sims, YachtNNet 256 x 6) exactly as bench.py runs it - the
+    valid-only forward and the expand's prior branch - with every 64th game's predictions
+    recorded: the oracle replays those 64 games bit for bit (visit counts of every move,
+    actions, counters, values, final boards), and the recorded priors match the oracle net."""
+    _, E, N = Y
+    n, sims, seed, base, stride = 4096, 100, 2024, 0, 64
+    sd = spec.closed_form_weights(256, 6)
+    eng = E.SelfPlayEngine(n, sims, 1.5, 15, net=N.YkNet(sd, 256, 6), max_moves=48, record_predictions=True,
+                           max_expansions=48 * sims + 8, record_stride=stride)
+    eng.run(seed, base)
+    st = eng.stats()
+    assert st["errors"] == 0 and st["sims"] == 48 * sims  # lock-step simulations over the 48 moves
+    rec = eng.records()
+    assert (rec["n_moves"] == 48).all()
+    pi, v, cnt, leaves = eng.predictions(leaves=True)
+    pick = np.arange(0, n, stride)
+    replay = [(pi[r, :cnt[r]], v[r, :cnt[r]]) for r in range(len(pick))]
+    orc = O.selfplay(base + pick, seed, sims, 1.5, 15, O.MODE_REPLAY, replay=replay, max_moves=48, threads=16)
+    assert orc["nerr"] == 0
+    assert np.array_equal(orc["stats"][:, 1], cnt)
+    for r, e in enumerate(pick):
+        M = int(orc["stats"][r, 0])
+        assert rec["n_moves"][e] == M
+        assert np.array_equal(rec["states"][e, :M], orc["canon"][r, :M])
+        assert np.array_equal(rec["info"][e, :M, :7], orc["mv"][r, :M, :7]), e
+        assert np.array_equal(rec["ctr"][e, :M], orc["ctr"][r, :M])
+        for m in range(M):
+            assert np.array_equal(_dense_counts(rec, e, m), orc["counts"][r, m]), (e, m)
+        assert np.array_equal(rec["values"][e, :M], orc["values"][r, :M])
+        assert np.array_equal(rec["final"][e], orc["final"][r])
+    assert check_recorded_priors(pi, v, cnt, leaves, sd, every=16) > 10000
+
+
+def test_selfplay_hash_prior_at_bench_size(Y):
+    """Config 2's shape (4096 games x 100 sims) with the hash prior: every 64th game against the
+    oracle's own independent run (no replay), bit for bit."""
+    _, E, _ = Y
+    n, sims, seed, base = 4096, 100, 77, 5000
+    eng = E.SelfPlayEngine(n, sims, 1.5, 15, prior="hash", max_moves=48)
+    eng.run(seed, base)
+    st = eng.stats()
+    assert st["errors"] == 0
+    rec = eng.records()
+    pick = np.arange(0, n, 64)
+    orc = O.selfplay(base + pick, seed, sims, 1.5, 15, O.MODE_HASH, max_moves=48, threads=16)
+    assert orc["nerr"] == 0
+    for r, e in enumerate(pick):
+        M = int(orc["stats"][r, 0])
+        assert rec["n_moves"][e] == M == 48
+        assert np.array_equal(rec["info"][e, :M, :7], orc["mv"][r, :M, :7]), e
+        assert np.array_equal(rec["ctr"][e, :M], orc["ctr"][r, :M])
+        for m in range(M):
+            assert np.array_equal(_dense_counts(rec, e, m), orc["counts"][r, m]), (e, m)
+        assert np.array_equal(rec["values"][e, :M], orc["values"][r, :M])
+        assert np.array_equal(rec["final"][e], orc["final"][r])
 
 
 def test_plugin_classes_replay_reference_episode(Y, golden):

@@ -178,3 +178,23 @@ def test_arena_player_pairings_match_reference(golden, fixture, agent, opponent)
     assert np.array_equal(r["stats"][:, 4], g["ctr_end"])
     for i, n in enumerate(g["n_moves"]):
         assert np.array_equal(r["actions"][i, :n], g["actions"][i, :n])
+
+
+def test_prior_checker_accepts_the_oracle_net_and_rejects_a_perturbed_one(golden):
+    """tests/helpers.check_recorded_priors (the GPU tests' prior check) on the CPU: the oracle's
+    f32 net, recorded the way the engine records (Ps * valids), passes against the float64
+    forward; the same priors with one logit moved by 1e-3 do not."""
+    from helpers import check_recorded_priors
+    sd = spec.closed_form_weights(64, 1)
+    W = golden("states.npz")["states"][::23][:400]
+    pi, v = O.Net(sd, 64, 1).predict_states(W)
+    ok = O.valid(W, 1)[0].astype(bool)
+    rec = np.where(ok, pi, 0.0).astype(np.float32)[None]
+    cnt = np.array([len(W)])
+    assert check_recorded_priors(rec, v[None], cnt, W[None], sd, 64, 1) == len(W)
+    bad = rec.copy()
+    r = int(np.argmax((ok.sum(1) > 1) & (ok.sum(1) < 20)))
+    a = int(np.flatnonzero(ok[r])[0])
+    bad[0, r, a] *= np.float32(np.exp(1e-3))
+    with pytest.raises(AssertionError):
+        check_recorded_priors(bad, v[None], cnt, W[None], sd, 64, 1)
