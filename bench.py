@@ -166,6 +166,8 @@ def main():
     ap.add_argument("--no-arena", action="store_true", help="skip the config-4 Arena leg")
     ap.add_argument("--no-train", action="store_true", help="skip the config-5 train-step leg")
     ap.add_argument("--dist-backend", default=None, help="nccl (RCCL, default on GPUs) or gloo (rehearsal)")
+    ap.add_argument("--groups", type=int, default=0,
+                    help="game groups on their own streams (0: the engine's auto choice)")
     ap.add_argument("--arena-entries", type=int, default=0,
                     help="P-arena entries per game (0: the engine's overflow-free default)")
     args = ap.parse_args()
@@ -185,7 +187,8 @@ def main():
     model = YachtNNet(hidden=H, nblocks=NB)  # random init of the reference architecture
     sd = model.state_dict()
     net = YkNet(sd, H, NB)
-    eng = SelfPlayEngine(args.envs, args.sims, 1.5, 15, net=net, max_moves=64, arena_entries=args.arena_entries)
+    eng = SelfPlayEngine(args.envs, args.sims, 1.5, 15, net=net, max_moves=64, arena_entries=args.arena_entries,
+                         groups=args.groups)
     stream = torch.cuda.current_stream()
     env_base = D.env_base(rank, args.envs)
     gathered_bytes = 0
@@ -255,6 +258,7 @@ def main():
         "episodes_per_s": games / elapsed,
         "expansions_per_s_per_gpu": value / world,
         "expansions_per_episode_batch": exps / args.steps,
+        "game_groups": st["groups"],
         "capacity_use": {k: int(st[k]) for k in ("max_nodes", "node_cap", "max_edges", "edge_cap", "max_arena",
                                                  "arena_cap")},
     }

@@ -149,6 +149,9 @@ typedef struct {
     int64_t arena_entries;  /* per game per generation P/edge-slot entries; 0 = default */
     int record_stride;      /* record_predictions samples games e with e % record_stride == 0 (0 = 1:
                                every game); recording never changes the search path */
+    int groups;             /* game groups, each on its own stream so that one group's forward runs
+                               beside another's expand (results do not depend on it); 0 = auto
+                               (2 with the net prior at >= 8192 games, else 1), at most 8 */
 } yk_engine_config_t;
 
 typedef struct yk_engine yk_engine_t;
@@ -167,7 +170,8 @@ int yk_engine_profile(yk_engine_t* eng, int enable);
 int yk_engine_kernel_times(yk_engine_t* eng, double* ms, int64_t* launches);
 /* HOST out[16]: 0 expansions, 1 valid entries scanned by UCB, 2 real moves (max over games),
  * 3 device error flags, 4 max live nodes, 5 max live edges, 6 max arena entries used (per shard),
- * 7 new-node valid entries written, 8 search path edges backed up, 9 lock-step sims run */
+ * 7 new-node valid entries written, 8 search path edges backed up, 9 lock-step sims run,
+ * 10-13 node / edge / arena / visit capacities, 14 game groups */
 int yk_engine_stats(yk_engine_t* eng, int64_t* out);
 /* Copies the last episode batch to HOST arrays (any may be NULL):
  *   states[n][max_moves][8]  canonical board of each example (Coach.py:57,61)

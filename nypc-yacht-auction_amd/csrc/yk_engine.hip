@@ -26,6 +26,8 @@
 #include "yk_common.h"
 #include "yk_net.h"
 
+#define YK_MAX_GROUPS 8
+
 using namespace yk;
 
 namespace {
@@ -33,6 +35,7 @@ namespace {
 constexpr int MAXD = 64;          // max search depth (path entries)
 constexpr int LUT_N = 1 << 16;    // f32(sqrt(Ns)), f32(sqrt(Ns + 1e-8)) table size
 constexpr int GAMES_PER_BLOCK = 4;
+constexpr int GROUP_ALIGN = 16;   // group boundaries on forward row tiles
 #ifndef YK_EXPAND_WPE
 #define YK_EXPAND_WPE 4  // waves per SIMD the expand kernel is register-budgeted for
 #endif
@@ -57,6 +60,7 @@ struct Edge {             // 16 bytes
 
 struct EngDev {
     int E, NCAP, HCAP, ECAP, M, VCAP;
+    int e_lo, e_hi;        // the game group a per-game launch covers ([0, E) unless pipelined)
     int64_t AE;
     int sims, temp_threshold;
     float c32;
@@ -376,8 +380,8 @@ __global__ void k_reset(EngDev d, int start_games, uint32_t env_base) {
 // game's tree into the other buffer, keeping nodes whose round >= the root's.  One wave per game.
 __global__ __launch_bounds__(256) void k_move_begin(EngDev d, int move, int external_root) {
     const int lane = threadIdx.x & 63;
-    const int e = blockIdx.x * GAMES_PER_BLOCK + (threadIdx.x >> 6);
-    if (e >= d.E) return;
+    const int e = d.e_lo + blockIdx.x * GAMES_PER_BLOCK + (threadIdx.x >> 6);
+    if (e >= d.e_hi) return;
     if (lane == 0) d.root_c[2 * e] = make_uint4(0, 0, 0, 0);  // ids move at a compaction: look the root up afresh
     if (!external_root) {
         if (d.done[e]) return;
@@ -638,8 +642,8 @@ __device__ __forceinline__ void select_game(const EngDev& d, int e, int lane, co
 
 __global__ __launch_bounds__(256) void k_select(EngDev d, const uint32_t* env_ids, uint64_t* ctr_arr) {
     const int lane = threadIdx.x & 63;
-    const int e = blockIdx.x * GAMES_PER_BLOCK + (threadIdx.x >> 6);
-    if (e >= d.E) return;
+    const int e = d.e_lo + blockIdx.x * GAMES_PER_BLOCK + (threadIdx.x >> 6);
+    if (e >= d.e_hi) return;
     select_game(d, e, lane, env_ids, ctr_arr);
 }
 
@@ -650,8 +654,8 @@ __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int l
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(YK_EXPAND_WPE))) void k_expand_backup(
     EngDev d, int do_select, const uint32_t* env_ids, uint64_t* ctr_arr) {
     const int lane = threadIdx.x & 63;
-    const int e = blockIdx.x * GAMES_PER_BLOCK + (threadIdx.x >> 6);
-    if (e >= d.E) return;
+    const int e = d.e_lo + blockIdx.x * GAMES_PER_BLOCK + (threadIdx.x >> 6);
+    if (e >= d.e_hi) return;
     if (d.done[e]) return;
 #ifdef YK_SEL_TIMING
     const unsigned long long t_ex = __builtin_amdgcn_s_memtime();
@@ -915,8 +919,8 @@ __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int l
 __global__ __launch_bounds__(256) void k_move_end(EngDev d, int move) {
     __shared__ uint32_t vis_all[GAMES_PER_BLOCK][ASIZE];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int e = blockIdx.x * GAMES_PER_BLOCK + w;
-    if (e >= d.E) return;
+    const int e = d.e_lo + blockIdx.x * GAMES_PER_BLOCK + w;
+    if (e >= d.e_hi) return;
     if (d.done[e]) return;
     uint32_t* vis = vis_all[w];
     const int g = d.gen[e];
@@ -1070,8 +1074,8 @@ __global__ void k_finalize(EngDev d) {
 // dense root visit counts for the MCTS plugin (MCTS.py:41-42)
 __global__ void k_root_counts(EngDev d, int32_t* counts) {
     const int lane = threadIdx.x & 63;
-    const int e = blockIdx.x * GAMES_PER_BLOCK + (threadIdx.x >> 6);
-    if (e >= d.E) return;
+    const int e = d.e_lo + blockIdx.x * GAMES_PER_BLOCK + (threadIdx.x >> 6);
+    if (e >= d.e_hi) return;
     int32_t* c = counts + (long)e * ASIZE;
     for (int a = lane; a < ASIZE; a += 64) c[a] = 0;
     wave_sync();
@@ -1115,11 +1119,18 @@ struct yk_engine {
     uint32_t* mcts_env = nullptr;
     bool have_records = false;
     bool have_arena = false;
-    // profiling (yk_engine_profile): per-kernel-class HIP events, accumulated per move
+    // game groups: the batch is split into `ngroups` ranges, each on its own
+    // stream, so one group's forward runs beside another group's expand
+    int ngroups = 1;
+    hipStream_t gs[YK_MAX_GROUPS] = {};
+    hipEvent_t ev_fork = nullptr, ev_join[YK_MAX_GROUPS] = {}, ev_fwd[YK_MAX_GROUPS] = {};
+    // profiling (yk_engine_profile): per-kernel-class HIP events on each group's stream
     bool prof = false;
-    std::vector<hipEvent_t> ev;
-    std::vector<int> ev_cls;
-    int ev_used = 0;
+    struct ProfLog {
+        std::vector<hipEvent_t> ev;
+        std::vector<int> cls;
+        int used = 0;
+    } pg[YK_MAX_GROUPS];
     double kms[8] = {0};
     int64_t klaunch[8] = {0};
 };
@@ -1128,29 +1139,49 @@ namespace {
 // kernel classes for yk_engine_kernel_times
 enum { KC_SELECT = 0, KC_FORWARD = 1, KC_SCAN = 2, KC_EXPAND = 3, KC_MOVE_BEGIN = 4, KC_MOVE_END = 5, KC_N = 8 };
 
-void prof_mark(yk_engine* eng, int cls, hipStream_t s) {  // records an event pair boundary
+void prof_mark(yk_engine* eng, int g, int cls, hipStream_t s) {  // records an event pair boundary
     if (!eng->prof) return;
-    if (eng->ev_used + 1 >= (int)eng->ev.size()) {
-        const size_t old = eng->ev.size();
-        eng->ev.resize(old + 4096);
-        eng->ev_cls.resize(old + 4096);
-        for (size_t i = old; i < eng->ev.size(); i++) (void)hipEventCreate(&eng->ev[i]);
+    auto& L = eng->pg[g];
+    if (L.used + 1 >= (int)L.ev.size()) {
+        const size_t old = L.ev.size();
+        L.ev.resize(old + 4096);
+        L.cls.resize(old + 4096);
+        for (size_t i = old; i < L.ev.size(); i++) (void)hipEventCreate(&L.ev[i]);
     }
-    eng->ev_cls[eng->ev_used] = cls;
-    (void)hipEventRecord(eng->ev[eng->ev_used++], s);
+    L.cls[L.used] = cls;
+    (void)hipEventRecord(L.ev[L.used++], s);
 }
 void prof_collect(yk_engine* eng) {  // call after a stream sync
     if (!eng->prof) return;
-    for (int i = 0; i + 1 < eng->ev_used; i++) {
-        const int cls = eng->ev_cls[i];
-        if (cls < 0) continue;
-        float ms = 0.f;
-        if (hipEventElapsedTime(&ms, eng->ev[i], eng->ev[i + 1]) == hipSuccess) {
-            eng->kms[cls] += ms;
-            eng->klaunch[cls] += 1;
+    for (int g = 0; g < eng->ngroups; g++) {
+        auto& L = eng->pg[g];
+        for (int i = 0; i + 1 < L.used; i++) {
+            const int cls = L.cls[i];
+            if (cls < 0) continue;
+            float ms = 0.f;
+            if (hipEventElapsedTime(&ms, L.ev[i], L.ev[i + 1]) == hipSuccess) {
+                eng->kms[cls] += ms;
+                eng->klaunch[cls] += 1;
+            }
         }
+        L.used = 0;
     }
-    eng->ev_used = 0;
+}
+
+// the device view of group g (its game range)
+EngDev group_dev(const yk_engine* eng, int g) {
+    EngDev d = eng->d;
+    const int G = eng->ngroups;
+    auto bound = [&](int k) {
+        const long b = (long)d.E * k / G;
+        return k == G ? d.E : (int)std::min<long>(d.E, (b + GROUP_ALIGN - 1) / GROUP_ALIGN * GROUP_ALIGN);
+    };
+    d.e_lo = bound(g);
+    d.e_hi = bound(g + 1);
+    return d;
+}
+dim3 game_grid(const EngDev& d) {
+    return dim3((unsigned)std::max(1, (d.e_hi - d.e_lo + GAMES_PER_BLOCK - 1) / GAMES_PER_BLOCK));
 }
 
 template <class T>
@@ -1172,26 +1203,39 @@ int check_errors(yk_engine* eng, hipStream_t s) {
     if (err) return YK_ERR_STATE;
     return YK_OK;
 }
-int run_sims(yk_engine* eng, int sims, const uint32_t* env_ids, uint64_t* ctr, hipStream_t s) {
-    EngDev& d = eng->d;
-    const dim3 gb((d.E + GAMES_PER_BLOCK - 1) / GAMES_PER_BLOCK), bb(256);
+// `sims` simulations for every game of groups 0 .. G-1, group g on stream st[g].  Within a group
+// (and a game) the simulations are sequential; group g's forward k waits for group g-1's forward
+// k, which staggers the groups so that a forward runs beside the other groups' expand.
+int run_sims(yk_engine* eng, int G, const hipStream_t* st, int sims, const uint32_t* env_ids, uint64_t* ctr) {
+    const dim3 bb(256);
     if (sims <= 0) return YK_OK;
-    prof_mark(eng, KC_SELECT, s);  // the first descent; later ones run in k_expand_backup's tail
-    hipLaunchKernelGGL(k_select, gb, bb, 0, s, d, env_ids, ctr);
-    YK_LAUNCHED();
-    for (int k = 0; k < sims; k++) {
-        if (d.prior == 0) {
-            prof_mark(eng, KC_FORWARD, s);
-            // predict row = game: no compaction; workgroups without a leaf exit at once
-            int rc = launch_forward(eng->net->dev, d.leaf_state, nullptr, nullptr, nullptr, d.E, eng->logits, eng->vpred, s,
-                                    d.leaf_flag, eng->mlse, true);
-            if (rc) return rc;
-        }
-        prof_mark(eng, KC_EXPAND, s);
-        hipLaunchKernelGGL(k_expand_backup, gb, bb, 0, s, d, k + 1 < sims ? 1 : 0, env_ids, ctr);
+    EngDev dg[YK_MAX_GROUPS];
+    for (int g = 0; g < G; g++) {
+        dg[g] = G == 1 ? eng->d : group_dev(eng, g);
+        prof_mark(eng, g, KC_SELECT, st[g]);  // the first descent; later ones run in k_expand_backup's tail
+        hipLaunchKernelGGL(k_select, game_grid(dg[g]), bb, 0, st[g], dg[g], env_ids, ctr);
         YK_LAUNCHED();
     }
-    prof_mark(eng, -1, s);
+    for (int k = 0; k < sims; k++) {
+        for (int g = 0; g < G; g++) {
+            const EngDev& d = dg[g];
+            if (d.prior == 0) {
+                if (g > 0) YK_HIP(hipStreamWaitEvent(st[g], eng->ev_fwd[g - 1], 0));
+                prof_mark(eng, g, KC_FORWARD, st[g]);
+                // predict row = game: no compaction; workgroups without a leaf exit at once
+                const int lo = d.e_lo;
+                int rc = launch_forward(eng->net->dev, d.leaf_state + lo, nullptr, nullptr, nullptr, d.e_hi - lo,
+                                        eng->logits + (size_t)lo * PI_LD, eng->vpred + lo, st[g], d.leaf_flag + lo,
+                                        eng->mlse + lo, true);
+                if (rc) return rc;
+                if (G > 1) YK_HIP(hipEventRecord(eng->ev_fwd[g], st[g]));
+            }
+            prof_mark(eng, g, KC_EXPAND, st[g]);
+            hipLaunchKernelGGL(k_expand_backup, game_grid(d), bb, 0, st[g], d, k + 1 < sims ? 1 : 0, env_ids, ctr);
+            YK_LAUNCHED();
+        }
+    }
+    for (int g = 0; g < G; g++) prof_mark(eng, g, -1, st[g]);
     return YK_OK;
 }
 }  // namespace
@@ -1245,6 +1289,15 @@ int yk_engine_create(yk_engine_t** out, const yk_engine_config_t* cfg, yk_net_t*
     d.rec_pred = cfg->record_predictions ? 1 : 0;
     d.max_exp = cfg->record_predictions ? std::max(cfg->max_expansions, 1) : 0;
     d.rec_stride = std::max(cfg->record_stride, 1);
+    d.e_lo = 0;
+    d.e_hi = d.E;
+    // game groups: auto = 2 with the net prior at >= 8192 games (the forward of 4096 rows fills the
+    // chip in one round, so there a second group's forward beside the first's expand pays: +3.8 %
+    // measured), else 1 (below that each simulation is latency-bound: F + X per group does not
+    // shrink with the group); each group needs at least one forward row tile
+    int G = cfg->groups > 0 ? cfg->groups : ((cfg->prior == 0 && cfg->n_envs >= 8192) ? 2 : 1);
+    G = std::max(1, std::min({G, YK_MAX_GROUPS, (cfg->n_envs + GROUP_ALIGN - 1) / GROUP_ALIGN}));
+    eng->ngroups = G;
     const size_t R = ((size_t)cfg->n_envs + d.rec_stride - 1) / d.rec_stride;
     const size_t E = (size_t)d.E;
     int rc = YK_OK;
@@ -1306,6 +1359,14 @@ int yk_engine_create(yk_engine_t** out, const yk_engine_config_t* cfg, yk_net_t*
     }
 #undef A
     if (rc == YK_OK && hipHostMalloc((void**)&eng->host_done, sizeof(int32_t)) != hipSuccess) rc = YK_ERR_NOMEM;
+    if (rc == YK_OK && G > 1) {
+        if (hipEventCreateWithFlags(&eng->ev_fork, hipEventDisableTiming) != hipSuccess) rc = YK_ERR_HIP;
+        for (int g = 0; g < G && rc == YK_OK; g++)
+            if (hipStreamCreateWithFlags(&eng->gs[g], hipStreamNonBlocking) != hipSuccess ||
+                hipEventCreateWithFlags(&eng->ev_join[g], hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&eng->ev_fwd[g], hipEventDisableTiming) != hipSuccess)
+                rc = YK_ERR_HIP;
+    }
     if (rc != YK_OK) {
         yk_engine_destroy(eng);
         return rc;
@@ -1331,7 +1392,14 @@ int yk_engine_create(yk_engine_t** out, const yk_engine_config_t* cfg, yk_net_t*
 
 int yk_engine_destroy(yk_engine_t* eng) {
     if (!eng) return YK_OK;
-    for (hipEvent_t e : eng->ev) (void)hipEventDestroy(e);
+    for (auto& L : eng->pg)
+        for (hipEvent_t e : L.ev) (void)hipEventDestroy(e);
+    for (int g = 0; g < YK_MAX_GROUPS; g++) {
+        if (eng->gs[g]) (void)hipStreamDestroy(eng->gs[g]);
+        if (eng->ev_join[g]) (void)hipEventDestroy(eng->ev_join[g]);
+        if (eng->ev_fwd[g]) (void)hipEventDestroy(eng->ev_fwd[g]);
+    }
+    if (eng->ev_fork) (void)hipEventDestroy(eng->ev_fork);
     for (void* p : eng->allocs) (void)hipFree(p);
     if (eng->host_done) (void)hipHostFree(eng->host_done);
     delete eng;
@@ -1346,24 +1414,43 @@ namespace {
 int play_batch(yk_engine* eng, uint64_t seed, uint32_t env_base, hipStream_t s) {
     EngDev& d = eng->d;
     d.seed = seed;
-    const dim3 gb((d.E + GAMES_PER_BLOCK - 1) / GAMES_PER_BLOCK), bb(256);
+    const int G = eng->ngroups;
+    hipStream_t st[YK_MAX_GROUPS];
+    EngDev dg[YK_MAX_GROUPS];
+    for (int g = 0; g < G; g++) {
+        st[g] = G == 1 ? s : eng->gs[g];
+        dg[g] = G == 1 ? d : group_dev(eng, g);
+    }
+    const dim3 bb(256);
     YK_HIP(hipMemsetAsync(d.err, 0, sizeof(uint32_t), s));
     YK_HIP(hipMemsetAsync(d.hidx[0], 0, sizeof(uint32_t) * (size_t)d.E * d.HCAP, s));
     hipLaunchKernelGGL(k_reset, dim3((d.E + 255) / 256), dim3(256), 0, s, d, 1, env_base);
     YK_LAUNCHED();
+    if (G > 1) {  // the group streams start after the reset on the caller's stream
+        YK_HIP(hipEventRecord(eng->ev_fork, s));
+        for (int g = 0; g < G; g++) YK_HIP(hipStreamWaitEvent(st[g], eng->ev_fork, 0));
+    }
     eng->have_records = false;
     for (int move = 0; move < d.M; move++) {
-        prof_mark(eng, KC_MOVE_BEGIN, s);
-        hipLaunchKernelGGL(k_move_begin, gb, bb, 0, s, d, move, 0);
-        YK_LAUNCHED();
+        for (int g = 0; g < G; g++) {
+            prof_mark(eng, g, KC_MOVE_BEGIN, st[g]);
+            hipLaunchKernelGGL(k_move_begin, game_grid(dg[g]), bb, 0, st[g], dg[g], move, 0);
+            YK_LAUNCHED();
+        }
         if (!d.arena || d.arena_agent == YK_PLAYER_MCTS || d.arena_opp == YK_PLAYER_MCTS) {
-            int rc = run_sims(eng, d.sims, d.env_id, d.ctr, s);
+            int rc = run_sims(eng, G, st, d.sims, d.env_id, d.ctr);
             if (rc) return rc;
         }
-        prof_mark(eng, KC_MOVE_END, s);
-        hipLaunchKernelGGL(k_move_end, gb, bb, 0, s, d, move);
-        YK_LAUNCHED();
-        prof_mark(eng, -1, s);
+        for (int g = 0; g < G; g++) {
+            prof_mark(eng, g, KC_MOVE_END, st[g]);
+            hipLaunchKernelGGL(k_move_end, game_grid(dg[g]), bb, 0, st[g], dg[g], move);
+            YK_LAUNCHED();
+            prof_mark(eng, g, -1, st[g]);
+            if (G > 1) {
+                YK_HIP(hipEventRecord(eng->ev_join[g], st[g]));
+                YK_HIP(hipStreamWaitEvent(s, eng->ev_join[g], 0));
+            }
+        }
         hipLaunchKernelGGL(k_count_done, dim3(1), dim3(1024), 0, s, d.done, d.E, eng->done_count);
         YK_LAUNCHED();
         YK_HIP(hipMemcpyAsync(eng->host_done, eng->done_count, sizeof(int32_t), hipMemcpyDeviceToHost, s));
@@ -1438,7 +1525,7 @@ int yk_arena_results(yk_engine_t* eng, double* result, int32_t* totals, int32_t*
 int yk_engine_profile(yk_engine_t* eng, int enable) {
     if (!eng) return YK_ERR_ARG;
     eng->prof = enable != 0;
-    eng->ev_used = 0;
+    for (auto& L : eng->pg) L.used = 0;
     for (int i = 0; i < 8; i++) {
         eng->kms[i] = 0;
         eng->klaunch[i] = 0;
@@ -1483,6 +1570,7 @@ int yk_engine_stats(yk_engine_t* eng, int64_t* out) {
     out[11] = d.ECAP;
     out[12] = d.AE;
     out[13] = d.VCAP;
+    out[14] = eng->ngroups;
     return YK_OK;
 }
 
@@ -1600,13 +1688,13 @@ int yk_mcts_search(yk_engine_t* eng, const yk_state_t* roots, uint64_t seed, con
     hipStream_t s = as_stream(stream);
     EngDev& d = eng->d;
     d.seed = seed;
-    const dim3 gb((d.E + GAMES_PER_BLOCK - 1) / GAMES_PER_BLOCK), bb(256);
+    const dim3 gb = game_grid(d), bb(256);
     YK_HIP(hipMemcpyAsync(d.root, roots, sizeof(yk_state_t) * (size_t)d.E, hipMemcpyDeviceToDevice, s));
     YK_HIP(hipMemsetAsync(d.done, 0, (size_t)d.E, s));
     YK_HIP(hipMemsetAsync(d.err, 0, sizeof(uint32_t), s));
     hipLaunchKernelGGL(k_move_begin, gb, bb, 0, s, d, 0, 1);
     YK_LAUNCHED();
-    int rc = run_sims(eng, sims, env_ids, rng_ctr, s);
+    int rc = run_sims(eng, 1, &s, sims, env_ids, rng_ctr);  // the plugin path: one group on the caller's stream
     if (rc) return rc;
     hipLaunchKernelGGL(k_root_counts, gb, bb, 0, s, d, counts);
     YK_LAUNCHED();

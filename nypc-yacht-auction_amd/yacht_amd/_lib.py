@@ -33,7 +33,8 @@ class YkError(RuntimeError):
 class YkEngineConfig(C.Structure):
     _fields_ = [("n_envs", C.c_int), ("sims", C.c_int), ("cpuct", C.c_double), ("temp_threshold", C.c_int),
                 ("max_moves", C.c_int), ("prior", C.c_int), ("record_predictions", C.c_int),
-                ("max_expansions", C.c_int), ("arena_entries", C.c_int64), ("record_stride", C.c_int)]
+                ("max_expansions", C.c_int), ("arena_entries", C.c_int64), ("record_stride", C.c_int),
+                ("groups", C.c_int)]
 
 
 # name -> argtypes (restype int unless listed in _RESTYPE)

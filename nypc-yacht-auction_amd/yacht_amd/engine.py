@@ -21,7 +21,7 @@ ACTION_SIZE = 3226
 class SelfPlayEngine:
     def __init__(self, n_envs: int, sims: int, cpuct: float = 1.5, temp_threshold: int = 15, net=None,
                  prior: str = "net", max_moves: int = 64, record_predictions: bool = False,
-                 max_expansions: int = 0, arena_entries: int = 0, record_stride: int = 1):
+                 max_expansions: int = 0, arena_entries: int = 0, record_stride: int = 1, groups: int = 0):
         if prior not in ("net", "hash"):
             raise ValueError("prior is 'net' (YachtNNet on MFMA) or 'hash' (deterministic test prior)")
         if prior == "net" and net is None:
@@ -30,7 +30,8 @@ class SelfPlayEngine:
                                   max_moves=max_moves, prior=0 if prior == "net" else 1,
                                   record_predictions=int(record_predictions),
                                   max_expansions=max_expansions or (max_moves * sims + 8),
-                                  arena_entries=arena_entries, record_stride=max(int(record_stride), 1))
+                                  arena_entries=arena_entries, record_stride=max(int(record_stride), 1),
+                                  groups=int(groups))
         self.net = net  # keep the weights alive
         h = C.c_void_p()
         call("yk_engine_create", C.byref(h), C.byref(self.cfg), C.c_void_p(net.handle if net is not None else None))
@@ -92,7 +93,7 @@ class SelfPlayEngine:
         return {k: (float(ms[i]), int(n[i])) for i, k in enumerate(self.KERNEL_CLASSES) if k != "unused"}
 
     STAT_NAMES = ("expansions", "scanned", "moves", "errors", "max_nodes", "max_edges", "max_arena", "vnew",
-                  "path_edges", "sims", "node_cap", "edge_cap", "arena_cap", "visit_cap")
+                  "path_edges", "sims", "node_cap", "edge_cap", "arena_cap", "visit_cap", "groups")
 
     def stats(self) -> dict:
         out = np.zeros(16, dtype=np.int64)

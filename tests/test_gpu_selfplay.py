@@ -232,3 +232,24 @@ def test_game_plugin_methods(Y, golden):
     assert game.getCanonicalForm(s, 1) is s
     assert game.getValidMoves(s, 1).dtype == np.uint8 and game.getValidMoves(s, 1).shape == (3226,)
     assert game.getBoardSize() == (1, 59) and game.getActionSize() == 3226
+
+
+@pytest.mark.parametrize("prior", ["net", "hash"])
+def test_game_groups_do_not_change_results(Y, prior):
+    """The pipelined engine (game groups on their own streams, a group's forward beside another
+    group's expand) plays exactly the games of the single-stream engine, uneven groups included."""
+    _, E, N = Y
+    n, sims, seed, base = 200, 10, 606, 70
+    net = N.YkNet(spec.closed_form_weights(256, 6), 256, 6) if prior == "net" else None
+    out = []
+    for groups in (1, 2, 3):
+        eng = E.SelfPlayEngine(n, sims, 1.5, 15, net=net, prior=prior, max_moves=48, groups=groups)
+        eng.run(seed, base)
+        st = eng.stats()
+        assert st["errors"] == 0 and st["groups"] == groups
+        out.append((eng.records(), st["expansions"]))
+        eng.close()
+    for rec, x in out[1:]:
+        assert x == out[0][1]
+        for k in ("states", "info", "ctr", "values", "final", "n_moves", "visits_off", "visits"):
+            assert np.array_equal(rec[k], out[0][0][k]), k
