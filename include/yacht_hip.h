@@ -152,6 +152,8 @@ typedef struct {
     int groups;             /* game groups, each on its own stream so that one group's forward runs
                                beside another's expand (results do not depend on it); 0 = auto
                                (2 with the net prior at >= 8192 games, else 1), at most 8 */
+    int dual_trees;         /* arena: two trees per game, so MCTS vs MCTS plays two MCTS objects with
+                               their own trees and nets (Coach.py:117-125's pmcts / nmcts) */
 } yk_engine_config_t;
 
 typedef struct yk_engine yk_engine_t;
@@ -215,6 +217,9 @@ int yk_arena(yk_engine_t* eng, uint64_t seed, uint32_t env_base, const int32_t* 
  * (Arena.py:93, from player 1's view: +1 / -1 / +-1e-4 draw), totals[n][2] (player 1, player 2,
  * with bonus), n_moves[n], actions[n][max_moves] (-1 past the end), final_states[n][8],
  * rng_ctr[n] (stream counter at the end).  yk_engine_records also works after yk_arena. */
+/* The opponent seat's net for MCTS vs MCTS arenas of a dual_trees engine (default: the engine's
+ * net).  The gating arena of Coach.learn: yk_arena(agent = previous net's MCTS, opponent = new). */
+int yk_engine_set_opponent_net(yk_engine_t* eng, yk_net_t* net);
 int yk_arena_results(yk_engine_t* eng, double* result, int32_t* totals, int32_t* n_moves, int32_t* actions,
                      uint64_t* final_states, uint64_t* rng_ctr);
 

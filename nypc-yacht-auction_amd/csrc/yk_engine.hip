@@ -61,6 +61,8 @@ struct Edge {             // 16 bytes
 struct EngDev {
     int E, NCAP, HCAP, ECAP, M, VCAP;
     int e_lo, e_hi;        // the game group a per-game launch covers ([0, E) unless pipelined)
+    int T, dual;           // trees: T = E, or 2E with dual trees (one per arena seat: tree e is the
+                           // agent's, tree E + e the opponent's - two MCTS objects, Coach.py:120-125)
     int64_t AE;
     int sims, temp_threshold;
     float c32;
@@ -77,9 +79,9 @@ struct EngDev {
     float* arenaP;
     uint16_t* arenaS;
     uint32_t* arena_top;   // [E]
-    uint8_t* gen;          // [E]
-    uint8_t* cur_round;    // [E]
-    uint4* root_c;         // [E][2] the move's root once a descent found it: {id + 1 (0: not yet), p_off,
+    uint8_t* gen;          // [T]
+    uint8_t* cur_round;    // [T]
+    uint4* root_c;         // [T][2] the move's root once a descent found it: {id + 1 (0: not yet), p_off,
                            //        nvalid, -}, {vinfo lo, hi, -, -}
     // game state
     yk_state_t* board;
@@ -274,9 +276,9 @@ __device__ __forceinline__ uint64_t index_hash(const YkS& s) {
 }
 
 // open-addressing lookup; returns node id or -1.  Uniform across the wave.
-__device__ __forceinline__ int lookup(const EngDev& d, int g, int e, const YkS& s, uint64_t h) {
-    const uint32_t* hx = d.hidx[g] + (long)e * d.HCAP;
-    const NodeRec* nodes = d.nodes[g] + (long)e * d.NCAP;
+__device__ __forceinline__ int lookup(const EngDev& d, int g, int t, const YkS& s, uint64_t h) {  // t: tree
+    const uint32_t* hx = d.hidx[g] + (long)t * d.HCAP;
+    const NodeRec* nodes = d.nodes[g] + (long)t * d.NCAP;
     const uint32_t mask = (uint32_t)d.HCAP - 1;
     uint32_t slot = (uint32_t)h & mask;
     for (int probe = 0; probe < d.HCAP; probe++) {
@@ -288,8 +290,8 @@ __device__ __forceinline__ int lookup(const EngDev& d, int g, int e, const YkS& 
     }
     return -1;
 }
-__device__ __forceinline__ bool insert_index(const EngDev& d, int g, int e, uint64_t h, uint32_t id) {
-    uint32_t* hx = d.hidx[g] + (long)e * d.HCAP;
+__device__ __forceinline__ bool insert_index(const EngDev& d, int g, int t, uint64_t h, uint32_t id) {
+    uint32_t* hx = d.hidx[g] + (long)t * d.HCAP;
     const uint32_t mask = (uint32_t)d.HCAP - 1;
     uint32_t slot = (uint32_t)h & mask;
     for (int probe = 0; probe < d.HCAP; probe++) {
@@ -300,6 +302,12 @@ __device__ __forceinline__ bool insert_index(const EngDev& d, int g, int e, uint
         slot = (slot + 1) & mask;
     }
     return false;
+}
+
+// the tree game e searches with at its current move: its own, or with dual trees the one of the
+// seat to move (the agent's tree e, the opponent's tree E + e)
+__device__ __forceinline__ int tree_of(const EngDev& d, int e) {
+    return (d.dual && d.cur[e] != d.seat[e]) ? e + d.E : e;
 }
 
 // orders this wave's LDS / global accesses across lanes (waves of a block diverge, so no
@@ -353,11 +361,13 @@ __global__ void k_lut(float* sq, float* sqe) {
 __global__ void k_reset(EngDev d, int start_games, uint32_t env_base) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= d.E) return;
-    d.node_count[e] = d.node_count[d.E + e] = 0;
-    d.edge_count[e] = d.edge_count[d.E + e] = 0;
-    d.arena_top[e] = 0;
-    d.gen[e] = 0;
-    d.cur_round[e] = 0;
+    for (int t = e; t < d.T; t += d.E) {  // the game's tree(s)
+        d.node_count[t] = d.node_count[d.T + t] = 0;
+        d.edge_count[t] = d.edge_count[d.T + t] = 0;
+        d.arena_top[t] = 0;
+        d.gen[t] = 0;
+        d.cur_round[t] = 0;
+    }
 #pragma unroll
     for (int k = 0; k < 8; k++) d.gstats[(long)e * 8 + k] = 0;
     if (!start_games) return;
@@ -382,7 +392,8 @@ __global__ __launch_bounds__(256) void k_move_begin(EngDev d, int move, int exte
     const int lane = threadIdx.x & 63;
     const int e = d.e_lo + blockIdx.x * GAMES_PER_BLOCK + (threadIdx.x >> 6);
     if (e >= d.e_hi) return;
-    if (lane == 0) d.root_c[2 * e] = make_uint4(0, 0, 0, 0);  // ids move at a compaction: look the root up afresh
+    const int t = tree_of(d, e);
+    if (lane == 0) d.root_c[2 * t] = make_uint4(0, 0, 0, 0);  // ids move at a compaction: look the root up afresh
     if (!external_root) {
         if (d.done[e]) return;
         const YkS b = ld_state(d.board + e);
@@ -399,23 +410,23 @@ __global__ __launch_bounds__(256) void k_move_begin(EngDev d, int move, int exte
     }
     const YkS r = ld_state(d.root + e);
     const int rr = s_round(r);
-    const int cr = d.cur_round[e];
+    const int cr = d.cur_round[t];
     if (rr == cr) return;
     if (rr < cr) {
         if (lane == 0) atomicOr(d.err, ERR_ROUND);
         return;
     }
     // ---- compaction g -> g ^ 1 (in-place for the arena: survivors only move down)
-    const int g = d.gen[e], h = g ^ 1;
-    uint32_t* hx = d.hidx[h] + (long)e * d.HCAP;
+    const int g = d.gen[t], h = g ^ 1;
+    uint32_t* hx = d.hidx[h] + (long)t * d.HCAP;
     for (int i = lane; i < d.HCAP; i += 64) hx[i] = 0;
-    const NodeRec* src = d.nodes[g] + (long)e * d.NCAP;
-    NodeRec* dst = d.nodes[h] + (long)e * d.NCAP;
-    const Edge* esrc = d.edges[g] + (long)e * d.ECAP;
-    Edge* edst = d.edges[h] + (long)e * d.ECAP;
-    float* P = d.arenaP + (long)e * d.AE;
-    uint16_t* S = d.arenaS + (long)e * d.AE;
-    const uint32_t cnt = d.node_count[g * d.E + e];
+    const NodeRec* src = d.nodes[g] + (long)t * d.NCAP;
+    NodeRec* dst = d.nodes[h] + (long)t * d.NCAP;
+    const Edge* esrc = d.edges[g] + (long)t * d.ECAP;
+    Edge* edst = d.edges[h] + (long)t * d.ECAP;
+    float* P = d.arenaP + (long)t * d.AE;
+    uint16_t* S = d.arenaS + (long)t * d.AE;
+    const uint32_t cnt = d.node_count[g * d.T + t];
     uint32_t nn = 0, ne = 0, top = 0;
     wave_sync();
     for (uint32_t id = 0; id < cnt; id++) {
@@ -449,16 +460,16 @@ __global__ __launch_bounds__(256) void k_move_begin(EngDev d, int move, int exte
         top += (uint32_t)VP;
         if (lane == 0) {
             dst[nn] = rec;
-            insert_index(d, h, e, rec.hash, nn);
+            insert_index(d, h, t, rec.hash, nn);
         }
         nn++;
     }
     if (lane == 0) {
-        d.node_count[h * d.E + e] = nn;
-        d.edge_count[h * d.E + e] = ne;
-        d.arena_top[e] = top;
-        d.gen[e] = (uint8_t)h;
-        d.cur_round[e] = (uint8_t)rr;
+        d.node_count[h * d.T + t] = nn;
+        d.edge_count[h * d.T + t] = ne;
+        d.arena_top[t] = top;
+        d.gen[t] = (uint8_t)h;
+        d.cur_round[t] = (uint8_t)rr;
     }
 }
 
@@ -484,13 +495,14 @@ __device__ __forceinline__ void select_game(const EngDev& d, int e, int lane, co
         }
         return;
     }
-    const int g = d.gen[e];
+    const int t = tree_of(d, e);
+    const int g = d.gen[t];
     YkS s = ld_state(d.root + e);
     Stream rs{d.seed, env_ids[e], ctr_arr[e]};
-    const NodeRec* nodes = d.nodes[g] + (long)e * d.NCAP;
-    const Edge* edges = d.edges[g] + (long)e * d.ECAP;
-    const float* Pbase = d.arenaP + (long)e * d.AE;
-    const uint16_t* Sbase = d.arenaS + (long)e * d.AE;
+    const NodeRec* nodes = d.nodes[g] + (long)t * d.NCAP;
+    const Edge* edges = d.edges[g] + (long)t * d.ECAP;
+    const float* Pbase = d.arenaP + (long)t * d.AE;
+    const uint16_t* Sbase = d.arenaS + (long)t * d.AE;
     uint64_t* path = d.path + (long)e * MAXD;
     int depth = 0;
     uint64_t scanned = 0;
@@ -509,12 +521,12 @@ __device__ __forceinline__ void select_game(const EngDev& d, int e, int lane, co
         // probe and the record's round trip before the prior / slot loads
         uint4 rc0 = make_uint4(0, 0, 0, 0), rc1 = rc0;
         if (depth == 0) {
-            rc0 = d.root_c[2 * e];
-            rc1 = d.root_c[2 * e + 1];
+            rc0 = d.root_c[2 * t];
+            rc1 = d.root_c[2 * t + 1];
         }
         const bool cached = rc0.x != 0;
         const uint64_t hsh = cached ? 0ull : index_hash(s);
-        const int nid = cached ? (int)rc0.x - 1 : lookup(d, g, e, s, hsh);
+        const int nid = cached ? (int)rc0.x - 1 : lookup(d, g, t, s, hsh);
         SEL_ACC(0, t_lv);
         if (nid < 0) {  // leaf: predict (MCTS.py:84-115)
             leaf = 1;
@@ -529,8 +541,8 @@ __device__ __forceinline__ void select_game(const EngDev& d, int e, int lane, co
         const int V = cached ? (int)rc0.z : (int)nd.nvalid;
         const uint64_t vinfo = cached ? ((uint64_t)rc1.x | ((uint64_t)rc1.y << 32)) : nd.vinfo;
         if (depth == 0 && !cached && lane == 0) {
-            d.root_c[2 * e] = make_uint4((uint32_t)nid + 1, p_off, (uint32_t)V, 0);
-            d.root_c[2 * e + 1] = make_uint4((uint32_t)vinfo, (uint32_t)(vinfo >> 32), 0, 0);
+            d.root_c[2 * t] = make_uint4((uint32_t)nid + 1, p_off, (uint32_t)V, 0);
+            d.root_c[2 * t + 1] = make_uint4((uint32_t)vinfo, (uint32_t)(vinfo >> 32), 0, 0);
         }
         if (V == 0) {  // no valid action: MCTS.py:141-147 returns 0 (python int)
             res = PyV{0.0, T_INT};
@@ -629,7 +641,7 @@ __device__ __forceinline__ void select_game(const EngDev& d, int e, int lane, co
     }
     SEL_ACC(3, t_all);
     if (lane == 0) {
-        d.leaf_flag[e] = (uint8_t)leaf;
+        d.leaf_flag[e] = (uint8_t)(leaf ? (t < d.E ? 1 : 2) : 0);  // which net predicts it (dual trees)
         d.path_len[e] = (uint8_t)depth;
         d.res_v[e] = res.v;
         d.res_t[e] = res.t;
@@ -671,7 +683,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(YK_EXPAND_W
 }
 
 __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int lane) {
-    const int g = d.gen[e];
+    const int t = tree_of(d, e);
+    const int g = d.gen[t];
     PyV res{d.res_v[e], d.res_t[e]};
     if (d.leaf_flag[e]) {
         SEL_T0(t_x0);
@@ -803,8 +816,8 @@ __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int l
         SEL_T0(t_x2);
         // ---- allocate + write P over the compact valid set, zero edge slots
         const int VP = pad4(V);
-        const uint32_t off = d.arena_top[e];
-        const uint32_t nid = d.node_count[g * d.E + e];
+        const uint32_t off = d.arena_top[t];
+        const uint32_t nid = d.node_count[g * d.T + t];
         bool ok = true;
         if ((int64_t)off + VP > d.AE) {
             if (lane == 0) atomicOr(d.err, ERR_ARENA);
@@ -815,8 +828,8 @@ __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int l
             ok = false;
         }
         if (ok) {
-            float* P = d.arenaP + (long)e * d.AE + off;
-            uint16_t* S = d.arenaS + (long)e * d.AE + off;
+            float* P = d.arenaP + (long)t * d.AE + off;
+            uint16_t* S = d.arenaS + (long)t * d.AE + off;
             const float inv_fallback = V > 0 ? 1.0f / (float)V : 0.0f;
             // P over the compact valid set (ascending action): Ps / sum, or the uniform fallback
             // (MCTS.py:90-107).  Written in compact order (coalesced), recomputing each prior
@@ -856,10 +869,10 @@ __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int l
                 r.nvalid = (uint32_t)V;
                 r.Ns = 0;
                 r.pad = 0;
-                d.nodes[g][(long)e * d.NCAP + nid] = r;
-                if (!insert_index(d, g, e, ihsh, nid)) atomicOr(d.err, ERR_HASH);
-                d.node_count[g * d.E + e] = nid + 1;
-                d.arena_top[e] = off + (uint32_t)VP;
+                d.nodes[g][(long)t * d.NCAP + nid] = r;
+                if (!insert_index(d, g, t, ihsh, nid)) atomicOr(d.err, ERR_HASH);
+                d.node_count[g * d.T + t] = nid + 1;
+                d.arena_top[t] = off + (uint32_t)VP;
                 uint64_t* gs = d.gstats + (long)e * 8;
                 gs[0] += 1;
                 gs[3] += (uint64_t)V;
@@ -875,10 +888,10 @@ __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int l
     const int depth = d.path_len[e];
     if (depth > 0) {
         const uint64_t* path = d.path + (long)e * MAXD;
-        NodeRec* nodes = d.nodes[g] + (long)e * d.NCAP;
-        Edge* edges = d.edges[g] + (long)e * d.ECAP;
-        uint16_t* Sb = d.arenaS + (long)e * d.AE;
-        const uint32_t ne0 = d.edge_count[g * d.E + e];
+        NodeRec* nodes = d.nodes[g] + (long)t * d.NCAP;
+        Edge* edges = d.edges[g] + (long)t * d.ECAP;
+        uint16_t* Sb = d.arenaS + (long)t * d.AE;
+        const uint32_t ne0 = d.edge_count[g * d.T + t];
         uint64_t pe = 0;
         uint16_t sl = 0;
         if (lane < depth) {
@@ -907,7 +920,7 @@ __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int l
             nodes[(uint32_t)pe].Ns += 1;
         }
         if (lane == 0) {
-            d.edge_count[g * d.E + e] = ne1;
+            d.edge_count[g * d.T + t] = ne1;
             uint64_t* gs = d.gstats + (long)e * 8;
             if (ne1 > gs[5]) gs[5] = ne1;
         }
@@ -923,19 +936,20 @@ __global__ __launch_bounds__(256) void k_move_end(EngDev d, int move) {
     if (e >= d.e_hi) return;
     if (d.done[e]) return;
     uint32_t* vis = vis_all[w];
-    const int g = d.gen[e];
+    const int t = tree_of(d, e);  // before the real step changes cur
+    const int g = d.gen[t];
     const YkS r = ld_state(d.root + e);
     const bool idle = d.idle[e] != 0;
-    const int nid = idle ? -1 : lookup(d, g, e, r, index_hash(r));
+    const int nid = idle ? -1 : lookup(d, g, t, r, index_hash(r));
     int nvis = 0;
     uint32_t root_ns = 0xFFFFFFFFu;
     if (idle) {
     } else if (nid >= 0) {
-        const NodeRec& nd = d.nodes[g][(long)e * d.NCAP + nid];
+        const NodeRec& nd = d.nodes[g][(long)t * d.NCAP + nid];
         root_ns = nd.Ns;
         const VInfo vi = unpack_vinfo(nd.vinfo, nd.nvalid);
-        const uint16_t* S = d.arenaS + (long)e * d.AE + nd.p_off;
-        const Edge* edges = d.edges[g] + (long)e * d.ECAP;
+        const uint16_t* S = d.arenaS + (long)t * d.AE + nd.p_off;
+        const Edge* edges = d.edges[g] + (long)t * d.ECAP;
         for (int j0 = 0; j0 < (int)nd.nvalid; j0 += 64) {
             const int j = j0 + lane;
             const uint16_t sl = j < (int)nd.nvalid ? S[j] : 0;
@@ -1108,6 +1122,7 @@ __global__ void k_count_done(const uint8_t* done, int E, int32_t* out) {
 struct yk_engine {
     yk_engine_config_t cfg;
     yk_net_t* net = nullptr;
+    yk_net_t* net2 = nullptr;  // the opponent seat's net with dual trees (default: net)
     EngDev d{};
     std::vector<void*> allocs;
     float* logits = nullptr;
@@ -1223,11 +1238,15 @@ int run_sims(yk_engine* eng, int G, const hipStream_t* st, int sims, const uint3
                 if (g > 0) YK_HIP(hipStreamWaitEvent(st[g], eng->ev_fwd[g - 1], 0));
                 prof_mark(eng, g, KC_FORWARD, st[g]);
                 // predict row = game: no compaction; workgroups without a leaf exit at once
+                // (dual trees: the agent's leaves on its net, then the opponent's on its own)
                 const int lo = d.e_lo;
-                int rc = launch_forward(eng->net->dev, d.leaf_state + lo, nullptr, nullptr, nullptr, d.e_hi - lo,
-                                        eng->logits + (size_t)lo * PI_LD, eng->vpred + lo, st[g], d.leaf_flag + lo,
-                                        eng->mlse + lo, true);
-                if (rc) return rc;
+                for (int side = 0; side < (d.dual ? 2 : 1); side++) {
+                    const yk_net_t* net = side ? eng->net2 : eng->net;
+                    int rc = launch_forward(net->dev, d.leaf_state + lo, nullptr, nullptr, nullptr, d.e_hi - lo,
+                                            eng->logits + (size_t)lo * PI_LD, eng->vpred + lo, st[g],
+                                            d.leaf_flag + lo, eng->mlse + lo, true, d.dual ? (uint8_t)(1u << side) : 0xFF);
+                    if (rc) return rc;
+                }
                 if (G > 1) YK_HIP(hipEventRecord(eng->ev_fwd[g], st[g]));
             }
             prof_mark(eng, g, KC_EXPAND, st[g]);
@@ -1282,7 +1301,7 @@ int yk_engine_create(yk_engine_t** out, const yk_engine_config_t* cfg, yk_net_t*
         const int64_t worst = (int64_t)d.NCAP * 3024;
         size_t free_b = 0, total_b = 0;
         (void)hipMemGetInfo(&free_b, &total_b);
-        const double need = (double)worst * 6.0 * cfg->n_envs;
+        const double need = (double)worst * 6.0 * cfg->n_envs * (cfg->dual_trees ? 2 : 1);
         d.AE = (need < 0.6 * (double)free_b) ? worst : (int64_t)cfg->sims * 9000 + 65536;
     }
     d.VCAP = 2 * cfg->max_moves * std::max(cfg->sims, 32);
@@ -1291,6 +1310,9 @@ int yk_engine_create(yk_engine_t** out, const yk_engine_config_t* cfg, yk_net_t*
     d.rec_stride = std::max(cfg->record_stride, 1);
     d.e_lo = 0;
     d.e_hi = d.E;
+    d.T = cfg->dual_trees ? 2 * d.E : d.E;
+    d.dual = 0;  // set by yk_arena for MCTS vs MCTS
+    eng->net2 = net;
     // game groups: auto = 2 with the net prior at >= 8192 games (the forward of 4096 rows fills the
     // chip in one round, so there a second group's forward beside the first's expand pays: +3.8 %
     // measured), else 1 (below that each simulation is latency-bound: F + X per group does not
@@ -1299,23 +1321,23 @@ int yk_engine_create(yk_engine_t** out, const yk_engine_config_t* cfg, yk_net_t*
     G = std::max(1, std::min({G, YK_MAX_GROUPS, (cfg->n_envs + GROUP_ALIGN - 1) / GROUP_ALIGN}));
     eng->ngroups = G;
     const size_t R = ((size_t)cfg->n_envs + d.rec_stride - 1) / d.rec_stride;
-    const size_t E = (size_t)d.E;
+    const size_t E = (size_t)d.E, T = (size_t)d.T;
     int rc = YK_OK;
 #define A(p, n) \
     if (rc == YK_OK) rc = dalloc(eng, &(p), (n))
     for (int g = 0; g < 2; g++) {
-        A(d.nodes[g], E * d.NCAP);
-        A(d.hidx[g], E * d.HCAP);
-        A(d.edges[g], E * d.ECAP);
+        A(d.nodes[g], T * d.NCAP);
+        A(d.hidx[g], T * d.HCAP);
+        A(d.edges[g], T * d.ECAP);
     }
-    A(d.node_count, 2 * E);
-    A(d.edge_count, 2 * E);
-    A(d.arenaP, E * (size_t)d.AE);
-    A(d.arenaS, E * (size_t)d.AE);
-    A(d.arena_top, E);
-    A(d.gen, E);
-    A(d.cur_round, E);
-    A(d.root_c, 2 * E);
+    A(d.node_count, 2 * T);
+    A(d.edge_count, 2 * T);
+    A(d.arenaP, T * (size_t)d.AE);
+    A(d.arenaS, T * (size_t)d.AE);
+    A(d.arena_top, T);
+    A(d.gen, T);
+    A(d.cur_round, T);
+    A(d.root_c, 2 * T);
     A(d.board, E);
     A(d.cur, E);
     A(d.ctr, E);
@@ -1423,7 +1445,7 @@ int play_batch(yk_engine* eng, uint64_t seed, uint32_t env_base, hipStream_t s) 
     }
     const dim3 bb(256);
     YK_HIP(hipMemsetAsync(d.err, 0, sizeof(uint32_t), s));
-    YK_HIP(hipMemsetAsync(d.hidx[0], 0, sizeof(uint32_t) * (size_t)d.E * d.HCAP, s));
+    YK_HIP(hipMemsetAsync(d.hidx[0], 0, sizeof(uint32_t) * (size_t)d.T * d.HCAP, s));
     hipLaunchKernelGGL(k_reset, dim3((d.E + 255) / 256), dim3(256), 0, s, d, 1, env_base);
     YK_LAUNCHED();
     if (G > 1) {  // the group streams start after the reset on the caller's stream
@@ -1487,11 +1509,22 @@ int yk_arena(yk_engine_t* eng, uint64_t seed, uint32_t env_base, const int32_t* 
     d.arena = 1;
     d.arena_agent = agent;
     d.arena_opp = opponent;
+    // two MCTS players each keep their own tree (and net) when the engine has dual trees
+    d.dual = (d.T == 2 * d.E && agent == YK_PLAYER_MCTS && opponent == YK_PLAYER_MCTS) ? 1 : 0;
     eng->have_arena = false;
     const int rc = play_batch(eng, seed, env_base, s);
     d.arena = 0;
+    d.dual = 0;
     eng->have_arena = rc == YK_OK || rc == YK_ERR_STATE;
     return rc;
+}
+
+int yk_engine_set_opponent_net(yk_engine_t* eng, yk_net_t* net) {
+    if (!eng || !net) return YK_ERR_ARG;
+    if (eng->d.T != 2 * eng->d.E || eng->d.prior != 0) return YK_ERR_ARG;  // needs dual trees and the net prior
+    if (net->dev.H != eng->net->dev.H) return YK_ERR_ARG;
+    eng->net2 = net;
+    return YK_OK;
 }
 
 int yk_arena_results(yk_engine_t* eng, double* result, int32_t* totals, int32_t* n_moves, int32_t* actions,
@@ -1674,7 +1707,7 @@ int yk_mcts_reset(yk_engine_t* eng) {
     if (!eng) return YK_ERR_ARG;
     EngDev& d = eng->d;
     YK_HIP(hipMemset(d.err, 0, sizeof(uint32_t)));
-    YK_HIP(hipMemset(d.hidx[0], 0, sizeof(uint32_t) * (size_t)d.E * d.HCAP));
+    YK_HIP(hipMemset(d.hidx[0], 0, sizeof(uint32_t) * (size_t)d.T * d.HCAP));
     YK_HIP(hipMemset(d.done, 0, (size_t)d.E));
     hipLaunchKernelGGL(k_reset, dim3((d.E + 255) / 256), dim3(256), 0, 0, d, 0, 0u);
     YK_LAUNCHED();

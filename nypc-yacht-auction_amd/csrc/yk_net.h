@@ -40,7 +40,8 @@ constexpr int vstat_size(int H) { return vs_bpi(H) + PI_LD; }
 // logits, so that exp(log_softmax(x))[a] = exp(x[a] - m - l) needs only the logits it is asked for.
 int launch_forward(const NetDev& net, const yk_state_t* states, const float* x, const int32_t* rows,
                    const int32_t* count, int n, float* logits, float* v, hipStream_t stream,
-                   const uint8_t* active = nullptr, float2* mlse = nullptr, bool valid_only = false);
+                   const uint8_t* active = nullptr, float2* mlse = nullptr, bool valid_only = false,
+                   uint8_t want = 0xFF);  // a row is predicted iff !active || (active[row] & want)
 // pi[n][3226] = exp(log_softmax(logits[:, :3226])) = exp(logits - m - l), (m, l) = mlse[row]
 int launch_softmax(const float* logits, const float2* mlse, float* pi, int n, hipStream_t stream);
 

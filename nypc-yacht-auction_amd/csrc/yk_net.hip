@@ -372,7 +372,7 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
                                                  const int32_t* __restrict__ count, int n,
                                                  float* __restrict__ logits, float* __restrict__ vout,
                                                  const uint8_t* __restrict__ active, float2* __restrict__ mlse,
-                                                 int valid_only) {
+                                                 int valid_only, uint32_t want) {
     constexpr int LD = (H > 128 ? H : 128) + 4;      // X also holds the 128-wide v_head hidden
     constexpr int SA = H + 8;                        // plane row stride (halves): conflict-free b128 reads
     constexpr int NT = H >= 16 * WAVES ? H / (16 * WAVES) : 1;  // 16-col tiles per wave, H-wide layers
@@ -410,10 +410,10 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
             const uint4 a4 = *reinterpret_cast<const uint4*>(active + row0);
             const uint32_t w4[4] = {a4.x, a4.y, a4.z, a4.w};
 #pragma unroll
-            for (int i = 0; i < ROWS; i++) amask |= (((w4[i >> 2] >> (8 * (i & 3))) & 0xFFu) != 0 ? 1u : 0u) << i;
+            for (int i = 0; i < ROWS; i++) amask |= (((w4[i >> 2] >> (8 * (i & 3))) & want) != 0 ? 1u : 0u) << i;
         } else {
 #pragma unroll
-            for (int i = 0; i < ROWS; i++) amask |= (row0 + i < n && active[row0 + i] ? 1u : 0u) << i;
+            for (int i = 0; i < ROWS; i++) amask |= (row0 + i < n && (active[row0 + i] & want) ? 1u : 0u) << i;
         }
         if (!amask) return;
     }
@@ -776,11 +776,11 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
         const float* wv2 = VS + VS_BV1 * H + 128;
         float s = silu(X[r * LD + 2 * lane]) * wv2[2 * lane] + silu(X[r * LD + 2 * lane + 1]) * wv2[2 * lane + 1];
         s = wave_sum(s);
-        if (lane == 0 && row < n) vout[row] = tanhf(s + net.b_v2[0]);
+        if (lane == 0 && row < n && ((amask >> r) & 1u)) vout[row] = tanhf(s + net.b_v2[0]);  // active rows only
     }
     if (mlse) {
         lds_barrier();
-        if (tid < ROWS && row0 + tid < n) {  // (max, log sum exp(x - max)) of the row: log_softmax = x - m - l
+        if (tid < ROWS && row0 + tid < n && ((amask >> tid) & 1u)) {  // (max, log sum exp(x - max)) of the row
             float m = -INFINITY, sm = 0.f;
 #pragma unroll
             for (int w = 0; w < WAVES; w++) stat_merge(m, sm, SS[w * ROWS + tid].x, SS[w * ROWS + tid].y);
@@ -861,15 +861,15 @@ namespace yk {
 
 int launch_forward(const NetDev& net, const yk_state_t* states, const float* x, const int32_t* rows,
                    const int32_t* count, int n, float* logits, float* v, hipStream_t stream, const uint8_t* active,
-                   float2* mlse, bool valid_only) {
+                   float2* mlse, bool valid_only, uint8_t want) {
     if (n <= 0) return YK_OK;
     const dim3 grid((n + ROWS - 1) / ROWS), block(NTHR);
     const int vo = valid_only ? 1 : 0;
     switch (net.H) {
-        case 64: hipLaunchKernelGGL(k_forward<64>, grid, block, 0, stream, net, states, x, rows, count, n, logits, v, active, mlse, vo); break;
-        case 128: hipLaunchKernelGGL(k_forward<128>, grid, block, 0, stream, net, states, x, rows, count, n, logits, v, active, mlse, vo); break;
-        case 256: hipLaunchKernelGGL(k_forward<256>, grid, block, 0, stream, net, states, x, rows, count, n, logits, v, active, mlse, vo); break;
-        case 512: hipLaunchKernelGGL(k_forward<512>, grid, block, 0, stream, net, states, x, rows, count, n, logits, v, active, mlse, vo); break;
+        case 64: hipLaunchKernelGGL(k_forward<64>, grid, block, 0, stream, net, states, x, rows, count, n, logits, v, active, mlse, vo, (uint32_t)want); break;
+        case 128: hipLaunchKernelGGL(k_forward<128>, grid, block, 0, stream, net, states, x, rows, count, n, logits, v, active, mlse, vo, (uint32_t)want); break;
+        case 256: hipLaunchKernelGGL(k_forward<256>, grid, block, 0, stream, net, states, x, rows, count, n, logits, v, active, mlse, vo, (uint32_t)want); break;
+        case 512: hipLaunchKernelGGL(k_forward<512>, grid, block, 0, stream, net, states, x, rows, count, n, logits, v, active, mlse, vo, (uint32_t)want); break;
         default: return YK_ERR_ARG;
     }
 #ifdef YK_TILESTAT

@@ -34,7 +34,7 @@ class YkEngineConfig(C.Structure):
     _fields_ = [("n_envs", C.c_int), ("sims", C.c_int), ("cpuct", C.c_double), ("temp_threshold", C.c_int),
                 ("max_moves", C.c_int), ("prior", C.c_int), ("record_predictions", C.c_int),
                 ("max_expansions", C.c_int), ("arena_entries", C.c_int64), ("record_stride", C.c_int),
-                ("groups", C.c_int)]
+                ("groups", C.c_int), ("dual_trees", C.c_int)]
 
 
 # name -> argtypes (restype int unless listed in _RESTYPE)
@@ -78,6 +78,7 @@ SIGNATURES = {
     "yk_trainer_set": [P, I, P, C.c_int64],
     "yk_trainer_step_count": [P],
     "yk_arena_results": [P, P, P, P, P, P, P],
+    "yk_engine_set_opponent_net": [P, P],
     "yk_engine_stats": [P, P],
     "yk_engine_profile": [P, I],
     "yk_engine_kernel_times": [P, P, P],

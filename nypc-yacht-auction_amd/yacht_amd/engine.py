@@ -21,7 +21,8 @@ ACTION_SIZE = 3226
 class SelfPlayEngine:
     def __init__(self, n_envs: int, sims: int, cpuct: float = 1.5, temp_threshold: int = 15, net=None,
                  prior: str = "net", max_moves: int = 64, record_predictions: bool = False,
-                 max_expansions: int = 0, arena_entries: int = 0, record_stride: int = 1, groups: int = 0):
+                 max_expansions: int = 0, arena_entries: int = 0, record_stride: int = 1, groups: int = 0,
+                 dual_trees: bool = False, opponent_net=None):
         if prior not in ("net", "hash"):
             raise ValueError("prior is 'net' (YachtNNet on MFMA) or 'hash' (deterministic test prior)")
         if prior == "net" and net is None:
@@ -31,12 +32,16 @@ class SelfPlayEngine:
                                   record_predictions=int(record_predictions),
                                   max_expansions=max_expansions or (max_moves * sims + 8),
                                   arena_entries=arena_entries, record_stride=max(int(record_stride), 1),
-                                  groups=int(groups))
+                                  groups=int(groups), dual_trees=int(bool(dual_trees)))
         self.net = net  # keep the weights alive
         h = C.c_void_p()
         call("yk_engine_create", C.byref(h), C.byref(self.cfg), C.c_void_p(net.handle if net is not None else None))
         self.handle = h.value
         self.n_envs, self.sims, self.max_moves = n_envs, sims, max_moves
+        self.opponent_net = opponent_net
+        if opponent_net is not None:
+            # MCTS vs MCTS with two nets, each seat its own tree (the gating arena, Coach.py:117-139)
+            call("yk_engine_set_opponent_net", self.handle, C.c_void_p(opponent_net.handle))
 
     ERROR_BITS = {1: "node pool", 2: "edge pool", 4: "arena", 8: "search depth", 16: "transition status",
                   32: "root round went backwards", 64: "visit records", 128: "move cap", 256: "zero visit counts",

@@ -53,6 +53,10 @@ def lib():
                                   C.c_int, C.c_int,
                                   C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                   C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+        _lib.or_arena_dual.restype = C.c_int
+        _lib.or_arena_dual.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_int, C.c_double, C.c_int,
+                                       C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
+                                       C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
         for name in ("or_step", "or_valid", "or_ended", "or_canonical", "or_featurize", "or_score_table",
                      "or_score_dice", "or_key_hash_batch", "or_hash_prior", "or_init_board", "or_draws",
                      "or_greedy_heuristic", "or_greedy_play"):
@@ -315,4 +319,29 @@ def arena(envs, agent_seat, seed, sims, cpuct=1.5, mode=MODE_HASH, net=None, rep
                           C.c_double(cpuct), max_moves, mode,
                           C.c_void_p(net.h if net is not None else None), rpi, rv, rn, _p(result), _p(totals), _p(actions),
                           _p(stats), _p(final), threads)
+    return dict(result=result, totals=totals, actions=actions, stats=stats, final=final, nerr=nerr)
+
+
+def arena_dual(envs, agent_seat, seed, sims, cpuct=1.5, mode=MODE_HASH, net=None, net2=None, replay=None,
+               shared=False, max_moves=64, threads=1):
+    """The gating arena of Coach.learn (Coach.py:117-139): MCTS(net, temp 0) in seat agent_seat[i] vs
+    MCTS(net2, temp 0), each seat with its own tree.  shared=True keeps both trees across the games,
+    played in order, as the reference's pmcts / nmcts live across Arena.playGames; False: fresh trees
+    per game.  replay: one (pi, v) log per game holding both seats' expansions in call order."""
+    e = np.ascontiguousarray(np.asarray(envs, dtype=np.uint32).reshape(-1))
+    n = len(e)
+    seat = np.ascontiguousarray(np.broadcast_to(np.asarray(agent_seat, dtype=np.int32), (n,)))
+    result = np.zeros(n, dtype=np.float64)
+    totals = np.zeros((n, 2), dtype=np.int32)
+    actions = np.zeros((n, max_moves), dtype=np.int32)
+    stats = np.zeros((n, 8), dtype=np.int64)
+    final = np.zeros((n, 8), dtype=np.uint64)
+    rpi = rv = rn = None
+    keep = []
+    if mode == MODE_REPLAY:
+        rpi, rv, rn = _replay_ptrs(replay, keep)
+    nerr = lib().or_arena_dual(n, _p(e), _p(seat), C.c_uint64(seed), sims, C.c_double(cpuct), max_moves, mode,
+                               C.c_void_p(net.h if net is not None else None),
+                               C.c_void_p(net2.h if net2 is not None else None), rpi, rv, rn, int(bool(shared)),
+                               _p(result), _p(totals), _p(actions), _p(stats), _p(final), threads)
     return dict(result=result, totals=totals, actions=actions, stats=stats, final=final, nerr=nerr)

@@ -968,15 +968,26 @@ void or_greedy_play(const uint64_t* states, uint64_t seed, const uint32_t* envs,
  * MCTS tree for the whole game.  out: result = curPlayer * getGameEnded (Arena.py:93),
  * totals, moves, actions[max_moves], final state, stream counter. */
 enum { PK_MCTS = 0, PK_RANDOM = 1, PK_GREEDY = 2 };
-static int run_arena(const ep_cfg_t* cfg, pred_t* pr, uint64_t seed, uint32_t env, int agent_seat, int agent_kind,
-                     int opp_kind, double* result, int32_t* totals, int32_t* actions, int64_t* stats,
-                     uint64_t* final_state) {
+/* One Arena.playGame (Arena.py:30-93).  Two MCTS seats share one tree unless `dual`, where the
+ * agent's seat searches with trees[0] and the opponent's with trees[1], each with its own
+ * predictor (Coach.py:120-125: pmcts and nmcts are two MCTS objects).  `trees` may carry state
+ * in from earlier games (the reference's MCTS objects live across a playGames call); NULL: fresh
+ * trees for this game. */
+static int run_arena(const ep_cfg_t* cfg, pred_t* pr, pred_t* pr2, uint64_t seed, uint32_t env, int agent_seat,
+                     int agent_kind, int opp_kind, int dual, mcts_t* trees, double* result, int32_t* totals,
+                     int32_t* actions, int64_t* stats, uint64_t* final_state) {
     init_comb();
     stream_t rs = {seed, env, 0};
-    mcts_t m;
-    memset(&m, 0, sizeof(m));
-    tree_init(&m.tree);
-    m.pred = pr; m.rs = &rs; m.c32 = (float)cfg->cpuct;
+    mcts_t own[2];
+    mcts_t* m = trees ? trees : own;
+    if (!trees) {
+        memset(own, 0, sizeof(own));
+        tree_init(&own[0].tree);
+        tree_init(&own[1].tree);
+    }
+    m[0].pred = pr; m[1].pred = dual ? pr2 : pr;
+    for (int k = 0; k < 2; k++) { m[k].rs = &rs; m[k].c32 = (float)cfg->cpuct; }
+    const long calls0 = pr->calls + (pr2 && pr2 != pr ? pr2->calls : 0);
     st_t board;
     memset(&board, 0, sizeof(board));
     board.round = 1; board.phase = 0;
@@ -991,12 +1002,13 @@ static int run_arena(const ep_cfg_t* cfg, pred_t* pr, uint64_t seed, uint32_t en
         int action = 0;
         const int kind = cur == agent_seat ? agent_kind : opp_kind;
         if (kind == PK_MCTS) {
-            for (int i = 0; i < cfg->sims; i++) search(&m, &canon);
-            if (m.error || pr->error) { err = m.error ? m.error : 2; break; }
+            mcts_t* mt = &m[dual && cur != agent_seat ? 1 : 0];
+            for (int i = 0; i < cfg->sims; i++) search(mt, &canon);
+            if (mt->error || mt->pred->error) { err = mt->error ? mt->error : 2; break; }
             uint64_t key[8];
             pack(&canon, key);
-            int id = tree_find(&m.tree, key, or_key_hash(key));
-            const node_t* nd = id >= 0 ? &m.tree.nodes[id] : NULL;
+            int id = tree_find(&mt->tree, key, or_key_hash(key));
+            const node_t* nd = id >= 0 ? &mt->tree.nodes[id] : NULL;
             int mx = 0, nb = 0;
             for (int a = 0; a < ASIZE; a++) {
                 int c = (nd && nd->eidx && nd->eidx[a] >= 0) ? nd->e[nd->eidx[a]].N : 0;
@@ -1027,12 +1039,16 @@ static int run_arena(const ep_cfg_t* cfg, pred_t* pr, uint64_t seed, uint32_t en
     }
     *result = (double)cur * game_ended(&board, cur, totals);
     if (stats) {
-        stats[0] = it; stats[1] = pr->calls; stats[2] = m.tree.n; stats[3] = m.scanned;
+        stats[0] = it; stats[1] = pr->calls + (pr2 && pr2 != pr ? pr2->calls : 0) - calls0;
+        stats[2] = m[0].tree.n + (dual ? m[1].tree.n : 0); stats[3] = m[0].scanned + m[1].scanned;
         stats[4] = (int64_t)rs.ctr; stats[5] = err;
     }
     if (final_state) pack(&board, final_state);
     free(valid);
-    tree_free(&m.tree);
+    if (!trees) {
+        tree_free(&own[0].tree);
+        tree_free(&own[1].tree);
+    }
     return err;
 }
 
@@ -1186,9 +1202,60 @@ int or_arena(int n, const uint32_t* envs, const int32_t* agent_seat, int agent_k
         pr.mode = mode;
         pr.net = (const net_t*)net;
         if (mode == 2) { pr.rpi = rpi[i]; pr.rv = rv[i]; pr.rn = rn[i]; }
-        if (run_arena(&cfg, &pr, seed, envs[i], agent_seat[i], agent_kind, opp_kind, result + i, totals + 2 * i,
-                      actions ? actions + (size_t)max_moves * i : NULL, stats ? stats + 8 * i : NULL,
+        if (run_arena(&cfg, &pr, NULL, seed, envs[i], agent_seat[i], agent_kind, opp_kind, 0, NULL, result + i,
+                      totals + 2 * i, actions ? actions + (size_t)max_moves * i : NULL, stats ? stats + 8 * i : NULL,
                       final_state ? final_state + 8 * i : NULL))
+            nerr++;
+    }
+    return nerr;
+}
+
+/* The gating arena of Coach.learn (Coach.py:117-139): MCTS (temp 0, net) in seat agent_seat[i]
+ * against MCTS (temp 0, net2), each with its own tree.  mode 2 replays ONE prediction log per game
+ * (both seats' expansions in call order).  shared = 1 plays the n games in order with the two
+ * trees kept across games, as the reference's pmcts / nmcts live across playGames (single thread);
+ * 0: fresh trees per game (the engine's semantics, parallel). */
+int or_arena_dual(int n, const uint32_t* envs, const int32_t* agent_seat, uint64_t seed, int sims, double cpuct,
+                  int max_moves, int mode, void* net, void* net2, const float* const* rpi, const float* const* rv,
+                  const int64_t* rn, int shared, double* result, int32_t* totals, int32_t* actions, int64_t* stats,
+                  uint64_t* final_state, int threads) {
+    init_comb();
+    ep_cfg_t cfg = {sims, 0, max_moves, cpuct, mode};
+    int nerr = 0;
+    if (shared) {
+        mcts_t m[2];
+        memset(m, 0, sizeof(m));
+        tree_init(&m[0].tree);
+        tree_init(&m[1].tree);
+        pred_t pr, pr2;
+        memset(&pr, 0, sizeof(pr));
+        memset(&pr2, 0, sizeof(pr2));
+        pr.mode = pr2.mode = mode;
+        pr.net = (const net_t*)net;
+        pr2.net = (const net_t*)(net2 ? net2 : net);
+        for (int i = 0; i < n; i++) {
+            if (mode == 2) { pr.rpi = rpi[i]; pr.rv = rv[i]; pr.rn = rn[i]; pr.ri = 0; }
+            if (run_arena(&cfg, &pr, mode == 2 ? &pr : &pr2, seed, envs[i], agent_seat[i], PK_MCTS, PK_MCTS, 1, m,
+                          result + i, totals + 2 * i, actions ? actions + (size_t)max_moves * i : NULL,
+                          stats ? stats + 8 * i : NULL, final_state ? final_state + 8 * i : NULL))
+                nerr++;
+        }
+        tree_free(&m[0].tree);
+        tree_free(&m[1].tree);
+        return nerr;
+    }
+#pragma omp parallel for schedule(dynamic, 1) num_threads(threads > 0 ? threads : 1) reduction(+ : nerr)
+    for (int i = 0; i < n; i++) {
+        pred_t pr, pr2;
+        memset(&pr, 0, sizeof(pr));
+        memset(&pr2, 0, sizeof(pr2));
+        pr.mode = pr2.mode = mode;
+        pr.net = (const net_t*)net;
+        pr2.net = (const net_t*)(net2 ? net2 : net);
+        if (mode == 2) { pr.rpi = rpi[i]; pr.rv = rv[i]; pr.rn = rn[i]; }
+        if (run_arena(&cfg, &pr, mode == 2 ? &pr : &pr2, seed, envs[i], agent_seat[i], PK_MCTS, PK_MCTS, 1, NULL,
+                      result + i, totals + 2 * i, actions ? actions + (size_t)max_moves * i : NULL,
+                      stats ? stats + 8 * i : NULL, final_state ? final_state + 8 * i : NULL))
             nerr++;
     }
     return nerr;

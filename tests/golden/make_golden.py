@@ -368,6 +368,79 @@ def make_arena(seed=777, n=12, sims=10, agent_kind="mcts", opp_kind="random", en
                 expansions=np.array([g["expansions"] for g in rows], dtype=np.int64))
 
 
+def make_gating_arena(seed=881, n=12, sims=10, env0=900, cpuct=1.5):
+    """The gating arena of the reference's Coach.learn (Coach.py:117-139): pmcts and nmcts - two
+    MCTS objects, each with its own tree - built once and kept across all games of
+    Arena.playGames(n) (pmcts is player 1 for the first n/2 games, then the seats swap,
+    Arena.py:95-130).  Both use the hash prior.  Game i draws from stream (seed, env0 + i).  The
+    same games are also played with fresh MCTS objects per game, so the fixture shows whether
+    the shared trees change anything."""
+    from utils import dotdict
+    from Arena import Arena
+    from MCTS import MCTS
+    import logging
+    logging.getLogger("Arena").setLevel(logging.WARNING)
+    args = dotdict(dict(numMCTSSims=sims, cpuct=cpuct))
+
+    def play(shared):
+        game = YachtGame()
+        pnet, nnet = HashNet(game), HashNet(game)
+        trees = [MCTS(game, pnet, args), MCTS(game, nnet, args)]
+        in_search = [False]
+        acts, rows = [], []
+        orig_next = game.getNextState
+
+        def nxt(board, player, action):
+            if not in_search[0]:
+                acts[-1].append(int(action))
+            return orig_next(board, player, action)
+        game.getNextState = nxt
+
+        def player(k):
+            def f(x):
+                in_search[0] = True
+                try:
+                    return int(np.argmax(trees[k].getActionProb(x, temp=0)))
+                finally:
+                    in_search[0] = False
+            return f
+        arena = Arena(player(0), player(1), game)
+        orig_play = arena.playGame
+        i = [0]
+
+        def play_game(verbose=False):
+            if not shared:
+                trees[0] = MCTS(game, pnet, args)
+                trees[1] = MCTS(game, nnet, args)
+            set_stream(seed, env0 + i[0])
+            acts.append([])
+            c0 = pnet.calls + nnet.calls
+            r = orig_play(verbose=verbose)
+            rows.append(dict(result=float(r), ctr_end=_STREAM[0].ctr, expansions=pnet.calls + nnet.calls - c0))
+            i[0] += 1
+            return r
+        arena.playGame = play_game
+        pw, nw, dr = arena.playGames(n)
+        return rows, acts, (pw, nw, dr), (len(trees[0].Ps), len(trees[1].Ps))
+
+    out = {}
+    for tag, shared in (("shared", True), ("fresh", False)):
+        rows, acts, wins, ntree = play(shared)
+        M = max(len(a) for a in acts)
+        A = np.full((n, M), -1, dtype=np.int32)
+        for k, a in enumerate(acts):
+            A[k, :len(a)] = a
+        out.update({f"{tag}_result": np.array([r["result"] for r in rows], dtype=np.float64),
+                    f"{tag}_actions": A, f"{tag}_n_moves": np.array([len(a) for a in acts], dtype=np.int32),
+                    f"{tag}_ctr_end": np.array([r["ctr_end"] for r in rows], dtype=np.int64),
+                    f"{tag}_expansions": np.array([r["expansions"] for r in rows], dtype=np.int64),
+                    f"{tag}_wins": np.array(wins, dtype=np.int64), f"{tag}_tree_sizes": np.array(ntree, dtype=np.int64)})
+    seats = np.array([1] * (n // 2) + [-1] * (n - n // 2), dtype=np.int32)
+    out.update(seed=np.uint64(seed), sims=np.int64(sims), cpuct=np.float64(cpuct),
+               env=np.arange(env0, env0 + n, dtype=np.int64), seat=seats)
+    return out
+
+
 def to_ref_state(w):
     """8 x u64 -> the reference's YachtState (fields per YachtGame.py:115-147)."""
     d = spec.unpack_words(w)
@@ -617,6 +690,10 @@ def main():
         np.savez_compressed(os.path.join(HERE, "bot_transcripts.npz"), **make_bot())
         print(f"bot fixture in {time.time() - t0:.1f}s")
         return
+    if len(sys.argv) > 1 and sys.argv[1] == "gating":
+        np.savez_compressed(os.path.join(HERE, "arena_gating_hash.npz"), **make_gating_arena())
+        print(f"gating arena fixture in {time.time() - t0:.1f}s")
+        return
     if len(sys.argv) > 1 and sys.argv[1] == "arena":
         np.savez_compressed(os.path.join(HERE, "arena_hash.npz"), **make_arena())
         make_players()
@@ -649,6 +726,7 @@ def main():
     np.savez_compressed(os.path.join(HERE, "episodes_hash.npz"), **pack_episodes(eps))
     np.savez_compressed(os.path.join(HERE, "arena_hash.npz"), **make_arena())
     make_players()
+    np.savez_compressed(os.path.join(HERE, "arena_gating_hash.npz"), **make_gating_arena())
     make_examples_pickle()
     np.savez_compressed(os.path.join(HERE, "train_h64_b1.npz"), **make_train())
     np.savez_compressed(os.path.join(HERE, "bot_transcripts.npz"), **make_bot())

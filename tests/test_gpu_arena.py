@@ -246,3 +246,53 @@ def test_sequential_arena_with_greedy_plugin(Y, golden):
     one, two, draws = MCTSArena(YachtGame(seed=5, env_id=0), None, dotdict(), agent="greedy",
                                 opponent="random").playGames(200)
     assert one + two + draws == 200 and one > 180  # the greedy player beats random almost always
+
+
+def test_gating_arena_matches_reference_games(Y, golden):
+    """The gating arena of Coach.learn (Coach.py:117-139) on the engine's dual trees: the REFERENCE
+    played these games with pmcts / nmcts kept across all games of Arena.playGames (and again with
+    fresh MCTS objects per game: identical, tests/golden/arena_gating_hash.npz); the engine (one tree
+    per seat per game) reproduces results, actions, counters and expansions bit for bit."""
+    E, _ = Y
+    g = golden("arena_gating_hash.npz")
+    n = len(g["env"])
+    for k in ("result", "actions", "ctr_end", "expansions"):  # the reference: shared trees change nothing here
+        assert np.array_equal(g["shared_" + k], g["fresh_" + k]), k
+    eng = E.SelfPlayEngine(n, int(g["sims"]), float(g["cpuct"]), 0, prior="hash", max_moves=48, dual_trees=True)
+    eng.arena(g["seat"], int(g["seed"]), int(g["env"][0]), agent="mcts", opponent="mcts")
+    r = eng.arena_results()
+    assert np.array_equal(r["result"], g["shared_result"])
+    assert np.array_equal(r["n_moves"], g["shared_n_moves"])
+    assert np.array_equal(r["ctr"], g["shared_ctr_end"].astype(np.uint64))
+    for i, m in enumerate(g["shared_n_moves"]):
+        assert np.array_equal(r["actions"][i, :m], g["shared_actions"][i, :m]), i
+    assert eng.stats()["expansions"] == int(g["shared_expansions"].sum())
+
+
+def test_gating_arena_two_nets_replayed_by_oracle(Y):
+    """Two different nets, one per seat, each its own tree: the oracle (dual trees) replays the
+    engine's recorded predictions and ends every game identically; every recorded value is the
+    value of one of the two nets at that leaf, and both nets are used."""
+    from helpers import torch_predict
+    E, N = Y
+    n, sims, seed, base = 256, 10, 515, 7000
+    sd_a = spec.closed_form_weights(256, 6)
+    sd_b = {k: (np.asarray(v, dtype=np.float32) * np.float32(0.9) if k.endswith("weight") else v)
+            for k, v in sd_a.items()}
+    seats = np.where(np.arange(n) < n // 2, 1, -1).astype(np.int32)
+    eng = E.SelfPlayEngine(n, sims, 1.5, 0, net=N.YkNet(sd_a, 256, 6), opponent_net=N.YkNet(sd_b, 256, 6),
+                           max_moves=48, record_predictions=True, max_expansions=48 * sims + 16, dual_trees=True)
+    eng.arena(seats, seed, base, agent="mcts", opponent="mcts")
+    r = eng.arena_results()
+    pi, v, cnt, leaves = eng.predictions(leaves=True)
+    o = O.arena_dual(np.arange(base, base + n), seats, seed, sims, 1.5, O.MODE_REPLAY,
+                     replay=[(pi[e, :cnt[e]], v[e, :cnt[e]]) for e in range(n)], max_moves=48, threads=16)
+    assert np.array_equal(o["stats"][:, 1], cnt)
+    _compare_arena(r, o, n)
+    S = np.concatenate([leaves[e, :cnt[e]:7] for e in range(n)])
+    V = np.concatenate([v[e, :cnt[e]:7] for e in range(n)])
+    import torch
+    _, va = torch_predict(sd_a, 256, 6, S, torch.float64)
+    _, vb = torch_predict(sd_b, 256, 6, S, torch.float64)
+    is_a, is_b = np.abs(V - va) <= 2e-5, np.abs(V - vb) <= 2e-5
+    assert (is_a | is_b).all() and (is_a & ~is_b).any() and (is_b & ~is_a).any()

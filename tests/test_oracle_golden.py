@@ -198,3 +198,32 @@ def test_prior_checker_accepts_the_oracle_net_and_rejects_a_perturbed_one(golden
     bad[0, r, a] *= np.float32(np.exp(1e-3))
     with pytest.raises(AssertionError):
         check_recorded_priors(bad, v[None], cnt, W[None], sd, 64, 1)
+
+
+@pytest.mark.parametrize("tag", ["shared", "fresh"])
+def test_gating_arena_matches_reference(golden, tag):
+    """The oracle's dual-tree arena (Coach.learn's pmcts vs nmcts, Coach.py:117-139) against the
+    REFERENCE's games: trees kept across the games of playGames (shared) and fresh per game."""
+    g = golden("arena_gating_hash.npz")
+    o = O.arena_dual(g["env"], g["seat"], int(g["seed"]), int(g["sims"]), float(g["cpuct"]), shared=tag == "shared")
+    assert o["nerr"] == 0
+    assert np.array_equal(o["result"], g[tag + "_result"])
+    assert np.array_equal(o["stats"][:, 4], g[tag + "_ctr_end"])
+    assert np.array_equal(o["stats"][:, 1], g[tag + "_expansions"])
+    for i, m in enumerate(g[tag + "_n_moves"]):
+        assert np.array_equal(o["actions"][i, :m], g[tag + "_actions"][i, :m]), i
+
+
+def test_gating_arena_fresh_trees_equal_shared_trees():
+    """Where the engine differs from the reference by construction - one tree per game instead of
+    pmcts / nmcts kept across the games of playGames - the oracle plays both ways: no game differs
+    (96 games here; 400 games at 25 sims measured identical too)."""
+    n = 96
+    env = np.arange(n) + 123
+    seats = np.where(np.arange(n) < n // 2, 1, -1)
+    a = O.arena_dual(env, seats, 17, 10, 1.5, shared=True)
+    b = O.arena_dual(env, seats, 17, 10, 1.5, shared=False, threads=8)
+    assert a["nerr"] == 0 and b["nerr"] == 0
+    for k in ("result", "totals", "final", "actions"):
+        assert np.array_equal(a[k], b[k]), k
+    assert np.array_equal(a["stats"][:, 1], b["stats"][:, 1]) and np.array_equal(a["stats"][:, 4], b["stats"][:, 4])
