@@ -201,6 +201,19 @@ int yk_engine_predictions(yk_engine_t* eng, float* pi, float* v, yk_state_t* lea
 int64_t yk_engine_record_bytes(yk_engine_t* eng);
 int yk_engine_pack_records(yk_engine_t* eng, void* dst, int64_t capacity, void* stream);
 
+/* The replay buffer's examples: n_images packed record images back to back (each
+ * yk_engine_record_bytes of an engine with n_envs games, max_moves, sims - e.g. every rank's image
+ * after the all-gather) -> one example per move of the first n_games games (image-major; < 0 = all),
+ * in (image, game, move) order: Coach.executeEpisode's (canonicalBoard, pi, v) (Coach.py:57-72)
+ * as NNetWrapper.train consumes it - states[k] the board, targets[k] = argmax(pi) (NNet.py:145-146:
+ * the played action at temp 0, the most visited action at temp 1, lowest on ties), values[k] = v
+ * (float32).  The first `skip` examples are dropped (the maxlenOfQueue deque keeps the last ones,
+ * Coach.py:86-90); at most `capacity` are written.  states = NULL: count only.  HOST *n_examples =
+ * examples written (or countable).  Synchronises `stream`. */
+int yk_examples_from_records(const void* images, int n_images, int n_envs, int max_moves, int sims,
+                             int64_t n_games, int64_t skip, int64_t capacity, yk_state_t* states, int32_t* targets,
+                             float* values, int64_t* n_examples, void* stream);
+
 /* ---------------------------------------------------------------- Arena
  * Batched Arena.playGame (Arena.py:30-93), n_envs games in lock-step: `agent` in seat
  * agent_seat[i] (HOST, [n]; 1 = moves first, -1) against `opponent` in the other seat, each a

@@ -1304,7 +1304,7 @@ int yk_engine_create(yk_engine_t** out, const yk_engine_config_t* cfg, yk_net_t*
         const double need = (double)worst * 6.0 * cfg->n_envs * (cfg->dual_trees ? 2 : 1);
         d.AE = (need < 0.6 * (double)free_b) ? worst : (int64_t)cfg->sims * 9000 + 65536;
     }
-    d.VCAP = 2 * cfg->max_moves * std::max(cfg->sims, 32);
+    d.VCAP = (int)record_vcap(cfg->max_moves, cfg->sims);
     d.rec_pred = cfg->record_predictions ? 1 : 0;
     d.max_exp = cfg->record_predictions ? std::max(cfg->max_expansions, 1) : 0;
     d.rec_stride = std::max(cfg->record_stride, 1);
@@ -1668,38 +1668,28 @@ int yk_engine_predictions(yk_engine_t* eng, float* pi, float* v, yk_state_t* lea
     return YK_OK;
 }
 
-static void record_parts(yk_engine* eng, void** p, int64_t* b) {
+static void record_parts(yk_engine* eng, void** p, RecordLayout& L) {
     EngDev& d = eng->d;
-    const int64_t E = d.E, M = d.M;
-    void* pp[] = {d.rec_state, d.rec_info, d.rec_ctr, d.rec_val, d.rec_visits, d.rec_voff, d.nmoves, d.board};
-    int64_t bb[] = {E * M * 64, E * M * 8 * 4, E * M * 2 * 8, E * M * 8, E * d.VCAP * 4, E * (M + 1) * 4, E * 4,
-                    E * 64};
-    for (int i = 0; i < 8; i++) {
-        p[i] = pp[i];
-        b[i] = bb[i];
-    }
+    L = record_layout(d.E, d.M, d.VCAP);
+    void* pp[REC_PARTS] = {d.rec_state, d.rec_info, d.rec_ctr, d.rec_val, d.rec_visits, d.rec_voff, d.nmoves, d.board};
+    for (int i = 0; i < REC_PARTS; i++) p[i] = pp[i];
 }
 
 int64_t yk_engine_record_bytes(yk_engine_t* eng) {
     if (!eng) return YK_ERR_ARG;
-    void* p[8];
-    int64_t b[8], t = 0;
-    record_parts(eng, p, b);
-    for (int i = 0; i < 8; i++) t += (b[i] + 15) & ~15LL;
-    return t;
+    return record_layout(eng->d.E, eng->d.M, eng->d.VCAP).total;
 }
 
 int yk_engine_pack_records(yk_engine_t* eng, void* dst, int64_t capacity, void* stream) {
     if (!eng || !dst) return YK_ERR_ARG;
     if (!eng->have_records) return YK_ERR_STATE;
-    if (capacity < yk_engine_record_bytes(eng)) return YK_ERR_ARG;
-    void* p[8];
-    int64_t b[8], off = 0;
-    record_parts(eng, p, b);
-    for (int i = 0; i < 8; i++) {
-        YK_HIP(hipMemcpyAsync((char*)dst + off, p[i], (size_t)b[i], hipMemcpyDeviceToDevice, as_stream(stream)));
-        off += (b[i] + 15) & ~15LL;
-    }
+    void* p[REC_PARTS];
+    RecordLayout L;
+    record_parts(eng, p, L);
+    if (capacity < L.total) return YK_ERR_ARG;
+    for (int i = 0; i < REC_PARTS; i++)
+        YK_HIP(hipMemcpyAsync((char*)dst + L.off[i], p[i], (size_t)L.bytes[i], hipMemcpyDeviceToDevice,
+                              as_stream(stream)));
     return YK_OK;
 }
 

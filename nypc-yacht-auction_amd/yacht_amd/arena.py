@@ -146,3 +146,45 @@ class MCTSArena:
         one = int((agent == 1).sum())
         two = int((agent == -1).sum())
         return one, two, len(seats) - one - two
+
+
+class GatingArena:
+    """Coach.learn's gating arena (Coach.py:117-139): ``Arena(pmcts, nmcts).playGames(num)`` with
+    pmcts = MCTS over the previous net and nmcts = MCTS over the new one, each
+    ``np.argmax(getActionProb(x, temp=0))``, as ONE device batch on a dual-tree engine (one tree
+    per seat, each seat its own net).  pmcts is player one of the first num/2 games and player
+    two of the rest (Arena.py:118).  Game k uses stream (game seed, env_base + k).
+
+    Under torch.distributed the games are sharded over the ranks (rank r plays games
+    [r*c, (r+1)*c)) and the tallies summed, so every rank gets the single-GPU result."""
+
+    def __init__(self, game, pnet, nnet, args):
+        self.game, self.pnet, self.nnet, self.args = game, pnet, nnet, args
+        self.last = None
+
+    def playGames(self, num, env_base: int = None):
+        """-> (pwins, nwins, draws): (oneWon, twoWon, draws) of Arena.playGames with pmcts as one."""
+        from . import dist as D
+        rank, world = D.rank_world()
+        half = int(num / 2)
+        total = 2 * half
+        base = self.game.rng.env if env_base is None else env_base
+        c, lo, hi = D.shard(total, rank, world)
+        one = two = 0
+        self.last = None
+        if hi > lo:
+            seats = np.where(np.arange(lo, hi) < half, 1, -1).astype(np.int32)
+            hashed = getattr(self.pnet, "yk_prior", None) == "hash" and getattr(self.nnet, "yk_prior", None) == "hash"
+            a = self.args
+            eng = SelfPlayEngine(hi - lo, a.numMCTSSims, a.get("cpuct", 1.0), 0,
+                                 net=None if hashed else self.pnet.yk_net(), prior="hash" if hashed else "net",
+                                 opponent_net=None if hashed else self.nnet.yk_net(), max_moves=48, dual_trees=True)
+            try:
+                eng.arena(seats, self.game.rng.seed, base + lo, agent="mcts", opponent="mcts")
+                self.last = eng.arena_results()
+            finally:
+                eng.close()
+            p = self.last["result"] * seats  # +1: pmcts won
+            one, two = int((p == 1).sum()), int((p == -1).sum())
+        one, two, n = D.allreduce_counts([one, two, hi - lo], device="cuda")
+        return one, two, n - one - two

@@ -28,22 +28,36 @@ from .state import ACTION_SIZE, PlayerState, YachtState, pack_many, unpack
 # ---------------------------------------------------------------- native format
 def save_examples(path: str, history) -> None:
     """history: list (iterations) of iterables of (YachtState, pi, v)."""
-    sizes, boards, rows, cols, vals, values = [], [], [], [], [], []
+    from .replay import ExampleShard
+    sizes, chunks, rows, cols, vals, values = [], [], [], [], [], []
     k = 0
     for it in history:
+        if isinstance(it, ExampleShard):  # the device replay buffer: straight from its arrays
+            h = it.host()
+            n = len(it)
+            sizes.append(n)
+            lens = np.diff(h["pi_indptr"])
+            rows.append(np.repeat(np.arange(k, k + n, dtype=np.int32), lens))
+            cols.append(h["pi_cols"].astype(np.int16))
+            vals.append(h["pi_vals"].astype(np.float64))
+            chunks.append(np.asarray(h["states"], dtype=np.uint64).reshape(-1, 8))
+            values.extend(float(v) for v in h["values"])
+            k += n
+            continue
         it = list(it)
         sizes.append(len(it))
+        if it:
+            chunks.append(pack_many([b for b, _, _ in it]))
         for b, pi, v in it:
             p = np.asarray(pi, dtype=np.float64)
             nz = np.nonzero(p)[0]
             rows.append(np.full(len(nz), k, dtype=np.int32))
             cols.append(nz.astype(np.int16))
             vals.append(p[nz])
-            boards.append(b)
             values.append(float(v))
             k += 1
     np.savez_compressed(path, format=np.array("yacht_amd.examples.v1"), sizes=np.array(sizes, dtype=np.int64),
-                        states=pack_many(boards) if boards else np.zeros((0, 8), np.uint64),
+                        states=np.concatenate(chunks) if chunks else np.zeros((0, 8), np.uint64),
                         pi_rows=np.concatenate(rows) if rows else np.zeros(0, np.int32),
                         pi_cols=np.concatenate(cols) if cols else np.zeros(0, np.int16),
                         pi_vals=np.concatenate(vals) if vals else np.zeros(0),

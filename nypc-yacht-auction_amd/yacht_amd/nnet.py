@@ -171,12 +171,22 @@ class NNetWrapper:
         """The reference loop: `epochs` passes over shuffled minibatches of `batch_size`
         (drop_last False), one CE(argmax pi) + vloss_weight * MSE step each, clip 5.0, AdamW.
         Shuffles come from a torch generator seeded per call (the reference uses the global
-        torch RNG); dropout masks from the trainer's Philox stream."""
-        from .train import examples_to_device
+        torch RNG); dropout masks from the trainer's Philox stream.
+
+        `examples`: the reference's list of (board, pi, v), an ExampleShard (device replay
+        buffer), or a list of either (trainExamplesHistory).  Under torch.distributed every
+        rank holds the same pooled examples and draws the same permutation; each minibatch is
+        split across the ranks, and the all-reduce of the share-weighted gradients gives every
+        rank the whole minibatch's gradient, so all ranks take the single-process step (up to
+        f32 summation order) and their parameters stay identical."""
+        from . import dist as D
+        from .replay import as_device_examples
         tr = self._trainer()
-        states, targets, values = examples_to_device(examples)
+        states, targets, values = as_device_examples(examples)
+        rank, world = D.rank_world()
         n = states.shape[0]
         bs = self.args.batch_size
+        vw = self.args.get("vloss_weight", 1.0)
         g = torch.Generator(device="cuda")
         g.manual_seed(int(self.args.get("seed", 0)) + 1000003 * tr.step_count)
         for epoch in range(self.args.epochs):
@@ -185,13 +195,23 @@ class NNetWrapper:
             total, count = 0.0, 0
             for i in range(0, n, bs):
                 idx = perm[i:i + bs]
-                tr.step(states, targets, values, idx=idx)
-                if report:
-                    ce, se, _ = tr.losses()
+                if world == 1:
+                    tr.step(states, targets, values, idx=idx)
                     b = idx.numel()
-                    total += ce / b + self.args.get("vloss_weight", 1.0) * se / b
+                else:
+                    loc = torch.tensor_split(idx, world)[rank]
+                    b = loc.numel()
+                    if b:
+                        tr.backward(states, targets, values, idx=loc)
+                    else:
+                        tr.grads().zero_()
+                    D.allreduce_grads(tr, weight=b / idx.numel())
+                    tr.apply()
+                if report and b:
+                    ce, se, _ = tr.losses()
+                    total += ce / b + vw * se / b
                     count += 1
-            if report:
+            if report and rank == 0:
                 print(f"Epoch {epoch + 1}/{self.args.epochs}, Avg Loss: {total / max(count, 1):.4f}")
         with torch.no_grad():
             self.nnet.load_state_dict(tr.state_dict())  # the torch copy feeds checkpoints and predict

@@ -1,0 +1,196 @@
+"""The replay buffer (Coach.py:84-101): self-play examples kept on the device.
+
+Coach.learn keeps ``trainExamplesHistory``, one deque of ``(canonicalBoard, pi, v)`` per
+iteration.  At config 5's scale (65536 games x 48 moves per iteration) those Python lists do
+not fit (a dense pi is 3226 floats), and NNetWrapper.train only uses ``argmax(pi)`` of them
+(NNet.py:145-146).  So an iteration's examples are an ``ExampleShard``: device arrays of
+packed boards (64 B), argmax targets and float32 values, built by ``yk_examples_from_records``
+straight from the (all-gathered) trajectory record images.  The record image stays on the
+device as the shard's source, so the full visit policies - for the examples file
+(Coach.py:144-151) or for code that iterates the reference's tuples - are recovered on demand.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from collections import deque
+
+import numpy as np
+import torch
+
+from ._lib import call, stream_ptr
+from .engine import unpack_record_image
+
+
+def _vcap(max_moves: int, sims: int) -> int:
+    return 2 * max_moves * max(sims, 32)
+
+
+class ExampleShard:
+    """One iteration's examples (``iterationTrainExamples``, Coach.py:86-90) on the device:
+    ``states`` int64[n, 8] (packed canonical boards), ``targets`` int32[n] (argmax pi),
+    ``values`` float32[n].  ``len`` and iteration behave like the reference's deque of
+    ``(YachtState, pi list, v)`` tuples (built lazily from the record images)."""
+
+    def __init__(self, states, targets, values, source=None):
+        self.states, self.targets, self.values = states, targets, values
+        self._source = source  # (images u8 [R, nbytes] device, n_envs, max_moves, sims, n_games, skip)
+        self._host = None
+
+    def __len__(self):
+        return int(self.targets.numel())
+
+    def host(self) -> dict:
+        """Host arrays of the shard with the full policies (sparse CSR, float64 as
+        MCTS.getActionProb returns them): states u64[n, 8], pi_indptr i64[n+1], pi_cols i32,
+        pi_vals f64, values f64[n], targets i32[n]."""
+        if self._host is None:
+            if self._source is None:
+                raise ValueError("this shard has no record images to rebuild policies from")
+            images, E, M, sims, n_games, skip = self._source
+            h = host_examples(images.cpu().numpy(), E, M, sims, n_games)
+            n = len(self)
+            self._host = _tail(h, skip, n)
+        return self._host
+
+    def __iter__(self):
+        from .state import ACTION_SIZE, unpack
+        h = self.host()
+        for k in range(len(self)):
+            pi = [0.0] * ACTION_SIZE
+            a0, a1 = int(h["pi_indptr"][k]), int(h["pi_indptr"][k + 1])
+            for c, v in zip(h["pi_cols"][a0:a1], h["pi_vals"][a0:a1]):
+                pi[int(c)] = float(v)
+            yield unpack(h["states"][k]), pi, float(h["values"][k])
+
+    def __getitem__(self, k):
+        from .state import ACTION_SIZE, unpack
+        h = self.host()
+        k = range(len(self))[k]
+        pi = [0.0] * ACTION_SIZE
+        a0, a1 = int(h["pi_indptr"][k]), int(h["pi_indptr"][k + 1])
+        for c, v in zip(h["pi_cols"][a0:a1], h["pi_vals"][a0:a1]):
+            pi[int(c)] = float(v)
+        return unpack(h["states"][k]), pi, float(h["values"][k])
+
+
+def examples_from_images(images: torch.Tensor, n_envs: int, max_moves: int, sims: int, n_games: int = -1,
+                         maxlen: int = None, stream=None) -> ExampleShard:
+    """Record images (device uint8 [R, nbytes]: every rank's yk_engine_pack_records after the
+    all-gather) -> ExampleShard of the first n_games games, keeping the last `maxlen` examples
+    (the maxlenOfQueue deque, Coach.py:86-90)."""
+    imgs = images.reshape(images.shape[0] if images.dim() > 1 else 1, -1).contiguous()
+    R = imgs.shape[0]
+    cnt = C.c_int64()
+    sp = stream_ptr(stream)
+    call("yk_examples_from_records", imgs.data_ptr(), R, n_envs, max_moves, sims, n_games, 0, 0, None, None, None,
+         C.byref(cnt), sp)
+    total = int(cnt.value)
+    skip = max(total - int(maxlen), 0) if maxlen is not None else 0
+    n = total - skip
+    states = torch.empty((max(n, 1), 8), dtype=torch.int64, device="cuda")
+    targets = torch.empty(max(n, 1), dtype=torch.int32, device="cuda")
+    values = torch.empty(max(n, 1), dtype=torch.float32, device="cuda")
+    call("yk_examples_from_records", imgs.data_ptr(), R, n_envs, max_moves, sims, n_games, skip, n,
+         states.data_ptr(), targets.data_ptr(), values.data_ptr(), C.byref(cnt), sp)
+    if int(cnt.value) != n:
+        raise RuntimeError(f"yk_examples_from_records wrote {cnt.value} examples, expected {n}")
+    return ExampleShard(states[:n], targets[:n], values[:n], source=(imgs, n_envs, max_moves, sims, n_games, skip))
+
+
+# ---------------------------------------------------------------- host side (numpy)
+def host_examples(images: np.ndarray, n_envs: int, max_moves: int, sims: int, n_games: int = -1) -> dict:
+    """The same examples from host copies of the record images, with the full policies
+    (Coach.py:57-61: MCTS.getActionProb's pi per move - one-hot at the played action at temp 0,
+    N / sum(N) at temp 1, MCTS.py:44-54) as a sparse CSR.  Used for the examples file and as an
+    independent restatement of yk_examples_from_records in tests."""
+    imgs = np.ascontiguousarray(images).reshape(images.shape[0] if images.ndim > 1 else 1, -1)
+    total_games = imgs.shape[0] * n_envs
+    n_games = total_games if n_games is None or n_games < 0 else min(n_games, total_games)
+    parts = {k: [] for k in ("states", "values", "targets", "cols", "vals", "lens")}
+    for r in range(imgs.shape[0]):
+        g = min(max(n_games - r * n_envs, 0), n_envs)
+        if g == 0:
+            continue
+        img = unpack_record_image(imgs[r], n_envs, max_moves, sims)
+        nm = np.clip(img["n_moves"][:g], 0, max_moves)
+        mask = np.arange(max_moves)[None, :] < nm[:, None]
+        e_idx, m_idx = np.nonzero(mask)
+        info = img["info"][:g][mask]
+        temp, action = info[:, 0], info[:, 2]
+        voff = img["voff"]
+        a0, a1 = voff[e_idx, m_idx].astype(np.int64), voff[e_idx, m_idx + 1].astype(np.int64)
+        hot = temp != 0
+        lens = np.where(hot, a1 - a0, 1)
+        n = len(temp)
+        starts = np.concatenate([[0], np.cumsum(lens)])
+        within = np.arange(starts[-1]) - np.repeat(starts[:-1], lens)
+        row = np.repeat(np.arange(n), lens)
+        vcap = _vcap(max_moves, sims)
+        raw = img["visits_raw"].reshape(-1)[(e_idx[row].astype(np.int64) * vcap + a0[row] + within)
+                                           .clip(0, n_envs * vcap - 1)]
+        cols = np.where(hot[row], (raw >> 16).astype(np.int64), action[row].astype(np.int64))
+        cnt = np.where(hot[row], (raw & 0xFFFF).astype(np.float64), 1.0)
+        sums = np.bincount(row, weights=cnt, minlength=n)
+        vals = cnt / np.where(sums[row] > 0, sums[row], 1.0)
+        # argmax(pi): the most visited action, the lowest on ties (ascending action order)
+        mx = np.zeros(n)
+        np.maximum.at(mx, row, cnt)
+        big = np.iinfo(np.int64).max
+        first = np.full(n, big, dtype=np.int64)
+        np.minimum.at(first, row, np.where(cnt == mx[row], cols, big))
+        targets = np.where((first == big) | (mx == 0), action, first).astype(np.int32)
+        keep = cnt > 0  # the examples file stores the nonzero entries of pi
+        kl = np.bincount(row[keep], minlength=n)
+        parts["states"].append(img["states"][:g][mask])
+        parts["values"].append(img["values"][:g][mask])
+        parts["targets"].append(targets)
+        parts["cols"].append(cols[keep].astype(np.int32))
+        parts["vals"].append(vals[keep])
+        parts["lens"].append(kl)
+    cat = {k: (np.concatenate(v) if v else None) for k, v in parts.items()}
+    n = 0 if cat["targets"] is None else len(cat["targets"])
+    lens = cat["lens"] if cat["lens"] is not None else np.zeros(0, np.int64)
+    return dict(states=cat["states"] if n else np.zeros((0, 8), np.uint64),
+                values=cat["values"] if n else np.zeros(0),
+                targets=cat["targets"] if n else np.zeros(0, np.int32),
+                pi_indptr=np.concatenate([[0], np.cumsum(lens)]).astype(np.int64),
+                pi_cols=cat["cols"] if n else np.zeros(0, np.int32),
+                pi_vals=cat["vals"] if n else np.zeros(0))
+
+
+def _tail(h: dict, skip: int, n: int) -> dict:
+    """Examples skip .. skip+n of host_examples' output."""
+    ip = h["pi_indptr"]
+    a0, a1 = int(ip[skip]), int(ip[skip + n])
+    return dict(states=h["states"][skip:skip + n], values=h["values"][skip:skip + n],
+                targets=h["targets"][skip:skip + n], pi_indptr=ip[skip:skip + n + 1] - a0,
+                pi_cols=h["pi_cols"][a0:a1], pi_vals=h["pi_vals"][a0:a1])
+
+
+# ---------------------------------------------------------------- what NNetWrapper.train takes
+def _is_example(x) -> bool:
+    return isinstance(x, tuple) and len(x) == 3 and not isinstance(x[0], (ExampleShard, list, deque))
+
+
+def as_device_examples(examples):
+    """examples: an ExampleShard, a list of (board, pi, v) tuples (Coach.py:72), or a list of
+    either (trainExamplesHistory) -> device (states int64[n, 8], targets int32[n], values f32[n])."""
+    from .train import examples_to_device
+    if isinstance(examples, ExampleShard):
+        return examples.states, examples.targets, examples.values
+    items = list(examples)
+    if not items or _is_example(items[0]):
+        if not items:
+            return (torch.zeros((0, 8), dtype=torch.int64, device="cuda"),
+                    torch.zeros(0, dtype=torch.int32, device="cuda"), torch.zeros(0, dtype=torch.float32, device="cuda"))
+        return examples_to_device(items)
+    parts = [as_device_examples(x) for x in items]
+    parts = [p for p in parts if p[1].numel()]
+    if not parts:
+        return as_device_examples([])
+    if len(parts) == 1:
+        return parts[0]
+    return tuple(torch.cat([p[i] for p in parts]) for i in range(3))
+
+
+__all__ = ["ExampleShard", "examples_from_images", "host_examples", "as_device_examples"]

@@ -1,0 +1,197 @@
+"""Config 5 on the GPU: the device replay buffer and the multi-rank Coach iteration
+(Coach.py:74-139).
+
+* yk_examples_from_records (the device replay buffer) against two independent host
+  restatements: replay.host_examples (numpy over the packed image) and coach.examples_from_records
+  (the reference's per-move (board, pi, v) tuples, argmax'd as NNet.py:145-146 does);
+* sharding: the images of games split over "ranks" pool into exactly the single-batch examples;
+* two ranks (gloo) sharing GPU 0 run the Coach's pieces and Coach.learn: the pooled buffer is
+  the union of both ranks' records and equals one process playing every game; both ranks hold
+  bit-identical parameters after training, equal to the single-process train within f32
+  summation order; the sharded gating arena's tally equals the single-GPU arena.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from oracle import spec
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+ARGS = dict(numIters=1, numEps=6, tempThreshold=15, updateThreshold=0.55, maxlenOfQueue=200000, numMCTSSims=4,
+            arenaCompare=6, cpuct=1.5, numItersForTrainExamplesHistory=5, lr=2e-3, weight_decay=1e-4, epochs=2,
+            batch_size=40, vloss_weight=1.5, cuda=True, hidden=64, nblocks=1, dropout=0.0, seed=3)
+
+
+@pytest.fixture(scope="module")
+def Y():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from yacht_amd import coach, engine, nnet, replay
+    return coach, engine, nnet, replay
+
+
+def _selfplay(E, net, n, sims, seed, base, max_moves=48):
+    eng = E.SelfPlayEngine(n, sims, 1.5, 15, net=net, max_moves=max_moves)
+    eng.run(seed, base)
+    assert eng.stats()["errors"] == 0
+    rec = eng.records()
+    img = eng.pack_records()
+    eng.close()
+    return rec, img
+
+
+def _assert_same_examples(shard, h, states_key="states"):
+    assert len(shard) == len(h["targets"])
+    assert np.array_equal(shard.states.cpu().numpy().view(np.uint64), h[states_key])
+    assert np.array_equal(shard.targets.cpu().numpy(), h["targets"])
+    assert np.array_equal(shard.values.cpu().numpy(), h["values"].astype(np.float32))
+
+
+def test_examples_kernel_matches_host_restatements(Y):
+    C, E, N, R = Y
+    n, sims, seed, base = 96, 12, 41, 300
+    net = N.YkNet(spec.closed_form_weights(256, 6), 256, 6)
+    rec, img = _selfplay(E, net, n, sims, seed, base)
+    shard = R.examples_from_images(img, n, 48, sims)
+    h = R.host_examples(img.cpu().numpy(), n, 48, sims)
+    _assert_same_examples(shard, h)
+    # the reference's tuples (Coach.py:72) -> argmax(pi) (NNet.py:145-146), values, boards
+    ref = [ex for ep in C.examples_from_records(rec, n) for ex in ep]
+    assert len(ref) == len(shard) == n * 48
+    from yacht_amd.state import pack_many
+    assert np.array_equal(pack_many([b for b, _, _ in ref]), h["states"])
+    assert np.array_equal(np.array([int(np.argmax(np.asarray(p))) for _, p, _ in ref], dtype=np.int32), h["targets"])
+    assert np.array_equal(np.array([v for _, _, v in ref]), h["values"])
+    # both temperatures occur, and a temp-1 target is not always the played action
+    temp = rec["info"][:, :48, 0].reshape(-1)
+    act = rec["info"][:, :48, 2].reshape(-1)
+    assert (temp == 1).any() and (temp == 0).any() and (h["targets"][temp == 1] != act[temp == 1]).any()
+    # the sparse policies are the reference's pi exactly
+    for k in (0, 1, 13, 14, 15, 47, 48 * 5 + 3, len(ref) - 1):
+        pi = np.zeros(3226)
+        a0, a1 = h["pi_indptr"][k], h["pi_indptr"][k + 1]
+        pi[h["pi_cols"][a0:a1]] = h["pi_vals"][a0:a1]
+        assert np.array_equal(pi, np.asarray(ref[k][1], dtype=np.float64)), k
+    # the deque's maxlen keeps the last examples; n_games trims whole games from the end
+    tail = R.examples_from_images(img, n, 48, sims, maxlen=1000)
+    assert len(tail) == 1000
+    assert torch.equal(tail.targets, shard.targets[-1000:]) and torch.equal(tail.states, shard.states[-1000:])
+    part = R.examples_from_images(img, n, 48, sims, n_games=7)
+    assert len(part) == 7 * 48 and torch.equal(part.targets, shard.targets[:7 * 48])
+    # lazy reference tuples of a shard
+    b, pi, v = tail[0]
+    assert pi == ref[len(ref) - 1000][1] and v == ref[len(ref) - 1000][2]
+    assert [int(x) for x in pack_many([b])[0]] == [int(x) for x in h["states"][len(ref) - 1000]]
+
+
+def test_sharded_images_pool_into_the_single_batch(Y):
+    """What the all-gather builds: images of games [0, c) and [c, 2c) (two ranks, stream
+    env0 + k for game k) give exactly the examples of one engine playing all games; a short
+    last shard is trimmed with n_games."""
+    C, E, N, R = Y
+    n, sims, seed, base = 45, 6, 77, 1000
+    net = N.YkNet(spec.closed_form_weights(256, 6), 256, 6)
+    _, whole = _selfplay(E, net, n, sims, seed, base)
+    c = 23
+    imgs = [_selfplay(E, net, c, sims, seed, base + r * c)[1] for r in range(2)]
+    pooled = R.examples_from_images(torch.stack(imgs), c, 48, sims, n_games=n)
+    single = R.examples_from_images(whole, n, 48, sims)
+    assert len(pooled) == len(single) == n * 48
+    for k in ("states", "targets", "values"):
+        assert torch.equal(getattr(pooled, k), getattr(single, k)), k
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _coach_worker(rank, world, port, ckdir, out):
+    import sys
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (here, os.path.join(here, "nypc-yacht-auction_amd")):
+        sys.path.insert(0, p)
+    torch.cuda.set_device(0)  # both ranks share the one GPU of the box
+    from yacht_amd.arena import GatingArena
+    from yacht_amd.coach import Coach
+    from yacht_amd.game import YachtGame
+    from yacht_amd.nnet import NNetWrapper
+    from yacht_amd.utils import dotdict
+    args = dotdict(ARGS, checkpoint=ckdir, load_folder_file=(ckdir, "best.pth.tar"))
+    torch.manual_seed(5)
+    game = YachtGame(seed=21, env_id=500)
+    coach = Coach(game, NNetWrapper(game, args), args)
+    # the pieces: sharded self-play + all-gather, DDP train, sharded gating arena
+    shard = coach.selfPlayExamples(args.numEps)
+    out[f"ex{rank}"] = (shard.states.cpu().numpy(), shard.targets.cpu().numpy(), shard.values.cpu().numpy())
+    coach.pnet.nnet.load_state_dict(coach.nnet.nnet.state_dict())
+    coach.nnet.train([shard], verbose=False)
+    out[f"p{rank}"] = {k: v.numpy().copy() for k, v in coach.nnet.nnet.state_dict().items()}
+    out[f"pit{rank}"] = GatingArena(game, coach.pnet, coach.nnet, args).playGames(args.arenaCompare, env_base=900)
+    # the loop itself (files written by rank 0, read back by every rank)
+    coach.learn()
+    out[f"learn{rank}"] = (coach.last_pit, len(coach.trainExamplesHistory[-1]),
+                           {k: v.numpy().copy() for k, v in coach.nnet.nnet.state_dict().items()})
+    dist.destroy_process_group()
+
+
+def test_coach_iteration_two_ranks_sharing_gpu0(Y, tmp_path):
+    import torch.multiprocessing as mp
+    C, E, N, R = Y
+    from yacht_amd.arena import GatingArena
+    from yacht_amd.game import YachtGame
+    from yacht_amd.nnet import NNetWrapper
+    from yacht_amd.utils import dotdict
+    mgr = mp.get_context("spawn").Manager()
+    out = mgr.dict()
+    ck = str(tmp_path / "ck")
+    mp.start_processes(_coach_worker, args=(2, _free_port(), ck, out), nprocs=2, start_method="spawn")
+    # the pooled buffer: identical on both ranks, the union of the ranks' games in env-id order
+    # (rank 0 played envs 500-502, rank 1 503-505), equal to one process playing all six
+    for a, b in zip(out["ex0"], out["ex1"]):
+        assert np.array_equal(a, b)
+    args = dotdict(ARGS, checkpoint=str(tmp_path / "single"), load_folder_file=(str(tmp_path), "x"))
+    torch.manual_seed(5)
+    game = YachtGame(seed=21, env_id=500)
+    coach = C.Coach(game, NNetWrapper(game, args), args)
+    single = coach.selfPlayExamples(args.numEps)
+    assert len(single) == 6 * 48
+    assert np.array_equal(single.states.cpu().numpy(), out["ex0"][0])
+    assert np.array_equal(single.targets.cpu().numpy(), out["ex0"][1])
+    assert np.array_equal(single.values.cpu().numpy(), out["ex0"][2])
+    net0 = NNetWrapper(game, args)
+    net0.nnet.load_state_dict(coach.nnet.nnet.state_dict())
+    _, img1 = _selfplay(E, coach.nnet.yk_net(), 3, 4, 21, 503)  # rank 1's own games
+    part = R.examples_from_images(img1, 3, 48, 4)
+    assert torch.equal(part.targets.cpu(), torch.from_numpy(out["ex0"][1][3 * 48:]))
+    # DDP: both ranks bit-identical; equal to the single-process train up to f32 summation order
+    p0, p1 = out["p0"], out["p1"]
+    assert all(np.array_equal(p0[k], p1[k]) for k in p0)
+    coach.nnet.train([single], verbose=False)
+    sp = coach.nnet.nnet.state_dict()
+    a = np.concatenate([p0[k].reshape(-1) for k in p0]).astype(np.float64)
+    b = np.concatenate([sp[k].numpy().reshape(-1) for k in p0]).astype(np.float64)
+    # AdamW divides by sqrt(v) + eps, so a gradient entry near eps can move its weight by up to
+    # 2 lr on a summation-order change; everything else agrees to f32 rounding
+    assert np.linalg.norm(a - b) / np.linalg.norm(b) < 1e-4
+    assert (np.abs(a - b) > 1e-5).mean() < 1e-3
+    # the sharded gating arena's tally is the single-GPU arena's
+    pit = GatingArena(game, net0, coach.nnet, args).playGames(args.arenaCompare, env_base=900)
+    assert out["pit0"] == out["pit1"]
+    assert sum(out["pit0"]) == 6 and sum(pit) == 6
+    # Coach.learn on two ranks: same verdict, examples and parameters on both
+    l0, l1 = out["learn0"], out["learn1"]
+    assert l0[0] == l1[0] and l0[1] == l1[1] == 6 * 48
+    assert all(np.array_equal(l0[2][k], l1[2][k]) for k in l0[2])
+    for f in ("temp.pth.tar", "checkpoint_0.pth.tar.examples.npz"):
+        assert os.path.exists(os.path.join(ck, f)), f
