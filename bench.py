@@ -38,10 +38,23 @@ H, NB, A = 256, 6, 3226
 PREDICT_FLOP = 2 * (59 * H + 2 * NB * H * H + H * 128 + 128 + H * A)  # = 3,320,576
 
 
+def host_cores():
+    """The host cores this process may use: OMP_NUM_THREADS when the box sets it (the GPU pool
+    gives each 1-GPU box a share of 16 of the machine's CPUs and exports OMP_NUM_THREADS=16),
+    else the CPUs in this process's affinity mask."""
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    if env.isdigit() and int(env) > 0:
+        return int(env), "OMP_NUM_THREADS"
+    return len(os.sched_getaffinity(0)), "affinity mask"
+
+
 def cpu_baseline(state_dict, sims, seconds_target=15.0, threads=None):
-    """The oracle restatement (C, OpenMP over games) on this host's cores: bounded sample."""
+    """The oracle restatement (C, OpenMP over games) on every host core this process may use:
+    a bounded sample of the same workload."""
     from oracle import oracle as O
-    threads = threads or min(16, os.cpu_count() or 1)
+    src = "argument"
+    if not threads:
+        threads, src = host_cores()
     net = O.Net(state_dict, H, NB)
     # calibrate: one game per thread, then scale the sample to ~seconds_target
     t0 = time.time()
@@ -58,21 +71,39 @@ def cpu_baseline(state_dict, sims, seconds_target=15.0, threads=None):
         exps += int(r["stats"][:, 1].sum())
         games += threads * k
     return {"value": exps / dt, "unit": "expansions/s", "cores": threads, "kind": "port",
+            "cores_source": f"{src}; the host has {os.cpu_count()} CPUs",
             "sample": f"{games} full self-play games x {sims} sims (C restatement, oracle/yk_oracle.c, "
-                      f"same net), {exps} expansions in {dt:.1f}s"}
+                      f"same net, one OpenMP thread per game), {exps} expansions in {dt:.1f}s",
+            "reference_python": "the reference's own Coach/MCTS (Python, 1 core) ran 236 expansions/s in the "
+                                "survey container (SURVEY.md section 6); it is not on the GPU box"}
 
 
-def measured_traffic(args):
-    """HBM bytes per k_forward launch from the committed rocprofv3 PMC passes of this exact
-    configuration (profiles/*_forward_traffic.json, tools/profile_bench.sh); None otherwise."""
+def measured_traffic(args, kind="forward"):
+    """HBM bytes per k_forward (kind "forward") / k_expand_backup ("expand") launch from the
+    committed rocprofv3 PMC passes of this exact configuration (profiles/*_{kind}_traffic.json,
+    tools/profile_bench.sh); None otherwise."""
     import glob
     best = None
-    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_forward_traffic.json"))):
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", f"*_{kind}_traffic.json"))):
         with open(f) as fh:
             t = json.load(fh)
         c = t.get("config", {})
         if (c.get("envs"), c.get("sims"), c.get("hidden"), c.get("nblocks")) == (args.envs, args.sims, H, NB):
             best = (t["hbm_bytes_per_launch"], os.path.relpath(f, REPO))
+    return best
+
+
+def measured_mfma(args):
+    """k_forward's MFMA busy fraction from the committed rocprofv3 SQ/GRBM pass of this exact
+    configuration (profiles/*_forward_mfma.json, tools/profile_bench.sh); None otherwise."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_forward_mfma.json"))):
+        with open(f) as fh:
+            t = json.load(fh)
+        c = t.get("config", {})
+        if (c.get("envs"), c.get("sims"), c.get("hidden"), c.get("nblocks")) == (args.envs, args.sims, H, NB):
+            best = dict(t, source=os.path.relpath(f, REPO))
     return best
 
 
@@ -153,6 +184,87 @@ def train_leg(model_sd, eng, steps=40, batch=512, seed=0):
             "last_loss": ce / batch + 1.5 * se / batch}
 
 
+def shape_leg(net, envs=2048, sims=200, seed=0):
+    """Config 3's per-GPU shape (16384 games x 200 sims over 8 GPUs = 2048 games/GPU x 200 sims):
+    one full episode batch on this GPU after one warm-up batch, with the node-pool capacity use
+    (NCAP is sized from sims)."""
+    import torch
+
+    from yacht_amd.engine import SelfPlayEngine
+    eng = SelfPlayEngine(envs, sims, 1.5, 15, net=net, max_moves=64)
+    eng.run(seed + 500, 0)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    eng.run(seed + 501, 0)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    st = eng.stats()
+    eng.close()
+    if st["errors"]:
+        raise SystemExit(f"config-3 leg: engine error flags {st['errors']}")
+    return {"config": f"{envs} games x {sims} sims on one GPU (config 3's per-GPU shape), full episodes",
+            "expansions_per_s": st["expansions"] / dt, "episodes_per_s": envs / dt, "s_per_batch": dt,
+            "capacity_use": {k: int(st[k]) for k in ("max_nodes", "node_cap", "max_edges", "edge_cap", "max_arena",
+                                                     "arena_cap")}}
+
+
+def coach_leg(model, image, n_envs, max_moves, sims, world, train_steps=60, arena_games=256, arena_sims=25,
+              seed=0):
+    """Config 5's Coach iteration after the self-play the timed steps just did (Coach.py:74-139),
+    on every rank: the pooled replay buffer from the (all-gathered) record images
+    (yk_examples_from_records), `train_steps` DDP train steps of the reference minibatch (512
+    examples split over the ranks, gradient all-reduce, clip, AdamW; NNetWrapper.train), and
+    the gating arena (previous vs new net, MCTS temp 0 each, one dual-tree batch sharded over
+    the ranks).  Returns this rank's phase times; rank 0 reports them."""
+    import numpy as np
+    import torch
+
+    from yacht_amd import dist as D
+    from yacht_amd.arena import GatingArena
+    from yacht_amd.game import YachtGame
+    from yacht_amd.nnet import DEFAULT_ARGS, NNetWrapper
+    from yacht_amd.replay import examples_from_images
+    from yacht_amd.utils import dotdict
+    rank, _ = D.rank_world()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    shard = examples_from_images(image, n_envs, max_moves, sims)
+    torch.cuda.synchronize()
+    t_ex = time.perf_counter() - t0
+    args = dotdict(DEFAULT_ARGS, epochs=1, numMCTSSims=arena_sims, cpuct=1.5, seed=seed)
+    game = YachtGame(seed=seed + 77, env_id=10**6)
+    prev, new = NNetWrapper(game, args), NNetWrapper(game, args)
+    prev.nnet.load_state_dict(model.state_dict())
+    new.nnet.load_state_dict(model.state_dict())
+    bs = args.batch_size
+    n = len(shard)
+    sub = torch.randperm(n, generator=torch.Generator().manual_seed(seed))[:bs * (train_steps + 3)]
+    few = (shard.states[sub.to("cuda")], shard.targets[sub.to("cuda")], shard.values[sub.to("cuda")])
+    from yacht_amd.replay import ExampleShard
+    warm = ExampleShard(*(x[:3 * bs] for x in few))
+    new.train(warm, verbose=False)  # warm-up: 3 steps (rocBLAS kernel selection)
+    timed = ExampleShard(*(x[3 * bs:] for x in few))
+    D.barrier()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    new.train(timed, verbose=False)
+    torch.cuda.synchronize()
+    train_steps = -(-len(timed) // bs)
+    t_tr = (time.perf_counter() - t1) / max(train_steps, 1)
+    D.barrier()
+    t2 = time.perf_counter()
+    pw, nw, dr = GatingArena(game, prev, new, args).playGames(arena_games, env_base=10**6)
+    torch.cuda.synchronize()
+    t_ar = time.perf_counter() - t2
+    return {"config": f"pooled examples of the timed batch ({n} examples from {world} rank(s)); "
+                      f"{train_steps} train steps of minibatch {bs} split over {world} rank(s) (DDP all-reduce, "
+                      f"clip 5.0, AdamW, dropout {args.dropout}, f32); gating arena {arena_games} games, "
+                      f"{arena_sims} sims, previous vs new net on dual trees, sharded",
+            "examples": n, "examples_ms": 1000.0 * t_ex, "train_ms_per_step": 1000.0 * t_tr,
+            "train_examples_per_s": bs / t_tr, "arena_s": t_ar, "arena_games_per_s": arena_games / t_ar,
+            "arena_tally_prev_new_draws": [pw, nw, dr]}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -165,6 +277,8 @@ def main():
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel event timing")
     ap.add_argument("--no-arena", action="store_true", help="skip the config-4 Arena leg")
     ap.add_argument("--no-train", action="store_true", help="skip the config-5 train-step leg")
+    ap.add_argument("--no-coach", action="store_true", help="skip the config-5 Coach-iteration leg")
+    ap.add_argument("--no-shape", action="store_true", help="skip the config-3 shape leg (2048 x 200)")
     ap.add_argument("--dist-backend", default=None, help="nccl (RCCL, default on GPUs) or gloo (rehearsal)")
     ap.add_argument("--groups", type=int, default=0,
                     help="game groups on their own streams (0: the engine's auto choice)")
@@ -239,6 +353,11 @@ def main():
         sums = tot[1:].clone()
         dist.all_reduce(sums, op=dist.ReduceOp.SUM)
         elapsed, exps, games = float(t_max[0]), float(sums[0]), float(sums[1])
+    coach = None
+    if not args.no_coach:
+        img = last_gather[0] if world > 1 else eng.pack_records(stream=stream)
+        coach = coach_leg(model, img, args.envs, 64, args.sims, world, seed=args.seed)
+        del img
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()
@@ -256,6 +375,8 @@ def main():
                    "envs_per_gpu": args.envs, "sims": args.sims, "cpuct": 1.5, "temp_threshold": 15,
                    "parallelism": f"games sharded over {world} GPU(s), RCCL all-gather of trajectories"},
         "episodes_per_s": games / elapsed,
+        "value_basis": "whole job: expansions of all GPUs / the slowest rank's time (the metric's per-GPU "
+                       "rate is expansions_per_s_per_gpu)",
         "expansions_per_s_per_gpu": value / world,
         "expansions_per_episode_batch": exps / args.steps,
         "game_groups": st["groups"],
@@ -278,30 +399,47 @@ def main():
         out["kernel_ms"] = {k: {"avg_ms": round(a, 5), "launches": n, "total_ms": round(t, 2)}
                             for k, (a, n, t) in per.items()}
         dom = max(per, key=lambda k: per[k][2])
-        if dom == "forward":
-            # algorithmic FLOP per launch = expansions predicted per launch x 3,320,576
-            exp_per_launch = exps / world / max(per["forward"][1], 1)
+        fwd = env = None
+        if "forward" in per and per["forward"][1]:
+            # k_forward (MFMA): algorithmic FLOP per launch = expansions predicted per launch x 3,320,576
+            exp_per_launch = exps / world / args.steps / max(per["forward"][1] / args.steps, 1)
             flop = PREDICT_FLOP * exp_per_launch
-            ach = flop / (per[dom][0] * 1e-3) / 1e12
+            ach = flop / (per["forward"][0] * 1e-3) / 1e12
             tr = measured_traffic(args)  # per-GPU configuration, so per-launch bytes hold at any N
-            out["roofline"] = {"kernel": "k_forward", "bound": "mfma", "achieved": ach,
-                               "peak": SPLIT_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": ach / SPLIT_PEAK_TFLOPS,
-                               "traffic": tr[0] if tr else None,
-                               "traffic_source": tr[1] if tr else None,
-                               "work_per_launch": f"{exp_per_launch:.0f} expansions x {PREDICT_FLOP} FLOP (f32)",
-                               "peak_basis": "f16 dense MFMA peak / 3: every f32 product runs as hi*hi + hi*lo + "
-                                             "lo*hi on fp16 planes with f32 accumulation",
-                               "limiter": "per-CU weight stream: each 16-row tile streams all 6.7 MB of weight "
-                                          "planes through its CU; MFMA issue and vector-memory streaming do not "
-                                          "overlap on a CU (tools/stream_bench.hip, DESIGN.md section 6)"}
-        else:
-            # env/MCTS kernels: algorithmic bytes = 4*S_scan + 16*D + 4*V_new + 364 per expansion
+            fwd = {"kernel": "k_forward", "bound": "mfma", "achieved": ach,
+                   "peak": SPLIT_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": ach / SPLIT_PEAK_TFLOPS,
+                   "traffic": tr[0] if tr else None,
+                   "traffic_source": tr[1] if tr else None,
+                   "work_per_launch": f"{exp_per_launch:.0f} expansions x {PREDICT_FLOP} FLOP (f32)",
+                   "peak_basis": "f16 dense MFMA peak / 3: every f32 product runs as hi*hi + hi*lo + "
+                                 "lo*hi on fp16 planes with f32 accumulation",
+                   "limiter": "per-CU weight stream: each 16-row tile streams all 6.7 MB of weight "
+                              "planes through its CU; MFMA issue and vector-memory streaming do not "
+                              "overlap on a CU (tools/stream_bench.hip, DESIGN.md section 6)"}
+            mf = measured_mfma(args)
+            if mf:
+                fwd["mfma_busy"] = {k: mf[k] for k in ("busy_frac", "formula", "source") if k in mf}
+        if "expand_backup_select" in per and per["expand_backup_select"][1]:
+            # k_expand_backup (HBM): algorithmic bytes = 4*S_scan + 16*D + 4*V_new + 364 per
+            # expansion, from the engine's own counters of the last batch, per launch
             scan_b = 4 * st["scanned"] + 16 * st["path_edges"] + 4 * st["vnew"] + 364 * st["expansions"]
             b = scan_b / max(st["sims"], 1)
-            ach = b / (per[dom][0] * 1e-3) / 1e9
-            out["roofline"] = {"kernel": "k_" + dom, "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS,
-                               "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "traffic": None,
-                               "work_per_launch": f"{b:.0f} algorithmic bytes"}
+            ach = b / (per["expand_backup_select"][0] * 1e-3) / 1e9
+            tr = measured_traffic(args, "expand")
+            env = {"kernel": "k_expand_backup", "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS,
+                   "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "traffic": tr[0] if tr else None,
+                   "traffic_source": tr[1] if tr else None,
+                   "work_per_launch": f"{b:.0f} algorithmic bytes = (4 x {st['scanned']} UCB entries scanned + "
+                                      f"16 x {st['path_edges']} path edges + 4 x {st['vnew']} new valid entries + "
+                                      f"364 x {st['expansions']} expansions) / {st['sims']} launches"}
+        if dom == "forward":
+            out["roofline"], out["roofline_env"] = fwd, env
+        else:
+            out["roofline"], out["roofline_mfma"] = env, fwd
+    if coach is not None:
+        out["coach"] = coach
+    if world == 1 and not args.no_shape:
+        out["config3_shape"] = shape_leg(net, seed=args.seed)
     if world == 1 and not args.no_arena:
         out["arena"] = arena_leg(net, seed=args.seed)
     if world == 1 and not args.no_train:

@@ -190,6 +190,45 @@ def test_mcts_arena_playgames_and_sequential_arena(Y):
     assert res == o["result"][0]
 
 
+def test_mcts_plugin_resets_its_tree_for_a_new_game(Y):
+    """One MCTS object over two games (Arena.playGames reuses pmcts / nmcts, Coach.py:120-125):
+    when the next root has a lower round the plugin resets its tree
+    and plays the second game exactly as a fresh MCTS object does; the raw C call refuses the
+    lower round without the reset."""
+    from yacht_amd._lib import YkError, call
+    from yacht_amd.arena import Arena, RandomYachtPlayer
+    from yacht_amd.game import YachtGame
+    from yacht_amd.mcts import MCTS
+    from yacht_amd.nnet import HashPriorNet
+    from yacht_amd.utils import dotdict
+    args = dotdict(numMCTSSims=6, cpuct=1.5)
+
+    def play(game, mcts):
+        return Arena(lambda x: int(np.argmax(mcts.getActionProb(x, temp=0))), RandomYachtPlayer(game).play,
+                     game).playGame(), game.rng.ctr
+
+    g1 = YachtGame(seed=12, env_id=300)
+    shared = MCTS(g1, HashPriorNet(g1), args)
+    play(g1, shared)                     # game 1 leaves a tree of late rounds behind
+    g1.rng.env, g1.rng.ctr = 301, 0      # game 2 on its own stream
+    reused = play(g1, shared)
+    g2 = YachtGame(seed=12, env_id=301)
+    fresh = play(g2, MCTS(g2, HashPriorNet(g2), args))
+    assert reused == fresh
+    # the C ABI itself: a lower-round root without yk_mcts_reset is an engine state error
+    import torch as T
+    from yacht_amd import kernels as K
+    from yacht_amd.state import ACTION_SIZE, pack
+    eng = shared._eng()
+    late = K.states_to_device(pack(g1.getInitBoard()))
+    counts = T.zeros((1, ACTION_SIZE), dtype=T.int32, device="cuda")
+    env = T.tensor([301], dtype=T.int32, device="cuda")
+    ctr = T.tensor([0], dtype=T.int64, device="cuda")
+    with pytest.raises(YkError):
+        call("yk_mcts_search", eng.handle, late.data_ptr(), 12, env.data_ptr(), ctr.data_ptr(), 2,
+             counts.data_ptr(), 0)
+
+
 def test_greedy_heuristic_kernel_matches_reference(Y, golden):
     """yk_greedy_action on all 11,403 fixture states against the reference GreedyYachtPlayer's
     choices (tests/golden/greedy.npz) and the C restatement."""

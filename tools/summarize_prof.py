@@ -26,6 +26,18 @@ for c in ("FETCH_SIZE", "WRITE_SIZE"):
     for k, v in vals.items():
         out.setdefault("pmc", {}).setdefault(k, {})[c + "_KiB_mean"] = sum(v) / len(v)
         out["pmc"][k]["launches"] = len(v)
+f = glob.glob(os.path.join(d, "MFMA", "**", "*counter_collection.csv"), recursive=True)
+if f:
+    acc = defaultdict(lambda: defaultdict(list))
+    for r in csv.DictReader(open(f[0])):
+        acc[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    for k, cs in acc.items():
+        m = {c: sum(v) / len(v) for c, v in cs.items()}
+        e = out.setdefault("pmc", {}).setdefault(k, {})
+        e.update({c + "_mean": x for c, x in m.items()})
+        if m.get("GRBM_GUI_ACTIVE"):
+            # GRBM_GUI_ACTIVE is summed over the 8 XCDs (MI355X_MICROARCH.md, DVFS); 256 CUs x 4 SIMDs
+            e["mfma_busy_frac"] = m.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) / (m["GRBM_GUI_ACTIVE"] / 8 * 1024)
 for k, v in out.get("pmc", {}).items():
     if "FETCH_SIZE_KiB_mean" in v and "WRITE_SIZE_KiB_mean" in v:
         v["hbm_bytes_per_launch"] = 1024 * (2 * v["FETCH_SIZE_KiB_mean"] + v["WRITE_SIZE_KiB_mean"])
