@@ -22,7 +22,7 @@ for v in "$@"; do
     *) bash tools/variant_lib.sh "$n" $f > /dev/null || exit 3; LIB[$n]=/tmp/yk_$n/libyacht_hip.so; ARGS[$n]="" ;;
   esac
 done
-B="python -u bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-arena --no-train"
+B="python -u bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-arena --no-train --no-coach --no-shape"
 for r in $(seq 1 "$R"); do
   for n in "${names[@]}"; do
     YK_LIB_PATH=${LIB[$n]} timeout -k 10 120 $B ${ARGS[$n]} > gpurun_out/ab_${n}_$r.json 2> gpurun_out/ab_${n}_$r.err || exit $?

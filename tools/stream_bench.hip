@@ -366,7 +366,8 @@ int main(int argc, char** argv) {
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
-    const int G = 256, it = 50;
+    const int it = 50;
+    int G = 256;
     auto run = [&](const char* name, auto kern) {
         for (int i = 0; i < 5; i++) hipLaunchKernelGGL(kern, dim3(G), dim3(NTHR), 0, 0, w, n4, out);
         hipEventRecord(a);
@@ -378,9 +379,19 @@ int main(int argc, char** argv) {
         const double us = 1000.0 * ms / it;
         unsigned long long clk[4];
         hipMemcpyFromSymbol(clk, HIP_SYMBOL(g_clk), sizeof(clk));
-        printf("%-28s %8.2f us per launch  %6.1f GB/s per CU  %6.2f TB/s from L2  clock %.2f GHz\n", name, us,
+        printf("G=%3d %-28s %8.2f us per launch  %6.1f GB/s per CU  %6.2f TB/s from L2  clock %.2f GHz\n", G, name, us,
                n4 * 16 / (us * 1e3), n4 * 16.0 * G / (us * 1e6), clk[1] ? 0.1 * clk[0] / clk[1] : 0.0);
     };
+    if (argc > 2) {  // grid sweep: is the per-CU rate of a shared weight set a per-CU or an L2-side limit?
+        for (int g : {256, 192, 128, 96, 64, 32}) {
+            G = g;
+            run("vgpr  D=8", k_vgpr<8>);
+            run("glds  8 waves", k_glds<8>);
+            run("f16x2 mfma only", k_f16_only);
+            run("f16x2 ring R=8", k_f16_ring<8>);
+        }
+        return 0;
+    }
     run("vgpr  D=4", k_vgpr<4>);
     run("vgpr  D=8", k_vgpr<8>);
     run("vgpr  D=16", k_vgpr<16>);

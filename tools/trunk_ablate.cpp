@@ -46,13 +46,13 @@ int main(int argc, char** argv) {
         printf("  total     %9.0f (max %9.0f)\n", s / nb, mx);
         // block 2 detail (16 fc1 GEMM, 17 LN1 vec+store+barrier, 18 LN1 pass, 19 fc2 GEMM,
         // 20 barrier, 21 store+barrier) and the end phase (22 tail barrier, 23 v store+barrier)
-        const int det[][2] = {{4, 16}, {16, 17}, {17, 18}, {18, 19}, {19, 20}, {20, 21}, {21, 5}, {14, 22}, {22, 23}, {23, 15}};
-        const char* dn[] = {"b2.fc1", "b2.st1", "b2.ln1", "b2.fc2", "b2.bar", "b2.st2", "b2.ln2", "tailbar", "vstore", "vfinal"};
+        const int det[][2] = {{4, 16}, {16, 13}, {13, 22}, {22, 17}, {18, 19}, {19, 20}, {20, 5}, {23, 15}};
+        const char* dn[] = {"b2.fc1", "b2.ep1st", "b2.ep1bar", "b2.ep1app", "b2.fc2", "b2.ep2", "b2.rest", "vfinal"};
         for (int w = 0; w < 8; w++) {  // per-wave end of the policy head, relative to the heads LN stamp
             double a = 0; for (int b = 0; b < nb; b++) a += (double)(t[b * 32 + 24 + w] - t[b * 32 + 9]);
             printf("  pi.w%d    %9.0f\n", w, a / nb);
         }
-        for (int k = 0; k < 10; k++) {
+        for (int k = 0; k < 8; k++) {
             double a = 0; for (int b = 0; b < nb; b++) a += (double)(t[b * 32 + det[k][1]] - t[b * 32 + det[k][0]]);
             printf("  %-9s %9.0f\n", dn[k], a / nb);
         }
