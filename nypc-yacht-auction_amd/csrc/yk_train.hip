@@ -176,41 +176,50 @@ __global__ void k_heads_fwd(const float* Hh, const float* gp, const float* bp, c
         Av[(long)row * H + c0 + i] = silu_f(y[i] * gv[c0 + i] + bv[c0 + i]);
     }
 }
-// v head tail + both losses + the output gradients.  One wave per row.
+// v head tail + both losses + the output gradients.  One 256-thread workgroup per row (13 logits
+// per lane: four times the memory parallelism of a wave per row); wave 0 also does the v head.
 //   Zv1 += bv1 (saved); v = tanh(silu(Zv1) . wv2 + bv2); mse_i = (v - z)^2
 //   logits += bpi; ce_i = lse - logit[t]; dlogits = (softmax - onehot(t)) / B
 //   dzv2 = vw * 2 (v - z) / B * (1 - v^2); dZv1 = dzv2 wv2 silu'(Zv1)
-constexpr int LOSS_NV = (ASIZE + 63) / 64;  // logits per lane
-__global__ void k_loss(const float* logits, const float* bpi, float* Zv1, const float* bv1, const float* wv2,
-                       const float* bv2, const int32_t* tgt, const float* vt, float* dlogits, float* dZv1, float* dzv2,
-                       float* v2prod, float* vout, double* loss_acc, int B, int A, float vw) {
-    const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+constexpr int LOSS_T = 256;
+constexpr int LOSS_NV = (ASIZE + LOSS_T - 1) / LOSS_T;  // logits per thread
+__global__ __launch_bounds__(LOSS_T) void k_loss(const float* logits, const float* bpi, float* Zv1, const float* bv1,
+                                                 const float* wv2, const float* bv2, const int32_t* tgt,
+                                                 const float* vt, float* dlogits, float* dZv1, float* dzv2,
+                                                 float* v2prod, float* vout, float2* lrow, int B, int A, float vw) {
+    __shared__ float red[2][LOSS_T / 64];
+    const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     if (row >= B) return;
     const float* z = logits + (long)row * A;
     float x[LOSS_NV];
     float m = -INFINITY;
 #pragma unroll
     for (int k = 0; k < LOSS_NV; k++) {
-        const int a = lane + 64 * k;
+        const int a = tid + LOSS_T * k;
         x[k] = a < A ? z[a] + bpi[a] : -INFINITY;
         m = fmaxf(m, x[k]);
     }
     m = wmax(m);
+    if (lane == 0) red[0][w] = m;
+    __syncthreads();
+    m = fmaxf(fmaxf(red[0][0], red[0][1]), fmaxf(red[0][2], red[0][3]));
     float se = 0.f;
 #pragma unroll
     for (int k = 0; k < LOSS_NV; k++) se += expf(x[k] - m);
     se = wsum(se);
+    if (lane == 0) red[1][w] = se;
+    __syncthreads();
+    se = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
     const float lse = m + logf(se);
     const int t = tgt[row];
     const float invB = 1.0f / (float)B;
-    float zt = 0.f;
 #pragma unroll
     for (int k = 0; k < LOSS_NV; k++) {
-        const int a = lane + 64 * k;
+        const int a = tid + LOSS_T * k;
         if (a < A) dlogits[(long)row * A + a] = (expf(x[k] - lse) - (a == t ? 1.0f : 0.0f)) * invB;
-        if (a == t) zt = x[k];
     }
-    zt = wsum(zt);  // exactly one lane holds the target logit
+    if (w != 0) return;
+    const float zt = z[t] + bpi[t];  // the target logit (the same sum as x[k] where a == t)
     // value head tail (128 hidden, 2 per lane)
     float s = 0.f, zz[2];
 #pragma unroll
@@ -230,11 +239,10 @@ __global__ void k_loss(const float* logits, const float* bpi, float* Zv1, const 
         dZv1[(long)row * 128 + c] = dv * wv2[c] * silu_grad(zz[k]);
         v2prod[(long)row * 128 + c] = dv * silu_f(zz[k]);  // rows of dL/d v_head.4.weight
     }
-    if (lane == 0) {
+    if (lane == 0) {  // the per-row losses; k_colsums sums them (no contended atomics)
         dzv2[row] = dv;
         vout[row] = v;
-        atomicAdd(&loss_acc[0], (double)(lse - zt));
-        atomicAdd(&loss_acc[1], (double)(e * e));
+        lrow[row] = make_float2(lse - zt, e * e);
     }
 }
 
@@ -377,8 +385,10 @@ __global__ void k_gather(const yk_state_t* states, const int32_t* tgt_all, const
         vt[i] = v_all[src];
     }
 }
-// sum of squares of the gradient buffer -> acc (double)
-__global__ void k_sqnorm(const float* g, long n, double* acc) {
+// sum of squares of the gradient buffer: one double partial per workgroup (no atomics); k_adamw
+// adds the SQ_BLOCKS partials in a fixed order
+constexpr int SQ_BLOCKS = 1024;
+__global__ void k_sqnorm(const float* g, long n, double* part_out) {
     __shared__ double part[TPB / 64];
     double s = 0.0;
     for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
@@ -392,14 +402,34 @@ __global__ void k_sqnorm(const float* g, long n, double* acc) {
     if (threadIdx.x == 0) {
         double t = 0.0;
         for (int w = 0; w < TPB / 64; w++) t += part[w];
-        atomicAdd(acc, t);
+        part_out[blockIdx.x] = t;
     }
 }
 // clip_grad_norm_ (coef = min(1, max_norm / (norm + 1e-6)), NNet.py:152-153) + AdamW
 // (torch single-tensor AdamW: decoupled decay, bias-corrected moments)
-__global__ void k_adamw(float* p, float* g, float* m, float* v, long n, const double* sq, float max_norm, float lr,
-                        float wd, float b1, float b2, float eps, float step_size, float bc2_sqrt) {
-    const float norm = (float)sqrt(*sq);
+__global__ void k_adamw(float* p, float* g, float* m, float* v, long n, const double* sq_part, double* sq_out,
+                        float max_norm, float lr, float wd, float b1, float b2, float eps, float step_size,
+                        float bc2_sqrt) {
+    __shared__ double red[TPB / 64];
+    __shared__ double sq_total;
+    {  // every workgroup adds the SQ_BLOCKS partials in the same fixed order
+        static_assert(SQ_BLOCKS % TPB == 0, "partials per thread");
+        double t = 0.0;
+#pragma unroll
+        for (int k = 0; k < SQ_BLOCKS / TPB; k++) t += sq_part[threadIdx.x + TPB * k];
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) t += __shfl_xor(t, o, 64);
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = t;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double u = 0.0;
+            for (int k = 0; k < TPB / 64; k++) u += red[k];
+            sq_total = u;
+            if (blockIdx.x == 0) *sq_out = u;
+        }
+        __syncthreads();
+    }
+    const float norm = (float)sqrt(sq_total);
     float coef = max_norm / (norm + 1e-6f);
     coef = coef > 1.0f ? 1.0f : coef;
     const float decay = 1.0f - lr * wd;
@@ -446,7 +476,10 @@ struct yk_trainer {
     ColJob* jobs = nullptr;
     int2* tiles = nullptr;
     int ntiles = 0;
-    double* acc = nullptr;  // [0] ce sum, [1] mse sum, [2] grad sq norm
+    double* acc = nullptr;  // [0] ce sum, [1] mse sum (unused), [2] grad sq norm
+    double* sqpart = nullptr;  // k_sqnorm partials
+    float2* lrow = nullptr;    // per-row (ce, squared value error) of the last batch
+    float* lsum = nullptr;     // their column sums (k_colsums)
     double host_loss[3] = {0, 0, 0};
 };
 
@@ -489,7 +522,6 @@ int step_impl(yk_trainer* t, const yk_state_t* states, const int32_t* targets, c
     auto Gt = [&](int k) { return t->G + t->off[k]; };
     const dim3 rows((B + 3) / 4), wave4(256);
     int rc;
-    YK_HIP(hipMemsetAsync(t->acc, 0, sizeof(double) * 3, s));
     hipLaunchKernelGGL(k_gather, dim3((B * 64 + 255) / 256), dim3(256), 0, s, states, targets, values, idx, t->X, t->tgt,
                        t->vt, B);
     YK_LAUNCHED();
@@ -514,14 +546,14 @@ int step_impl(yk_trainer* t, const yk_state_t* states, const int32_t* targets, c
     YK_LAUNCHED();
     if ((rc = gemm_rm(t, false, true, B, A, H, t->Api, H, Pt(t_head(NB, 2)), H, t->logits, A, 0.f))) return rc;
     if ((rc = gemm_rm(t, false, true, B, 128, H, t->Av, H, Pt(t_head(NB, 6)), H, t->Zv1, 128, 0.f))) return rc;
-    hipLaunchKernelGGL(k_loss, rows, wave4, 0, s, t->logits, Pt(t_head(NB, 3)), t->Zv1, Pt(t_head(NB, 7)),
+    hipLaunchKernelGGL(k_loss, dim3(B), dim3(LOSS_T), 0, s, t->logits, Pt(t_head(NB, 3)), t->Zv1, Pt(t_head(NB, 7)),
                        Pt(t_head(NB, 8)), Pt(t_head(NB, 9)), t->tgt, t->vt, t->dlogits, t->dZv1, t->dzv2, t->v2prod,
-                       t->vout, t->acc, B, A, t->cfg.vloss_weight);
+                       t->vout, t->lrow, B, A, t->cfg.vloss_weight);
     YK_LAUNCHED();
     // ---- backward: heads (bias / LayerNorm gradients are column sums, taken at the end)
     if ((rc = gemm_rm(t, true, false, A, H, B, t->dlogits, A, t->Api, H, Gt(t_head(NB, 2)), H, 0.f))) return rc;
-    if ((rc = gemm_rm(t, false, false, B, H, A, t->dlogits, A, Pt(t_head(NB, 2)), H, t->dA, H, 0.f))) return rc;
     if ((rc = gemm_rm(t, true, false, 128, H, B, t->dZv1, 128, t->Av, H, Gt(t_head(NB, 6)), H, 0.f))) return rc;
+    if ((rc = gemm_rm(t, false, false, B, H, A, t->dlogits, A, Pt(t_head(NB, 2)), H, t->dA, H, 0.f))) return rc;
     if ((rc = gemm_rm(t, false, false, B, H, 128, t->dZv1, 128, Pt(t_head(NB, 6)), H, t->dAv, H, 0.f))) return rc;
     hipLaunchKernelGGL(k_heads_bwd<VPL>, rows, wave4, 0, s, Hh, Pt(t_head(NB, 0)), Pt(t_head(NB, 1)), Pt(t_head(NB, 4)),
                        Pt(t_head(NB, 5)), t->mup, t->rsp, t->muv, t->rsv, t->dA, t->dAv, t->dH, t->rgp, t->rbp, t->rgv,
@@ -532,12 +564,12 @@ int step_impl(yk_trainer* t, const yk_state_t* states, const int32_t* targets, c
         hipLaunchKernelGGL(k_blk_bwd<VPL>, rows, wave4, 0, s, t->dH, (const uint8_t*)nullptr, 0.f, t->U2[b],
                            Pt(t_blk(b, 6)), t->mu2[b], t->rs2[b], t->dU2[b], t->rg2[b], t->rb2[b], B);
         YK_LAUNCHED();
-        if ((rc = gemm_rm(t, true, false, H, H, B, t->dU2[b], H, t->R1[b], H, Gt(t_blk(b, 4)), H, 0.f))) return rc;
+            if ((rc = gemm_rm(t, true, false, H, H, B, t->dU2[b], H, t->R1[b], H, Gt(t_blk(b, 4)), H, 0.f))) return rc;
         if ((rc = gemm_rm(t, false, false, B, H, H, t->dU2[b], H, Pt(t_blk(b, 4)), H, t->dT, H, 0.f))) return rc;  // dR1
         hipLaunchKernelGGL(k_blk_bwd<VPL>, rows, wave4, 0, s, t->dT, t->mask1[b], p, t->U1[b], Pt(t_blk(b, 2)), t->mu1[b],
                            t->rs1[b], t->dU1[b], t->rg1[b], t->rb1[b], B);
         YK_LAUNCHED();
-        if ((rc = gemm_rm(t, true, false, H, H, B, t->dU1[b], H, t->Hs[b], H, Gt(t_blk(b, 0)), H, 0.f))) return rc;
+            if ((rc = gemm_rm(t, true, false, H, H, B, t->dU1[b], H, t->Hs[b], H, Gt(t_blk(b, 0)), H, 0.f))) return rc;
         // dH_b = dH_{b+1} (residual) + dU1 . W1
         if ((rc = gemm_rm(t, false, false, B, H, H, t->dU1[b], H, Pt(t_blk(b, 0)), H, t->dH, H, 1.f))) return rc;
     }
@@ -629,6 +661,9 @@ int yk_trainer_create(yk_trainer_t** out, int H, int NB, const float* const* par
         TA(t->rg2[b], Bm * HH); TA(t->rb2[b], Bm * HH);
     }
     TA(t->acc, 3);
+    TA(t->sqpart, SQ_BLOCKS);
+    TA(t->lrow, Bm);
+    TA(t->lsum, 2);
     // the column-sum jobs: (row buffer, gradient tensor, width)
     std::vector<ColJob> jobs;
     if (rc == YK_OK) {
@@ -650,6 +685,7 @@ int yk_trainer_create(yk_trainer_t** out, int H, int NB, const float* const* par
             jobs.push_back({t->rb2[b], G(t_blk(b, 7)), H});
         }
         jobs.push_back({t->dZ0, G(T_BIN), H});
+        jobs.push_back({reinterpret_cast<const float*>(t->lrow), t->lsum, 2});  // the batch's two loss sums
         jobs.push_back({t->rg0, G(T_GIN), H});
         jobs.push_back({t->rb0, G(T_BEIN), H});
     }
@@ -677,6 +713,8 @@ int yk_trainer_create(yk_trainer_t** out, int H, int NB, const float* const* par
     (void)hipMemset(t->M, 0, sizeof(float) * o);
     (void)hipMemset(t->V, 0, sizeof(float) * o);
     (void)hipMemset(t->G, 0, sizeof(float) * o);
+    (void)hipMemset(t->acc, 0, sizeof(double) * 3);
+    (void)hipMemset(t->lsum, 0, sizeof(float) * 2);
     if (hipDeviceSynchronize() != hipSuccess) {
         yk_trainer_destroy(t);
         return YK_ERR_HIP;
@@ -723,9 +761,9 @@ int yk_trainer_apply(yk_trainer_t* t, void* stream) {
     const double b1 = t->cfg.beta1, b2 = t->cfg.beta2, st = (double)t->step;
     const double bc1 = 1.0 - std::pow(b1, st), bc2 = 1.0 - std::pow(b2, st);
     const float step_size = (float)(t->cfg.lr / bc1), bc2_sqrt = (float)std::sqrt(bc2);
-    hipLaunchKernelGGL(k_sqnorm, dim3(1024), dim3(TPB), 0, s, t->G, t->nparams, t->acc + 2);
+    hipLaunchKernelGGL(k_sqnorm, dim3(SQ_BLOCKS), dim3(TPB), 0, s, t->G, t->nparams, t->sqpart);
     YK_LAUNCHED();
-    hipLaunchKernelGGL(k_adamw, dim3(2048), dim3(TPB), 0, s, t->P, t->G, t->M, t->V, t->nparams, t->acc + 2,
+    hipLaunchKernelGGL(k_adamw, dim3(2048), dim3(TPB), 0, s, t->P, t->G, t->M, t->V, t->nparams, t->sqpart, t->acc + 2,
                        t->cfg.max_grad_norm, t->cfg.lr, t->cfg.weight_decay, t->cfg.beta1, t->cfg.beta2, t->cfg.eps,
                        step_size, bc2_sqrt);
     YK_LAUNCHED();
@@ -743,6 +781,10 @@ int yk_trainer_losses(yk_trainer_t* t, double* out) {
     if (!t || !out) return YK_ERR_ARG;
     YK_HIP(hipDeviceSynchronize());
     YK_HIP(hipMemcpy(out, t->acc, sizeof(double) * 3, hipMemcpyDeviceToHost));
+    float ls[2];
+    YK_HIP(hipMemcpy(ls, t->lsum, sizeof(ls), hipMemcpyDeviceToHost));
+    out[0] = ls[0];
+    out[1] = ls[1];
     return YK_OK;
 }
 

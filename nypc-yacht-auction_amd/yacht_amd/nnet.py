@@ -186,6 +186,7 @@ class NNetWrapper:
         rank, world = D.rank_world()
         n = states.shape[0]
         bs = self.args.batch_size
+        rows = bs * world if world > 1 and self.args.get("ddp_batch", "split") == "per_rank" else bs
         vw = self.args.get("vloss_weight", 1.0)
         g = torch.Generator(device="cuda")
         g.manual_seed(int(self.args.get("seed", 0)) + 1000003 * tr.step_count)
@@ -193,8 +194,8 @@ class NNetWrapper:
             perm = torch.randperm(n, generator=g, device="cuda").to(torch.int32)
             report = verbose and (epoch % 5 == 0 or epoch == self.args.epochs - 1)
             total, count = 0.0, 0
-            for i in range(0, n, bs):
-                idx = perm[i:i + bs]
+            for i in range(0, n, rows):
+                idx = perm[i:i + rows]
                 if world == 1:
                     tr.step(states, targets, values, idx=idx)
                     b = idx.numel()

@@ -138,6 +138,11 @@ def _coach_worker(rank, world, port, ckdir, out):
     coach.nnet.train([shard], verbose=False)
     out[f"p{rank}"] = {k: v.numpy().copy() for k, v in coach.nnet.nnet.state_dict().items()}
     out[f"pit{rank}"] = GatingArena(game, coach.pnet, coach.nnet, args).playGames(args.arenaCompare, env_base=900)
+    # DDP weak scaling: every rank its own batch_size rows (a global minibatch of 2 x batch_size)
+    wk = NNetWrapper(game, dotdict(args, ddp_batch="per_rank"))
+    wk.nnet.load_state_dict(coach.pnet.nnet.state_dict())
+    wk.train([shard], verbose=False)
+    out[f"pr{rank}"] = ({k: v.numpy().copy() for k, v in wk.nnet.state_dict().items()}, wk._trainer().step_count)
     # the loop itself (files written by rank 0, read back by every rank)
     coach.learn()
     out[f"learn{rank}"] = (coach.last_pit, len(coach.trainExamplesHistory[-1]),
@@ -185,6 +190,16 @@ def test_coach_iteration_two_ranks_sharing_gpu0(Y, tmp_path):
     # 2 lr on a summation-order change; everything else agrees to f32 rounding
     assert np.linalg.norm(a - b) / np.linalg.norm(b) < 1e-4
     assert (np.abs(a - b) > 1e-5).mean() < 1e-3
+    # per_rank: the single-process train at batch 2 x batch_size, in half the steps
+    pr0, pr1 = out["pr0"], out["pr1"]
+    assert all(np.array_equal(pr0[0][k], pr1[0][k]) for k in pr0[0])
+    wide = NNetWrapper(game, dotdict(args, batch_size=2 * args.batch_size))
+    wide.nnet.load_state_dict(net0.nnet.state_dict())
+    wide.train([single], verbose=False)
+    assert pr0[1] == wide._trainer().step_count == 2 * -(-len(single) // (2 * args.batch_size))
+    a = np.concatenate([pr0[0][k].reshape(-1) for k in pr0[0]]).astype(np.float64)
+    b = np.concatenate([wide.nnet.state_dict()[k].numpy().reshape(-1) for k in pr0[0]]).astype(np.float64)
+    assert np.linalg.norm(a - b) / np.linalg.norm(b) < 1e-4 and (np.abs(a - b) > 1e-5).mean() < 1e-3
     # the sharded gating arena's tally is the single-GPU arena's
     pit = GatingArena(game, net0, coach.nnet, args).playGames(args.arenaCompare, env_base=900)
     assert out["pit0"] == out["pit1"]

@@ -220,7 +220,7 @@ def test_coach_learn_iteration_and_resume(T, tmp_path):
     args = dotdict(numIters=1, numEps=8, tempThreshold=15, updateThreshold=0.55, maxlenOfQueue=200000,
                    numMCTSSims=4, arenaCompare=2, cpuct=1.5, checkpoint=d, load_folder_file=(d, "checkpoint_0.pth.tar"),
                    numItersForTrainExamplesHistory=5, lr=2e-3, weight_decay=1e-4, epochs=1, batch_size=64,
-                   vloss_weight=1.5, cuda=True, hidden=64, nblocks=1, dropout=0.3)
+                   vloss_weight=1.5, cuda=True, hidden=64, nblocks=1, dropout=0.3, examples_format="both")
     game = YachtGame(seed=3, env_id=0)
     c = Coach(game, NNetWrapper(game, args), args)
     c.learn()
