@@ -225,6 +225,69 @@ __device__ __forceinline__ void layernorm(float (&x)[VPL], const float* g, const
     for (int i = 0; i < VPL; i++) x[i] = (x[i] - mean) * rstd * g[c0 + i] + b[c0 + i];
 }
 
+// Packed forms of the row passes (two floats per VALU instruction: v_pk_add/mul_f32,
+// v_cvt_pk_f16_f32) for even VPL: the same operations per element as silu / layernorm /
+// put_planes, except that each lane's partial sums pair its values ((x0 + x2) + (x1 + x3)).
+// The trunk's LayerNorm phases are VALU-bound and on the forward's critical path.
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2v ld2(const float* p) { return *reinterpret_cast<const f2v*>(p); }
+__device__ __forceinline__ f2v silu2(f2v u) {
+    const f2v a = u * -1.4426950408889634f;  // exp(-u) = exp2(-u log2 e)
+    f2v d, rc;
+    d.x = __builtin_amdgcn_exp2f(a.x);
+    d.y = __builtin_amdgcn_exp2f(a.y);
+    d = d + 1.0f;
+    rc.x = __builtin_amdgcn_rcpf(d.x);
+    rc.y = __builtin_amdgcn_rcpf(d.y);
+    return u * rc;
+}
+// LayerNorm of a wave's R rows at once, NP value pairs per lane: one pass of shifted sums
+// (shift = the row's first value, so the variance E[(x-k)^2] - E[x-k]^2 does not cancel), the 2R
+// wave reductions independent of each other (their DPP latencies overlap), rstd by v_rsq_f32.
+template <int NP, int R>
+__device__ __forceinline__ void layernorm2(f2v (&x)[R][NP], const float* g, const float* b, int c0, int H) {
+    float sh[R], s[R], q[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        sh[r] = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, x[r][0].x)));
+        f2v a = {0.f, 0.f}, a2 = {0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < NP; i++) {
+            const f2v d = x[r][i] - sh[r];
+            a = a + d;
+            a2 = a2 + d * d;
+        }
+        s[r] = a.x + a.y;
+        q[r] = a2.x + a2.y;
+    }
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        s[r] = wave_sum(s[r]);
+        q[r] = wave_sum(q[r]);
+    }
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const float m = s[r] / (float)H;
+        const float var = fmaxf(q[r] / (float)H - m * m, 0.f);
+        const float rstd = __builtin_amdgcn_rsqf(var + 1e-5f);
+        const float mean = sh[r] + m;
+#pragma unroll
+        for (int i = 0; i < NP; i++) x[r][i] = (x[r][i] - mean) * rstd * ld2(g + c0 + 2 * i) + ld2(b + c0 + 2 * i);
+    }
+}
+template <int NP>
+__device__ __forceinline__ void put_planes2(_Float16* planes, int sa, int r, int c, const f2v (&x)[NP]) {
+#pragma unroll
+    for (int i = 0; i < NP; i++) {
+        const h2v h = __builtin_convertvector(x[i], h2v);
+        const f2v back = __builtin_convertvector(h, f2v);
+        const h2v l = __builtin_convertvector((x[i] - back) * SPLIT, h2v);
+        *reinterpret_cast<h2v*>(planes + r * sa + c + 2 * i) = h;
+        *reinterpret_cast<h2v*>(planes + ROWS * sa + r * sa + c + 2 * i) = l;
+    }
+}
+
 // Policy head chunks.  The workgroup computes the tiles of a list (every real tile, or the union
 // of its rows' valid columns, TL in LDS); wave w owns list entries w + WAVES k, PCH of them per
 // chunk, NTL <= PCH in a wave's last chunk.  The ring (RD slices of PCH tiles) streams across
@@ -567,14 +630,26 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
         if (gw) store_acc<NT>(T, LD, nt0, acc, nullptr);
         lds_barrier();  // T complete; every wave is done reading x's planes
         if (b == 2) TSTAMP(17);
+        if constexpr (VPL % 2 == 0) {
+            f2v x[RPW][VPL / 2];
 #pragma unroll
-        for (int rr = 0; rr < RPW; rr++) {
-            const int r = wave * RPW + rr;
-            float x[VPL];
+            for (int rr = 0; rr < RPW; rr++)
 #pragma unroll
-            for (int i = 0; i < VPL; i++) x[i] = silu(T[r * LD + c0 + i] + VB[c0 + i]);
-            layernorm<VPL>(x, VB + H, VB + 2 * H, c0, H);
-            put_planes<VPL>(P, SA, r, c0, x);  // fc2's input
+                for (int i = 0; i < VPL / 2; i++)
+                    x[rr][i] = silu2(ld2(T + (wave * RPW + rr) * LD + c0 + 2 * i) + ld2(VB + c0 + 2 * i));
+            layernorm2<VPL / 2, RPW>(x, VB + H, VB + 2 * H, c0, H);
+#pragma unroll
+            for (int rr = 0; rr < RPW; rr++) put_planes2<VPL / 2>(P, SA, wave * RPW + rr, c0, x[rr]);  // fc2's input
+        } else {
+#pragma unroll
+            for (int rr = 0; rr < RPW; rr++) {
+                const int r = wave * RPW + rr;
+                float x[VPL];
+#pragma unroll
+                for (int i = 0; i < VPL; i++) x[i] = silu(T[r * LD + c0 + i] + VB[c0 + i]);
+                layernorm<VPL>(x, VB + H, VB + 2 * H, c0, H);
+                put_planes<VPL>(P, SA, r, c0, x);  // fc2's input
+            }
         }
         lds_barrier();
         if (b == 2) TSTAMP(18);
@@ -586,19 +661,39 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
         if (gw) store_acc<NT>(T, LD, nt0, acc, nullptr);
         lds_barrier();  // T complete; every wave is done reading h's planes
         if (b == 2) TSTAMP(21);
+        if constexpr (VPL % 2 == 0) {
+            f2v x[RPW][VPL / 2];
 #pragma unroll
-        for (int rr = 0; rr < RPW; rr++) {
-            const int r = wave * RPW + rr;
-            float x[VPL];
+            for (int rr = 0; rr < RPW; rr++)
 #pragma unroll
-            for (int i = 0; i < VPL; i++) x[i] = silu(T[r * LD + c0 + i] + VB[3 * H + c0 + i]);
-            layernorm<VPL>(x, VB + 4 * H, VB + 5 * H, c0, H);
+                for (int i = 0; i < VPL / 2; i++)
+                    x[rr][i] = silu2(ld2(T + (wave * RPW + rr) * LD + c0 + 2 * i) + ld2(VB + 3 * H + c0 + 2 * i));
+            layernorm2<VPL / 2, RPW>(x, VB + 4 * H, VB + 5 * H, c0, H);
 #pragma unroll
-            for (int i = 0; i < VPL; i++) {
-                x[i] += X[r * LD + c0 + i];
-                X[r * LD + c0 + i] = x[i];
+            for (int rr = 0; rr < RPW; rr++) {
+                const int r = wave * RPW + rr;
+#pragma unroll
+                for (int i = 0; i < VPL / 2; i++) {
+                    x[rr][i] = x[rr][i] + ld2(X + r * LD + c0 + 2 * i);
+                    *reinterpret_cast<f2v*>(X + r * LD + c0 + 2 * i) = x[rr][i];
+                }
+                if (b + 1 < net.NB) put_planes2<VPL / 2>(P, SA, r, c0, x[rr]);  // the next fc1's input
             }
-            if (b + 1 < net.NB) put_planes<VPL>(P, SA, r, c0, x);  // the next fc1's input
+        } else {
+#pragma unroll
+            for (int rr = 0; rr < RPW; rr++) {
+                const int r = wave * RPW + rr;
+                float x[VPL];
+#pragma unroll
+                for (int i = 0; i < VPL; i++) x[i] = silu(T[r * LD + c0 + i] + VB[3 * H + c0 + i]);
+                layernorm<VPL>(x, VB + 4 * H, VB + 5 * H, c0, H);
+#pragma unroll
+                for (int i = 0; i < VPL; i++) {
+                    x[i] += X[r * LD + c0 + i];
+                    X[r * LD + c0 + i] = x[i];
+                }
+                if (b + 1 < net.NB) put_planes<VPL>(P, SA, r, c0, x);  // the next fc1's input
+            }
         }
         lds_barrier();
         if (b < 6) TSTAMP(3 + b);
