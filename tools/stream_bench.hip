@@ -227,7 +227,8 @@ __global__ __launch_bounds__(NTHR) void k_split(const float4* __restrict__ w, lo
 }
 
 // role split variants: MODE 0 = MFMA waves + VGPR-load stream waves; MODE 1 = VALU-FMA waves
-// + LDS-DMA stream waves; MODE 2 = VALU-FMA waves alone
+// + LDS-DMA stream waves; MODE 2 = VALU-FMA waves alone; MODE 3 = VALU-FMA waves + VGPR-load
+// stream waves; MODE 4 = VGPR-load stream waves alone
 template <int MODE>
 __global__ __launch_bounds__(NTHR) void k_split2(const float4* __restrict__ w, long n4, float* out) {
     CLK_BEGIN
@@ -235,7 +236,8 @@ __global__ __launch_bounds__(NTHR) void k_split2(const float4* __restrict__ w, l
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const long per = n4 / 64;
     if (wave < 4) {
-        if (MODE == 0) {
+        if (MODE == 4) {
+        } else if (MODE == 0) {
             floatx4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0, c2 = c0, c3 = c0;
             const float a = (float)lane * 0.001f;
             for (long f = 0; f < per / 4; f++) {
@@ -262,7 +264,7 @@ __global__ __launch_bounds__(NTHR) void k_split2(const float4* __restrict__ w, l
             for (int i = 0; i < 16; i++) t += x[i];
             if (t == 12345.f) out[blockIdx.x] = 1.f;
         }
-    } else if (MODE == 0) {
+    } else if (MODE == 0 || MODE == 3 || MODE == 4) {
         const int lw = wave - 4;
         float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
         constexpr int D = 12;
@@ -382,6 +384,15 @@ int main(int argc, char** argv) {
         printf("G=%3d %-28s %8.2f us per launch  %6.1f GB/s per CU  %6.2f TB/s from L2  clock %.2f GHz\n", G, name, us,
                n4 * 16 / (us * 1e3), n4 * 16.0 * G / (us * 1e6), clk[1] ? 0.1 * clk[0] / clk[1] : 0.0);
     };
+    if (argc > 2 && argv[2][0] == 'v') {  // vector-ALU waves beside a register-load stream
+        run("split2: valu alone", k_split2<2>);
+        run("split2: vgpr stream alone", k_split2<4>);
+        run("split2: valu + vgpr stream", k_split2<3>);
+        run("split2: valu + glds stream", k_split2<1>);
+        run("split2: mfma + vgpr stream", k_split2<0>);
+        run("split: mfma waves only", k_split<true, false>);
+        return 0;
+    }
     if (argc > 2) {  // grid sweep: is the per-CU rate of a shared weight set a per-CU or an L2-side limit?
         for (int g : {256, 192, 128, 96, 64, 32}) {
             G = g;
