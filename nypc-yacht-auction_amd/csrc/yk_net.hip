@@ -245,6 +245,30 @@ __device__ __forceinline__ f2v silu2(f2v u) {
 // LayerNorm of a wave's R rows at once, NP value pairs per lane: one pass of shifted sums
 // (shift = the row's first value, so the variance E[(x-k)^2] - E[x-k]^2 does not cancel), the 2R
 // wave reductions independent of each other (their DPP latencies overlap), rstd by v_rsq_f32.
+// Four full-wave sums at once by a halving butterfly: the two quad steps trade halves of the
+// 4-vector (3 DPP adds instead of 8), two row rotations and two cross-row shuffles then carry ONE
+// value per lane, and the sums are read from lanes 0 (v0), 2 (v1), 1 (v2), 3 (v3).
+__device__ __forceinline__ void wave_sum4(float (&v)[4]) {
+    const int lane = threadIdx.x & 63;
+    const bool b0 = (lane & 1) != 0, b1 = (lane & 2) != 0;
+    float k0 = b0 ? v[2] : v[0], k1 = b0 ? v[3] : v[1];
+    const float s0 = b0 ? v[0] : v[2], s1 = b0 ? v[1] : v[3];
+    k0 += dpp_f<0xB1, 0xF>(s0);  // quad_perm [1,0,3,2]: even lanes now hold v0 / v1, odd v2 / v3
+    k1 += dpp_f<0xB1, 0xF>(s1);
+    float k = b1 ? k1 : k0;
+    const float sd = b1 ? k0 : k1;
+    k += dpp_f<0x4E, 0xF>(sd);  // quad_perm [2,3,0,1]: lane & 3 = 0 -> v0, 2 -> v1, 1 -> v2, 3 -> v3
+    k += dpp_f<0x124, 0xF>(k);  // row_ror:4 and row_ror:8: the row's four quads (lane & 3 kept)
+    k += dpp_f<0x128, 0xF>(k);
+    k += __shfl_xor(k, 16, 64);  // the wave's four rows
+    k += __shfl_xor(k, 32, 64);
+    const int ki = __builtin_bit_cast(int, k);
+    v[0] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(ki, 0));
+    v[1] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(ki, 2));
+    v[2] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(ki, 1));
+    v[3] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(ki, 3));
+}
+
 template <int NP, int R>
 __device__ __forceinline__ void layernorm2(f2v (&x)[R][NP], const float* g, const float* b, int c0, int H) {
     float sh[R], s[R], q[R];
@@ -261,10 +285,19 @@ __device__ __forceinline__ void layernorm2(f2v (&x)[R][NP], const float* g, cons
         s[r] = a.x + a.y;
         q[r] = a2.x + a2.y;
     }
+    if constexpr (R == 2) {
+        float v4[4] = {s[0], q[0], s[1], q[1]};
+        wave_sum4(v4);
+        s[0] = v4[0];
+        q[0] = v4[1];
+        s[1] = v4[2];
+        q[1] = v4[3];
+    } else {
 #pragma unroll
-    for (int r = 0; r < R; r++) {
-        s[r] = wave_sum(s[r]);
-        q[r] = wave_sum(q[r]);
+        for (int r = 0; r < R; r++) {
+            s[r] = wave_sum(s[r]);
+            q[r] = wave_sum(q[r]);
+        }
     }
 #pragma unroll
     for (int r = 0; r < R; r++) {
