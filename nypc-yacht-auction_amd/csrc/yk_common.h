@@ -566,22 +566,26 @@ __device__ inline int greedy_heuristic_wave(const YkS& s, int lane) {
 }
 
 // ------------------------------------------------------------------ features
+// c_tab.die_scale / round_feat recomputed in registers (IEEE double division, then the f32
+// rounding the host table applies - the same values bit for bit): a per-lane table index would
+// be a vector load, and in k_forward that would retire only after the weight ring's first fill
+__device__ __forceinline__ float die_scale(uint32_t d) { return (float)(((double)d - 3.5) / 3.5); }
 // state_to_vec  yacht/NNet.py:65-86 (bit-exact f32).  f(i) for i in [0, 59).
 __device__ inline float feature(const YkS& s, int i) {
     const int round = s_round(s), phase = s_phase(s);
-    if (i == 0) return c_tab.round_feat[round];
+    if (i == 0) return (float)((double)round / 13.0);
     if (i == 1) return phase == 0 ? 1.0f : 0.0f;
     if (i == 2) return phase == 1 ? 1.0f : 0.0f;
     if (i < 23) {  // my / opp carry, pad -1
         const int p = (i - 3) / 10, k = (i - 3) % 10;
         const uint64_t wa = s_pw(s, p, 0);
-        return k < wa_n(wa) ? c_tab.die_scale[(wa >> (4 * k)) & 0xF] : -1.0f;
+        return k < wa_n(wa) ? die_scale((uint32_t)(wa >> (4 * k)) & 0xFu) : -1.0f;
     }
     if (i < 33) {  // rolls only when bidding (NNet.py:76-77)
         const int r = (i - 23) / 5, k = (i - 23) % 5;
         const bool has = (s.w[0] >> (5 + r)) & 1;
         if (!(phase == 0 && round != 13) || !has) return -1.0f;
-        return c_tab.die_scale[(s.w[0] >> (24 + 20 * r + 4 * k)) & 0xF];
+        return die_scale((uint32_t)(s.w[0] >> (24 + 20 * r + 4 * k)) & 0xFu);
     }
     if (i < 57) {
         const int p = (i - 33) / 12, k = (i - 33) % 12;

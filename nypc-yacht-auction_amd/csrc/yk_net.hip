@@ -396,17 +396,38 @@ constexpr TileMasks make_tile_masks() {
     }
     return m;
 }
-static __constant__ TileMasks c_tm = make_tile_masks();
+// word w of the mask of tiles t0 .. t1 (arithmetic: a per-lane constant-table load would be a
+// vector load retiring behind the weight ring's first fill)
+constexpr __host__ __device__ uint32_t tile_range_word(int t0, int t1, int w) {
+    const int lo = t0 > 32 * w ? t0 : 32 * w, hi = t1 < 32 * w + 31 ? t1 : 32 * w + 31;
+    return lo > hi ? 0u : (uint32_t)(((2ull << (hi - lo)) - 1ull) << (lo - 32 * w));
+}
+constexpr bool tile_words_match_tables() {
+    const TileMasks m = make_tile_masks();
+    for (int w = 0; w < TMW; w++) {
+        bool ok = m.all[w] == tile_range_word(0, (ASIZE - 1) / 16, w) && m.bid[w] == tile_range_word(0, (NBID - 1) / 16, w);
+        for (int c = 0; c < NCAT; c++) {
+            const int a0 = NBID + NCOMB * c;
+            ok = ok && m.cat[c][w] == tile_range_word(a0 / 16, (a0 + NCOMB - 1) / 16, w) &&
+                 m.first[c][w] == tile_range_word(a0 / 16, a0 / 16, w);
+        }
+        if (!ok) return false;
+    }
+    return true;
+}
+static_assert(tile_words_match_tables(), "arithmetic tile words == the range tables");
 // word w of the tile mask of a row with descriptor vd
 __device__ __forceinline__ uint32_t tile_word(uint32_t vd, int w) {
     const uint32_t m = vd & 0xF;
     if (m == LM_NONE) return 0u;
-    if (m == LM_ALL) return c_tm.all[w];
-    if (m == LM_BID) return c_tm.bid[w];
+    if (m == LM_ALL) return tile_range_word(0, (ASIZE - 1) / 16, w);
+    if (m == LM_BID) return tile_range_word(0, (NBID - 1) / 16, w);
     uint32_t x = 0;
 #pragma unroll
-    for (int c = 0; c < NCAT; c++)
-        if (!((vd >> (4 + c)) & 1u)) x |= m == LM_SCORE10 ? c_tm.cat[c][w] : c_tm.first[c][w];
+    for (int c = 0; c < NCAT; c++) {
+        const int a0 = NBID + NCOMB * c;
+        if (!((vd >> (4 + c)) & 1u)) x |= tile_range_word(a0 / 16, (m == LM_SCORE10 ? a0 + NCOMB - 1 : a0) / 16, w);
+    }
     return x;
 }
 
@@ -523,15 +544,13 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
     // wait behind the weight stream: vmcnt retires in order), then each wave's two state rows by
     // scalar loads (wave-uniform addresses: SMEM, lgkmcnt), then the weight stream - the input
     // layer and the trunk ring's first RW slices of fc1 - and only then the features
-    {
-        constexpr int NV4 = NVS / 4, PER = (NV4 + NTHR - 1) / NTHR;
-        float4 v[PER];
+    constexpr int NV4 = NVS / 4, PER = (NV4 + NTHR - 1) / NTHR;
+    float4 vsv[PER];
 #pragma unroll
-        for (int k = 0; k < PER; k++) v[k] = reinterpret_cast<const float4*>(net.vstat)[min(tid + NTHR * k, NV4 - 1)];
+    for (int k = 0; k < PER; k++) vsv[k] = reinterpret_cast<const float4*>(net.vstat)[min(tid + NTHR * k, NV4 - 1)];
 #pragma unroll
-        for (int k = 0; k < PER; k++)
-            if (tid + NTHR * k < NV4) reinterpret_cast<float4*>(VS)[tid + NTHR * k] = v[k];
-    }
+    for (int k = 0; k < PER; k++)
+        if (tid + NTHR * k < NV4) reinterpret_cast<float4*>(VS)[tid + NTHR * k] = vsv[k];
     constexpr int FPT = ROWS * 64 / NTHR;  // feature rows per wave (row = wave + WAVES k)
     static_assert(FPT * WAVES == ROWS, "one feature row per wave and k");
     YkS fs[FPT];
