@@ -461,12 +461,21 @@ __device__ __forceinline__ void pi_chunk(const _Float16* A, int sa, W2 (&ring)[R
             const int row = row0 + 4 * q + j;
             const bool mine = col < ASIZE && (allc[j] || ((rows >> j) & 1u));
             pa[t][j] += b;
-#ifndef YK_NO_STORE  // diagnostic: the policy head without its logits stores
+#if defined(YK_STORE_NOBR)  // diagnostic: every lane stores, the rows' unkept columns into row padding
+            {
+                const bool st = row < n && mine;
+                const long o = st ? (long)row * PI_LD + col : (long)(row < n ? row : row0) * PI_LD + 16 * REAL_TILES + rr;
+                logits[o] = pa[t][j];
+            }
+#elif !defined(YK_NO_STORE)  // diagnostic: the policy head without its logits stores
             if (row < n && mine) logits[(long)row * PI_LD + col] = pa[t][j];
 #endif
             if (!mine) pa[t][j] = -INFINITY;  // outside the row's softmax
         }
     }
+#ifdef YK_NO_STATS  // diagnostic: the policy head without its softmax statistics
+    if (lane < 0)
+#endif
 #pragma unroll
     for (int j = 0; j < 4; j++) {
         float mn = sm[j];
