@@ -414,8 +414,9 @@ def main():
                    "peak_basis": "f16 dense MFMA peak / 3: every f32 product runs as hi*hi + hi*lo + "
                                  "lo*hi on fp16 planes with f32 accumulation",
                    "limiter": "per-CU weight stream: each 16-row tile streams all 6.7 MB of weight "
-                              "planes through its CU; MFMA issue and vector-memory streaming do not "
-                              "overlap on a CU (tools/stream_bench.hip, DESIGN.md section 6)"}
+                              "planes through its CU, and one CU streams a weight set shared by all CUs "
+                              "at 110-123 GB/s at any CU count; the fp16 MFMAs overlap the stream "
+                              "(tools/stream_bench.hip, profiles/r02_stream_sweep.txt, DESIGN.md section 6)"}
             mf = measured_mfma(args)
             if mf:
                 fwd["mfma_busy"] = {k: mf[k] for k in ("busy_frac", "formula", "source") if k in mf}
