@@ -270,7 +270,7 @@ __device__ __forceinline__ void wave_sum4(float (&v)[4]) {
 }
 
 template <int NP, int R>
-__device__ __forceinline__ void layernorm2(f2v (&x)[R][NP], const float* g, const float* b, int c0, int H) {
+__device__ __forceinline__ void ln_stats2(const f2v (&x)[R][NP], float (&mean)[R], float (&rstd)[R], int H) {
     float sh[R], s[R], q[R];
 #pragma unroll
     for (int r = 0; r < R; r++) {
@@ -303,11 +303,23 @@ __device__ __forceinline__ void layernorm2(f2v (&x)[R][NP], const float* g, cons
     for (int r = 0; r < R; r++) {
         const float m = s[r] / (float)H;
         const float var = fmaxf(q[r] / (float)H - m * m, 0.f);
-        const float rstd = __builtin_amdgcn_rsqf(var + 1e-5f);
-        const float mean = sh[r] + m;
-#pragma unroll
-        for (int i = 0; i < NP; i++) x[r][i] = (x[r][i] - mean) * rstd * ld2(g + c0 + 2 * i) + ld2(b + c0 + 2 * i);
+        rstd[r] = __builtin_amdgcn_rsqf(var + 1e-5f);
+        mean[r] = sh[r] + m;
     }
+}
+template <int NP, int R>
+__device__ __forceinline__ void ln_apply2(f2v (&x)[R][NP], const float (&mean)[R], const float (&rstd)[R],
+                                          const float* g, const float* b, int c0) {
+#pragma unroll
+    for (int r = 0; r < R; r++)
+#pragma unroll
+        for (int i = 0; i < NP; i++) x[r][i] = (x[r][i] - mean[r]) * rstd[r] * ld2(g + c0 + 2 * i) + ld2(b + c0 + 2 * i);
+}
+template <int NP, int R>
+__device__ __forceinline__ void layernorm2(f2v (&x)[R][NP], const float* g, const float* b, int c0, int H) {
+    float mean[R], rstd[R];
+    ln_stats2<NP, R>(x, mean, rstd, H);
+    ln_apply2<NP, R>(x, mean, rstd, g, b, c0);
 }
 template <int NP>
 __device__ __forceinline__ void put_planes2(_Float16* planes, int sa, int r, int c, const f2v (&x)[NP]) {
@@ -658,19 +670,39 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
         }
         if (lane == 0) TC = base;
     }
+    if constexpr (VPL % 2 == 0) {
+        f2v x[RPW][VPL / 2];
 #pragma unroll
-    for (int rr = 0; rr < RPW; rr++) {
-        const int r = wave * RPW + rr;
-        float x[VPL];
+        for (int rr = 0; rr < RPW; rr++)
 #pragma unroll
-        for (int i = 0; i < VPL; i++) x[i] = T[r * LD + c0 + i] + VS[VS_BIN * H + c0 + i];
-        layernorm<VPL>(x, VS + VS_GIN * H, VS + VS_BEIN * H, c0, H);
+            for (int i = 0; i < VPL / 2; i++)
+                x[rr][i] = ld2(T + (wave * RPW + rr) * LD + c0 + 2 * i) + ld2(VS + VS_BIN * H + c0 + 2 * i);
+        layernorm2<VPL / 2, RPW>(x, VS + VS_GIN * H, VS + VS_BEIN * H, c0, H);
 #pragma unroll
-        for (int i = 0; i < VPL; i++) {
-            x[i] = silu(x[i]);
-            X[r * LD + c0 + i] = x[i];
+        for (int rr = 0; rr < RPW; rr++) {
+            const int r = wave * RPW + rr;
+#pragma unroll
+            for (int i = 0; i < VPL / 2; i++) {
+                x[rr][i] = silu2(x[rr][i]);
+                *reinterpret_cast<f2v*>(X + r * LD + c0 + 2 * i) = x[rr][i];
+            }
+            put_planes2<VPL / 2>(P, SA, r, c0, x[rr]);
         }
-        put_planes<VPL>(P, SA, r, c0, x);
+    } else {
+#pragma unroll
+        for (int rr = 0; rr < RPW; rr++) {
+            const int r = wave * RPW + rr;
+            float x[VPL];
+#pragma unroll
+            for (int i = 0; i < VPL; i++) x[i] = T[r * LD + c0 + i] + VS[VS_BIN * H + c0 + i];
+            layernorm<VPL>(x, VS + VS_GIN * H, VS + VS_BEIN * H, c0, H);
+#pragma unroll
+            for (int i = 0; i < VPL; i++) {
+                x[i] = silu(x[i]);
+                X[r * LD + c0 + i] = x[i];
+            }
+            put_planes<VPL>(P, SA, r, c0, x);
+        }
     }
     lds_barrier();
     TSTAMP(2);
@@ -769,26 +801,59 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
     W2 pring[RD][PCH];
 #pragma unroll
     for (int ks = 0; ks < RD; ks++) pring[ks][0] = ld_w2(net.w_v1, KS, wave, ks, lane);
+    if constexpr (VPL % 2 == 0) {
+        // both heads' LayerNorms see the same row: one set of statistics, two affine maps
+        f2v x[RPW][VPL / 2], y[RPW][VPL / 2];
 #pragma unroll
-    for (int rr = 0; rr < RPW; rr++) {
-        const int r = wave * RPW + rr;
-        float x[VPL], y[VPL];
+        for (int rr = 0; rr < RPW; rr++)
 #pragma unroll
-        for (int i = 0; i < VPL; i++) x[i] = y[i] = X[r * LD + c0 + i];
-        layernorm<VPL>(x, VS + VS_GPI * H, VS + VS_BEPI * H, c0, H);
-        layernorm<VPL>(y, VS + VS_GV * H, VS + VS_BEV * H, c0, H);
+            for (int i = 0; i < VPL / 2; i++) x[rr][i] = y[rr][i] = ld2(X + (wave * RPW + rr) * LD + c0 + 2 * i);
+        float mean[RPW], rstd[RPW];
+        ln_stats2<VPL / 2, RPW>(x, mean, rstd, H);
+        ln_apply2<VPL / 2, RPW>(x, mean, rstd, VS + VS_GPI * H, VS + VS_BEPI * H, c0);
+        ln_apply2<VPL / 2, RPW>(y, mean, rstd, VS + VS_GV * H, VS + VS_BEV * H, c0);
+        float h2[RPW];
 #pragma unroll
-        for (int i = 0; i < VPL; i++) {
-            x[i] = silu(x[i]);  // a_pi
-            y[i] = silu(y[i]);  // a_v
+        for (int rr = 0; rr < RPW; rr++) {
+            const int r = wave * RPW + rr;
+            f2v a = {0.f, 0.f};
+#pragma unroll
+            for (int i = 0; i < VPL / 2; i++) {
+                x[rr][i] = silu2(x[rr][i]);  // a_pi
+                y[rr][i] = silu2(y[rr][i]);  // a_v
+                a = a + x[rr][i] * x[rr][i];
+            }
+            put_planes2<VPL / 2>(P, SA, r, c0, x[rr]);
+            put_planes2<VPL / 2>(PV, SA, r, c0, y[rr]);
+            h2[rr] = a.x + a.y;
         }
-        put_planes<VPL>(P, SA, r, c0, x);
-        put_planes<VPL>(PV, SA, r, c0, y);
-        float h2 = 0.f;
 #pragma unroll
-        for (int i = 0; i < VPL; i++) h2 += x[i] * x[i];
-        h2 = wave_sum(h2);
-        if (lane == 0) HN[r] = h2;
+        for (int rr = 0; rr < RPW; rr++) {
+            const float t = wave_sum(h2[rr]);
+            if (lane == 0) HN[wave * RPW + rr] = t;
+        }
+    } else {
+#pragma unroll
+        for (int rr = 0; rr < RPW; rr++) {
+            const int r = wave * RPW + rr;
+            float x[VPL], y[VPL];
+#pragma unroll
+            for (int i = 0; i < VPL; i++) x[i] = y[i] = X[r * LD + c0 + i];
+            layernorm<VPL>(x, VS + VS_GPI * H, VS + VS_BEPI * H, c0, H);
+            layernorm<VPL>(y, VS + VS_GV * H, VS + VS_BEV * H, c0, H);
+#pragma unroll
+            for (int i = 0; i < VPL; i++) {
+                x[i] = silu(x[i]);  // a_pi
+                y[i] = silu(y[i]);  // a_v
+            }
+            put_planes<VPL>(P, SA, r, c0, x);
+            put_planes<VPL>(PV, SA, r, c0, y);
+            float h2 = 0.f;
+#pragma unroll
+            for (int i = 0; i < VPL; i++) h2 += x[i] * x[i];
+            h2 = wave_sum(h2);
+            if (lane == 0) HN[r] = h2;
+        }
     }
     lds_barrier();
     TSTAMP(9);
