@@ -479,6 +479,8 @@ __device__ __forceinline__ void pi_chunk(const _Float16* A, int sa, W2 (&ring)[R
                 const long o = st ? (long)row * PI_LD + col : (long)(row < n ? row : row0) * PI_LD + 16 * REAL_TILES + rr;
                 logits[o] = pa[t][j];
             }
+#elif defined(YK_NT_STORE)  // diagnostic: non-temporal logits stores
+            if (row < n && mine) __builtin_nontemporal_store(pa[t][j], logits + (long)row * PI_LD + col);
 #elif !defined(YK_NO_STORE)  // diagnostic: the policy head without its logits stores
             if (row < n && mine) logits[(long)row * PI_LD + col] = pa[t][j];
 #endif
