@@ -98,8 +98,8 @@ def allreduce_counts(counts, device=None):
     """Sum of small integer tallies over the ranks (the gating arena's wins / losses / draws)."""
     if rank_world()[1] == 1:
         return [int(x) for x in counts]
-    nccl = dist.get_backend() == "nccl"
-    t = torch.tensor([int(x) for x in counts], dtype=torch.int64, device=device if nccl else "cpu")
+    nccl = dist.get_backend() == "nccl"  # RCCL reduces device tensors only
+    t = torch.tensor([int(x) for x in counts], dtype=torch.int64, device=(device or "cuda") if nccl else "cpu")
     dist.all_reduce(t)
     return [int(x) for x in t.cpu().tolist()]
 
