@@ -429,9 +429,15 @@ __global__ __launch_bounds__(256) void k_move_begin(EngDev d, int move, int exte
     const uint32_t cnt = d.node_count[g * d.T + t];
     uint32_t nn = 0, ne = 0, top = 0;
     wave_sync();
-    for (uint32_t id = 0; id < cnt; id++) {
+    // 64 records' rounds at a time (one load per lane), then the survivors in id order: the
+    // records of earlier rounds cost no serial round trip
+    for (uint32_t b0 = 0; b0 < cnt; b0 += 64) {
+    const uint32_t il = b0 + (uint32_t)lane;
+    uint64_t live = __ballot(il < cnt && (int)(src[il < cnt ? il : 0].key[0] & 0xF) >= rr);
+    while (live) {
+        const uint32_t id = b0 + (uint32_t)__builtin_ctzll(live);
+        live &= live - 1;
         NodeRec rec = src[id];
-        if ((int)(rec.key[0] & 0xF) < rr) continue;
         const int V = (int)rec.nvalid, VP = pad4(V);
         const uint32_t so = rec.p_off;
         for (int j0 = 0; j0 < VP; j0 += 64) {
@@ -463,6 +469,7 @@ __global__ __launch_bounds__(256) void k_move_begin(EngDev d, int move, int exte
             insert_index(d, h, t, rec.hash, nn);
         }
         nn++;
+    }
     }
     if (lane == 0) {
         d.node_count[h * d.T + t] = nn;
