@@ -957,15 +957,34 @@ __global__ __launch_bounds__(256) void k_move_end(EngDev d, int move) {
         const VInfo vi = unpack_vinfo(nd.vinfo, nd.nvalid);
         const uint16_t* S = d.arenaS + (long)t * d.AE + nd.p_off;
         const Edge* edges = d.edges[g] + (long)t * d.ECAP;
-        for (int j0 = 0; j0 < (int)nd.nvalid; j0 += 64) {
-            const int j = j0 + lane;
-            const uint16_t sl = j < (int)nd.nvalid ? S[j] : 0;
-            const uint64_t bal = __ballot(sl != 0);
-            if (sl) {
-                const int pos = nvis + __popcll(bal & ((1ull << lane) - 1));
-                vis[pos] = ((uint32_t)compact_to_action(vi, j) << 16) | (edges[sl - 1].N & 0xFFFF);
+        // 8 pieces of 64 entries at a time: their slot loads, then their edge loads, all in flight
+        // together (one round trip each per 512 entries instead of per 64)
+        constexpr int MB = 8;
+        const int nv = (int)nd.nvalid;
+        for (int j0 = 0; j0 < nv; j0 += 64 * MB) {
+            uint16_t sl[MB];
+#pragma unroll
+            for (int b = 0; b < MB; b++) {
+                const int j = j0 + 64 * b + lane;
+                const uint16_t x = S[j < nv ? j : 0];  // unconditional loads (in bounds): no wait at a branch join
+                sl[b] = j < nv ? x : 0;
             }
-            nvis += __popcll(bal);
+            uint32_t n[MB];
+#pragma unroll
+            for (int b = 0; b < MB; b++) {
+                const uint32_t x = edges[sl[b] ? sl[b] - 1 : 0].N;
+                n[b] = sl[b] ? x : 0u;
+            }
+#pragma unroll
+            for (int b = 0; b < MB; b++) {
+                const int j = j0 + 64 * b + lane;
+                const uint64_t bal = __ballot(sl[b] != 0);
+                if (sl[b]) {
+                    const int pos = nvis + __popcll(bal & ((1ull << lane) - 1));
+                    vis[pos] = ((uint32_t)compact_to_action(vi, j) << 16) | (n[b] & 0xFFFF);
+                }
+                nvis += __popcll(bal);
+            }
         }
     } else if (lane == 0) {
         atomicOr(d.err, ERR_ROOT);
