@@ -659,7 +659,7 @@ __device__ __forceinline__ void select_game(const EngDev& d, int e, int lane, co
     }
 }
 
-__global__ __launch_bounds__(256) void k_select(EngDev d, const uint32_t* env_ids, uint64_t* ctr_arr) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_select(EngDev d, const uint32_t* env_ids, uint64_t* ctr_arr) {
     const int lane = threadIdx.x & 63;
     const int e = d.e_lo + blockIdx.x * GAMES_PER_BLOCK + (threadIdx.x >> 6);
     if (e >= d.e_hi) return;
