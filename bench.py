@@ -275,6 +275,9 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel event timing")
+    ap.add_argument("--profile-stride", type=int, default=8,
+                    help="time the forward / expand pair of every k-th simulation (1 = all; each event "
+                         "record between dependent launches costs GPU time: ~5 %% of the batch at 1)")
     ap.add_argument("--no-arena", action="store_true", help="skip the config-4 Arena leg")
     ap.add_argument("--no-train", action="store_true", help="skip the config-5 train-step leg")
     ap.add_argument("--no-coach", action="store_true", help="skip the config-5 Coach-iteration leg")
@@ -326,7 +329,7 @@ def main():
     torch.cuda.synchronize()
     exp0 = 0
     if not args.no_profile:
-        eng.profile(True)
+        eng.profile(True, stride=args.profile_stride)
     t0 = time.perf_counter()
     exps = 0
     games = 0
@@ -398,11 +401,15 @@ def main():
         per = {k: (ms / n if n else 0.0, n, ms) for k, (ms, n) in kt.items()}
         out["kernel_ms"] = {k: {"avg_ms": round(a, 5), "launches": n, "total_ms": round(t, 2)}
                             for k, (a, n, t) in per.items()}
+        out["kernel_ms_basis"] = (f"HIP event intervals on the engine's stream inside the timed region; forward and "
+                                  f"expand_backup_select timed in every {args.profile_stride}th simulation of "
+                                  f"each move (launches = the timed ones), the per-move kernels every time")
         dom = max(per, key=lambda k: per[k][2])
         fwd = env = None
         if "forward" in per and per["forward"][1]:
             # k_forward (MFMA): algorithmic FLOP per launch = expansions predicted per launch x 3,320,576
-            exp_per_launch = exps / world / args.steps / max(per["forward"][1] / args.steps, 1)
+            # (one forward launch per simulation and game group; st["sims"] = simulations per batch)
+            exp_per_launch = exps / world / args.steps / max(st["sims"] * st["groups"], 1)
             flop = PREDICT_FLOP * exp_per_launch
             ach = flop / (per["forward"][0] * 1e-3) / 1e12
             tr = measured_traffic(args)  # per-GPU configuration, so per-launch bytes hold at any N
@@ -424,7 +431,7 @@ def main():
             # k_expand_backup (HBM): algorithmic bytes = 4*S_scan + 16*D + 4*V_new + 364 per
             # expansion, from the engine's own counters of the last batch, per launch
             scan_b = 4 * st["scanned"] + 16 * st["path_edges"] + 4 * st["vnew"] + 364 * st["expansions"]
-            b = scan_b / max(st["sims"], 1)
+            b = scan_b / max(st["sims"] * st["groups"], 1)
             ach = b / (per["expand_backup_select"][0] * 1e-3) / 1e9
             tr = measured_traffic(args, "expand")
             env = {"kernel": "k_expand_backup", "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS,
@@ -432,7 +439,7 @@ def main():
                    "traffic_source": tr[1] if tr else None,
                    "work_per_launch": f"{b:.0f} algorithmic bytes = (4 x {st['scanned']} UCB entries scanned + "
                                       f"16 x {st['path_edges']} path edges + 4 x {st['vnew']} new valid entries + "
-                                      f"364 x {st['expansions']} expansions) / {st['sims']} launches"}
+                                      f"364 x {st['expansions']} expansions) / {st['sims'] * st['groups']} launches"}
         if dom == "forward":
             out["roofline"], out["roofline_env"] = fwd, env
         else:

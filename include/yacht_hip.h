@@ -163,8 +163,11 @@ int yk_engine_destroy(yk_engine_t* eng);
  * Synchronises `stream` once per real move to test termination.  Returns YK_OK, or
  * YK_ERR_CAPACITY / YK_ERR_STATE if a device-side check failed (see yk_engine_stats). */
 int yk_selfplay(yk_engine_t* eng, uint64_t seed, uint32_t env_base, void* stream);
-/* Per-kernel timing with HIP events on the engine's stream (adds an event pair around each
- * launch while enabled; resets the accumulators).  yk_engine_kernel_times: HOST ms[8],
+/* Per-kernel timing with HIP events on the engine's stream; resets the accumulators.
+ * enable = 0 off, k > 0 on: the per-move launches are timed every time, the per-simulation
+ * forward / expand pair in every k-th simulation of a move (1 = all; an event record between
+ * dependent launches costs GPU time, so a stride keeps the timed batch's rate).
+ * yk_engine_kernel_times (launches counts the timed ones): HOST ms[8],
  * launches[8] for classes 0 first descent of a move, 1 forward (the whole predict), 2 unused,
  * 3 expand + backup + the next descent, 4 move begin (root / tree compaction), 5 move end
  * (policy, sampling, real step). */

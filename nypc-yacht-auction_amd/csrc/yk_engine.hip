@@ -1165,8 +1165,11 @@ struct yk_engine {
     int ngroups = 1;
     hipStream_t gs[YK_MAX_GROUPS] = {};
     hipEvent_t ev_fork = nullptr, ev_join[YK_MAX_GROUPS] = {}, ev_fwd[YK_MAX_GROUPS] = {};
-    // profiling (yk_engine_profile): per-kernel-class HIP events on each group's stream
+    // profiling (yk_engine_profile): per-kernel-class HIP events on each group's stream; the
+    // forward / expand pair is timed in every prof_stride-th simulation (an event record between
+    // two dependent launches costs ~4 us of GPU time, so timing every one slows the batch ~5 %)
     bool prof = false;
+    int prof_stride = 1;
     struct ProfLog {
         std::vector<hipEvent_t> ev;
         std::vector<int> cls;
@@ -1258,11 +1261,12 @@ int run_sims(yk_engine* eng, int G, const hipStream_t* st, int sims, const uint3
         YK_LAUNCHED();
     }
     for (int k = 0; k < sims; k++) {
+        const bool timed = k % eng->prof_stride == 0;  // sim 0 always: it closes the select interval
         for (int g = 0; g < G; g++) {
             const EngDev& d = dg[g];
             if (d.prior == 0) {
                 if (g > 0) YK_HIP(hipStreamWaitEvent(st[g], eng->ev_fwd[g - 1], 0));
-                prof_mark(eng, g, KC_FORWARD, st[g]);
+                if (timed) prof_mark(eng, g, KC_FORWARD, st[g]);
                 // predict row = game: no compaction; workgroups without a leaf exit at once
                 // (dual trees: the agent's leaves on its net, then the opponent's on its own)
                 const int lo = d.e_lo;
@@ -1275,9 +1279,10 @@ int run_sims(yk_engine* eng, int G, const hipStream_t* st, int sims, const uint3
                 }
                 if (G > 1) YK_HIP(hipEventRecord(eng->ev_fwd[g], st[g]));
             }
-            prof_mark(eng, g, KC_EXPAND, st[g]);
+            if (timed) prof_mark(eng, g, KC_EXPAND, st[g]);
             hipLaunchKernelGGL(k_expand_backup, game_grid(d), bb, 0, st[g], d, k + 1 < sims ? 1 : 0, env_ids, ctr);
             YK_LAUNCHED();
+            if (timed && eng->prof_stride > 1) prof_mark(eng, g, -1, st[g]);  // untimed sims follow
         }
     }
     for (int g = 0; g < G; g++) prof_mark(eng, g, -1, st[g]);
@@ -1583,7 +1588,9 @@ int yk_arena_results(yk_engine_t* eng, double* result, int32_t* totals, int32_t*
 
 int yk_engine_profile(yk_engine_t* eng, int enable) {
     if (!eng) return YK_ERR_ARG;
+    if (enable < 0) return YK_ERR_ARG;
     eng->prof = enable != 0;
+    eng->prof_stride = enable > 0 ? enable : 1;
     for (auto& L : eng->pg) L.used = 0;
     for (int i = 0; i < 8; i++) {
         eng->kms[i] = 0;

@@ -88,8 +88,9 @@ class SelfPlayEngine:
     # class 0: the first descent of each move; class 3: expand + backup + the next descent
     KERNEL_CLASSES = ("select", "forward", "unused", "expand_backup_select", "move_begin", "move_end")
 
-    def profile(self, enable: bool = True):
-        call("yk_engine_profile", self.handle, int(enable))
+    def profile(self, enable: bool = True, stride: int = 1):
+        """Per-kernel HIP event timing; the forward / expand pair of every `stride`-th simulation."""
+        call("yk_engine_profile", self.handle, int(stride) if enable else 0)
 
     def kernel_times(self) -> dict:
         ms = np.zeros(8, dtype=np.float64)
