@@ -1248,8 +1248,10 @@ int check_errors(yk_engine* eng, hipStream_t s) {
     return YK_OK;
 }
 // `sims` simulations for every game of groups 0 .. G-1, group g on stream st[g].  Within a group
-// (and a game) the simulations are sequential; group g's forward k waits for group g-1's forward
-// k, which staggers the groups so that a forward runs beside the other groups' expand.
+// (and a game) the simulations are sequential; the groups' streams run free, so a forward runs
+// beside the other groups' expand.  (YK_STAGGER, diagnostic: group g's forward k waits for group
+// g-1's forward k through an event; at 8192 games x 2 groups that costs 1.2 %,
+// profiles/r02h_stagger_ab.log.)
 int run_sims(yk_engine* eng, int G, const hipStream_t* st, int sims, const uint32_t* env_ids, uint64_t* ctr) {
     const dim3 bb(256);
     if (sims <= 0) return YK_OK;
@@ -1265,7 +1267,9 @@ int run_sims(yk_engine* eng, int G, const hipStream_t* st, int sims, const uint3
         for (int g = 0; g < G; g++) {
             const EngDev& d = dg[g];
             if (d.prior == 0) {
+#ifdef YK_STAGGER
                 if (g > 0) YK_HIP(hipStreamWaitEvent(st[g], eng->ev_fwd[g - 1], 0));
+#endif
                 if (timed) prof_mark(eng, g, KC_FORWARD, st[g]);
                 // predict row = game: no compaction; workgroups without a leaf exit at once
                 // (dual trees: the agent's leaves on its net, then the opponent's on its own)
@@ -1277,7 +1281,9 @@ int run_sims(yk_engine* eng, int G, const hipStream_t* st, int sims, const uint3
                                             d.leaf_flag + lo, eng->mlse + lo, true, d.dual ? (uint8_t)(1u << side) : 0xFF);
                     if (rc) return rc;
                 }
+#ifdef YK_STAGGER
                 if (G > 1) YK_HIP(hipEventRecord(eng->ev_fwd[g], st[g]));
+#endif
             }
             if (timed) prof_mark(eng, g, KC_EXPAND, st[g]);
             hipLaunchKernelGGL(k_expand_backup, game_grid(d), bb, 0, st[g], d, k + 1 < sims ? 1 : 0, env_ids, ctr);
