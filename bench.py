@@ -204,6 +204,7 @@ def shape_leg(net, envs=2048, sims=200, seed=0):
         raise SystemExit(f"config-3 leg: engine error flags {st['errors']}")
     return {"config": f"{envs} games x {sims} sims on one GPU (config 3's per-GPU shape), full episodes",
             "expansions_per_s": st["expansions"] / dt, "episodes_per_s": envs / dt, "s_per_batch": dt,
+            "forward_parts": st["forward_parts"],
             "capacity_use": {k: int(st[k]) for k in ("max_nodes", "node_cap", "max_edges", "edge_cap", "max_arena",
                                                      "arena_cap")}}
 
@@ -383,6 +384,7 @@ def main():
         "expansions_per_s_per_gpu": value / world,
         "expansions_per_episode_batch": exps / args.steps,
         "game_groups": st["groups"],
+        "forward_parts": st["forward_parts"],
         "capacity_use": {k: int(st[k]) for k in ("max_nodes", "node_cap", "max_edges", "edge_cap", "max_arena",
                                                  "arena_cap")},
     }

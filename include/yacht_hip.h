@@ -176,7 +176,7 @@ int yk_engine_kernel_times(yk_engine_t* eng, double* ms, int64_t* launches);
 /* HOST out[16]: 0 expansions, 1 valid entries scanned by UCB, 2 real moves (max over games),
  * 3 device error flags, 4 max live nodes, 5 max live edges, 6 max arena entries used (per shard),
  * 7 new-node valid entries written, 8 search path edges backed up, 9 lock-step sims run,
- * 10-13 node / edge / arena / visit capacities, 14 game groups */
+ * 10-13 node / edge / arena / visit capacities, 14 game groups, 15 forward head parts (workgroups per 16-row tile) */
 int yk_engine_stats(yk_engine_t* eng, int64_t* out);
 /* Copies the last episode batch to HOST arrays (any may be NULL):
  *   states[n][max_moves][8]  canonical board of each example (Coach.py:57,61)

@@ -67,6 +67,7 @@ struct EngDev {
     int sims, temp_threshold;
     float c32;
     int prior;  // 0 net, 1 hash
+    int fparts; // forward head split: workgroups per 16-row tile (mlse holds fparts partials [p][E])
     int rec_pred, max_exp, rec_stride;  // record_predictions: games e % rec_stride == 0, slot e / rec_stride
     int arena;             // 1 while yk_arena runs
     int arena_agent, arena_opp;  // YK_PLAYER_* of the seat-agent_seat player and of the other seat
@@ -103,7 +104,8 @@ struct EngDev {
     uint32_t* res_t;
     const float* logits;   // [E][PI_LD]
     const float* vpred;    // [E]
-    const float2* mlse;    // [E] per-row (max, log sum exp) of the logits, from the forward
+    const float2* mlse;    // [E] per-row (max, log sum exp) of the logits, from the forward; with
+                           // fparts > 1, [fparts][E] raw partials (max, sum exp) merged by the expand
     const float* lut_sq;
     const float* lut_sqe;
     // records
@@ -723,6 +725,18 @@ __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int l
             const float2 ml = d.mlse[e];
             mx = ml.x;
             lse = ml.y;
+            if (d.fparts > 1) {  // merge the head parts' (max, sum exp), in part order
+                float ms = ml.y;
+                for (int p = 1; p < d.fparts; p++) {
+                    const float2 q = d.mlse[(long)p * d.E + e];
+                    const float mm = fmaxf(mx, q.x);
+                    if (mm != -INFINITY) {
+                        ms = ms * __expf(mx - mm) + q.y * __expf(q.x - mm);
+                        mx = mm;
+                    }
+                }
+                lse = __logf(ms);
+            }
             // score actions at 10 dice (most leaves): a group a .. a + 3 (a = 0 mod 4) holds at
             // most two categories, a's and a + 2's (category starts are 202 + 252 c = 2 mod 4)
             static_assert(NBID % 4 == 2 && NCOMB % 4 == 0, "category starts are 2 mod 4");
@@ -1278,7 +1292,8 @@ int run_sims(yk_engine* eng, int G, const hipStream_t* st, int sims, const uint3
                     const yk_net_t* net = side ? eng->net2 : eng->net;
                     int rc = launch_forward(net->dev, d.leaf_state + lo, nullptr, nullptr, nullptr, d.e_hi - lo,
                                             eng->logits + (size_t)lo * PI_LD, eng->vpred + lo, st[g],
-                                            d.leaf_flag + lo, eng->mlse + lo, true, d.dual ? (uint8_t)(1u << side) : 0xFF);
+                                            d.leaf_flag + lo, eng->mlse + lo, true, d.dual ? (uint8_t)(1u << side) : 0xFF,
+                                            d.fparts, d.E);
                     if (rc) return rc;
                 }
 #ifdef YK_STAGGER
@@ -1357,6 +1372,18 @@ int yk_engine_create(yk_engine_t** out, const yk_engine_config_t* cfg, yk_net_t*
     int G = cfg->groups > 0 ? cfg->groups : ((cfg->prior == 0 && cfg->n_envs >= 8192) ? 2 : 1);
     G = std::max(1, std::min({G, YK_MAX_GROUPS, (cfg->n_envs + GROUP_ALIGN - 1) / GROUP_ALIGN}));
     eng->ngroups = G;
+    // forward head split: when a group's row tiles do not fill the CUs, 2 or 4
+    // workgroups per tile each take a slice of the policy head (the trunk runs in each)
+#ifndef YK_FPARTS_MAX
+#define YK_FPARTS_MAX 1  // 4 once measured on the GPU (tools/fparts_ab.sh)
+#endif
+    {
+        int cus = 256, dev = 0;
+        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        const int tiles = ((cfg->n_envs + G - 1) / G + 15) / 16;
+        d.fparts = 1;
+        while (d.fparts * 2 <= YK_FPARTS_MAX && tiles * d.fparts * 2 <= cus) d.fparts *= 2;
+    }
     const size_t R = ((size_t)cfg->n_envs + d.rec_stride - 1) / d.rec_stride;
     const size_t E = (size_t)d.E, T = (size_t)d.T;
     int rc = YK_OK;
@@ -1390,7 +1417,7 @@ int yk_engine_create(yk_engine_t** out, const yk_engine_config_t* cfg, yk_net_t*
     A(d.res_v, E);
     A(d.res_t, E);
     A(eng->vpred, E);
-    A(eng->mlse, E);
+    A(eng->mlse, E * (size_t)d.fparts);
     A(eng->lut_sq, (size_t)LUT_N);
     A(eng->lut_sqe, (size_t)LUT_N);
     A(d.rec_state, E * d.M);
@@ -1643,6 +1670,7 @@ int yk_engine_stats(yk_engine_t* eng, int64_t* out) {
     out[12] = d.AE;
     out[13] = d.VCAP;
     out[14] = eng->ngroups;
+    out[15] = d.fparts;
     return YK_OK;
 }
 

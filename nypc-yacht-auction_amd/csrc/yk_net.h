@@ -41,7 +41,11 @@ constexpr int vstat_size(int H) { return vs_bpi(H) + PI_LD; }
 int launch_forward(const NetDev& net, const yk_state_t* states, const float* x, const int32_t* rows,
                    const int32_t* count, int n, float* logits, float* v, hipStream_t stream,
                    const uint8_t* active = nullptr, float2* mlse = nullptr, bool valid_only = false,
-                   uint8_t want = 0xFF);  // a row is predicted iff !active || (active[row] & want)
+                   uint8_t want = 0xFF,  // a row is predicted iff !active || (active[row] & want)
+                   int parts = 1, int mstride = 0);
+// parts > 1 (1, 2 or 4): `parts` workgroups per 16-row tile split the policy head's tile list
+// (each runs the trunk), for launches with fewer tiles than CUs; mlse[p * mstride + row] then holds
+// part p's raw (max, sum exp) of the row, which the consumer merges (max, then log of the sum).
 // pi[n][3226] = exp(log_softmax(logits[:, :3226])) = exp(logits - m - l), (m, l) = mlse[row]
 int launch_softmax(const float* logits, const float2* mlse, float* pi, int n, hipStream_t stream);
 

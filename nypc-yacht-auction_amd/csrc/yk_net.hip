@@ -512,7 +512,7 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
                                                  const int32_t* __restrict__ count, int n,
                                                  float* __restrict__ logits, float* __restrict__ vout,
                                                  const uint8_t* __restrict__ active, float2* __restrict__ mlse,
-                                                 int valid_only, uint32_t want) {
+                                                 int valid_only, uint32_t want, int parts, int mstride) {
     constexpr int LD = (H > 128 ? H : 128) + 4;      // X also holds the 128-wide v_head hidden
     constexpr int SA = H + 8;                        // plane row stride (halves): conflict-free b128 reads
     constexpr int NT = H >= 16 * WAVES ? H / (16 * WAVES) : 1;  // 16-col tiles per wave, H-wide layers
@@ -541,7 +541,11 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
     __shared__ uint16_t TRB[PI_TILES];                       // per tile: the rows that keep a column in it
 
     if (count) n = min(n, *count);
-    const int row0 = blockIdx.x * ROWS;
+    // head split (parts > 1): `parts` workgroups share a 16-row tile; each runs the trunk and the
+    // value head and the policy head over its slice of the tile list, and writes its raw partial
+    // (max, sum exp) to mlse[part * mstride + row] (the consumer merges them); part 0 writes v
+    const int part = (int)(blockIdx.x % (unsigned)parts);
+    const int row0 = (int)(blockIdx.x / (unsigned)parts) * ROWS;
     if (row0 >= n) return;
     uint32_t amask = 0xFFFFu;  // rows with a leaf (bit r: row row0 + r)
     if (active) {  // uniform: every wave reads the same 16 flags (one scalar load when whole)
@@ -907,8 +911,9 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
 #pragma unroll
     for (int r = 0; r < ROWS; r++) full |= row_allc(r);
     full = __builtin_amdgcn_readfirstlane(full ? 1 : 0) != 0;
-    const int cnt = full ? REAL_TILES : __builtin_amdgcn_readfirstlane(TC);
-    // this wave's list entries k = 0 .. m-1 (list index wave + WAVES k): nf full chunks in list
+    const int cnt_all = full ? REAL_TILES : __builtin_amdgcn_readfirstlane(TC);
+    const int lo = cnt_all * part / parts, cnt = cnt_all * (part + 1) / parts - lo;  // this part's slice
+    // this wave's list entries k = 0 .. m-1 (list index lo + wave + WAVES k): nf full chunks in list
     // order, then a last chunk of l entries.  Every workgroup walks its list in ascending tile
     // order: workgroups reading the same weight lines together is faster than spreading them
     // (a per-workgroup rotation of the chunk order cost 0.5 us)
@@ -919,7 +924,7 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
         const int k0 = PCH * c;
 #pragma unroll
         for (int t = 0; t < PCH; t++) {
-            const int i = wave + WAVES * (k0 + t);
+            const int i = lo + wave + WAVES * (k0 + t);
             tl[t] = c < nch && k0 + t < m ? (full ? i : __builtin_amdgcn_readfirstlane((int)TL[i])) : 0;
         }
     };
@@ -999,7 +1004,7 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
         const float* wv2 = VS + VS_BV1 * H + 128;
         float s = silu(X[r * LD + 2 * lane]) * wv2[2 * lane] + silu(X[r * LD + 2 * lane + 1]) * wv2[2 * lane + 1];
         s = wave_sum(s);
-        if (lane == 0 && row < n && ((amask >> r) & 1u)) vout[row] = tanhf(s + net.b_v2[0]);  // active rows only
+        if (lane == 0 && part == 0 && row < n && ((amask >> r) & 1u)) vout[row] = tanhf(s + net.b_v2[0]);  // active rows only
     }
     if (mlse) {
         lds_barrier();
@@ -1007,7 +1012,7 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
             float m = -INFINITY, sm = 0.f;
 #pragma unroll
             for (int w = 0; w < WAVES; w++) stat_merge(m, sm, SS[w * ROWS + tid].x, SS[w * ROWS + tid].y);
-            mlse[row0 + tid] = make_float2(m, __logf(sm));
+            mlse[(long)part * mstride + row0 + tid] = make_float2(m, parts > 1 ? sm : __logf(sm));
         }
     }
     TSTAMP(15);
@@ -1084,15 +1089,16 @@ namespace yk {
 
 int launch_forward(const NetDev& net, const yk_state_t* states, const float* x, const int32_t* rows,
                    const int32_t* count, int n, float* logits, float* v, hipStream_t stream, const uint8_t* active,
-                   float2* mlse, bool valid_only, uint8_t want) {
+                   float2* mlse, bool valid_only, uint8_t want, int parts, int mstride) {
     if (n <= 0) return YK_OK;
-    const dim3 grid((n + ROWS - 1) / ROWS), block(NTHR);
+    if (parts < 1 || parts > 4 || (parts > 1 && (!mlse || mstride < n))) return YK_ERR_ARG;
+    const dim3 grid((unsigned)((n + ROWS - 1) / ROWS * parts)), block(NTHR);
     const int vo = valid_only ? 1 : 0;
     switch (net.H) {
-        case 64: hipLaunchKernelGGL(k_forward<64>, grid, block, 0, stream, net, states, x, rows, count, n, logits, v, active, mlse, vo, (uint32_t)want); break;
-        case 128: hipLaunchKernelGGL(k_forward<128>, grid, block, 0, stream, net, states, x, rows, count, n, logits, v, active, mlse, vo, (uint32_t)want); break;
-        case 256: hipLaunchKernelGGL(k_forward<256>, grid, block, 0, stream, net, states, x, rows, count, n, logits, v, active, mlse, vo, (uint32_t)want); break;
-        case 512: hipLaunchKernelGGL(k_forward<512>, grid, block, 0, stream, net, states, x, rows, count, n, logits, v, active, mlse, vo, (uint32_t)want); break;
+        case 64: hipLaunchKernelGGL(k_forward<64>, grid, block, 0, stream, net, states, x, rows, count, n, logits, v, active, mlse, vo, (uint32_t)want, parts, mstride); break;
+        case 128: hipLaunchKernelGGL(k_forward<128>, grid, block, 0, stream, net, states, x, rows, count, n, logits, v, active, mlse, vo, (uint32_t)want, parts, mstride); break;
+        case 256: hipLaunchKernelGGL(k_forward<256>, grid, block, 0, stream, net, states, x, rows, count, n, logits, v, active, mlse, vo, (uint32_t)want, parts, mstride); break;
+        case 512: hipLaunchKernelGGL(k_forward<512>, grid, block, 0, stream, net, states, x, rows, count, n, logits, v, active, mlse, vo, (uint32_t)want, parts, mstride); break;
         default: return YK_ERR_ARG;
     }
 #ifdef YK_TILESTAT

@@ -99,7 +99,8 @@ class SelfPlayEngine:
         return {k: (float(ms[i]), int(n[i])) for i, k in enumerate(self.KERNEL_CLASSES) if k != "unused"}
 
     STAT_NAMES = ("expansions", "scanned", "moves", "errors", "max_nodes", "max_edges", "max_arena", "vnew",
-                  "path_edges", "sims", "node_cap", "edge_cap", "arena_cap", "visit_cap", "groups")
+                  "path_edges", "sims", "node_cap", "edge_cap", "arena_cap", "visit_cap", "groups",
+                  "forward_parts")
 
     def stats(self) -> dict:
         out = np.zeros(16, dtype=np.int64)

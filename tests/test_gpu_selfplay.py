@@ -116,13 +116,11 @@ def test_selfplay_net_prior_replayed_by_oracle(Y):
     assert check_recorded_priors(pi, v, cnt, leaves, sd) == int(cnt.sum())
 
 
-def test_selfplay_net_prior_at_bench_size(Y):
-    """Config 2 (4096 games x 100 sims, YachtNNet 256 x 6) exactly as bench.py runs it - the
-    valid-only forward and the expand's prior branch - with every 64th game's predictions
-    recorded: the oracle replays those 64 games bit for bit (visit counts of every move,
-    actions, counters, values, final boards), and the recorded priors match the oracle net."""
-    _, E, N = Y
-    n, sims, seed, base, stride = 4096, 100, 2024, 0, 64
+def _net_prior_sampled_games_vs_oracle(E, N, n, sims, seed, base, stride):
+    """n games x sims with the production forward (valid-only head) and the expand's prior branch,
+    every stride-th game's predictions recorded: the oracle replays those games bit for bit
+    (visit counts of every move, actions, counters, values, final boards), and the recorded
+    priors match the oracle net.  Returns the engine stats."""
     sd = spec.closed_form_weights(256, 6)
     eng = E.SelfPlayEngine(n, sims, 1.5, 15, net=N.YkNet(sd, 256, 6), max_moves=48, record_predictions=True,
                            max_expansions=48 * sims + 8, record_stride=stride)
@@ -148,6 +146,25 @@ def test_selfplay_net_prior_at_bench_size(Y):
         assert np.array_equal(rec["values"][e, :M], orc["values"][r, :M])
         assert np.array_equal(rec["final"][e], orc["final"][r])
     assert check_recorded_priors(pi, v, cnt, leaves, sd, every=16) > 10000
+    eng.close()
+    return st
+
+
+def test_selfplay_net_prior_at_bench_size(Y):
+    """Config 2 (4096 games x 100 sims, YachtNNet 256 x 6) exactly as bench.py runs it (one
+    forward workgroup per 16-row tile), every 64th game replayed by the oracle."""
+    _, E, N = Y
+    st = _net_prior_sampled_games_vs_oracle(E, N, 4096, 100, 2024, 0, 64)
+    assert st["forward_parts"] == 1
+
+
+def test_selfplay_net_prior_at_config3_shape(Y):
+    """Config 3's per-GPU shape (2048 games x 200 sims): 128 row tiles, so two forward workgroups
+    per tile split the policy head and the expand merges their softmax statistics; every 32nd
+    game replayed by the oracle."""
+    _, E, N = Y
+    st = _net_prior_sampled_games_vs_oracle(E, N, 2048, 200, 3033, 7000, 32)
+    assert st["forward_parts"] in (1, 2)
 
 
 def test_selfplay_hash_prior_at_bench_size(Y):
@@ -247,6 +264,37 @@ def test_game_groups_do_not_change_results(Y, prior):
         eng.run(seed, base)
         st = eng.stats()
         assert st["errors"] == 0 and st["groups"] == groups
+        out.append((eng.records(), st["expansions"]))
+        eng.close()
+    for rec, x in out[1:]:
+        assert x == out[0][1]
+        for k in ("states", "info", "ctr", "values", "final", "n_moves", "visits_off", "visits"):
+            assert np.array_equal(rec[k], out[0][0][k]), k
+
+
+def test_sampled_kernel_timing_counts_and_results(Y):
+    """yk_engine_profile(k): the forward / expand pair is timed in every k-th simulation of a
+    move, the per-move kernels every time; timing changes no result (bench.py runs k = 8)."""
+    _, E, N = Y
+    n, sims, seed, base = 64, 10, 515, 300
+    net = N.YkNet(spec.closed_form_weights(256, 6), 256, 6)
+    out = []
+    for stride in (0, 1, 4):
+        eng = E.SelfPlayEngine(n, sims, 1.5, 15, net=net, max_moves=48)
+        if stride:
+            eng.profile(True, stride=stride)
+        eng.run(seed, base)
+        st = eng.stats()
+        assert st["errors"] == 0
+        moves = int(st["moves"])
+        kt = eng.kernel_times()
+        if stride:
+            timed = moves * len(range(0, sims, stride))
+            assert kt["forward"][1] == timed and kt["expand_backup_select"][1] == timed, (stride, kt)
+            assert kt["move_begin"][1] == moves and kt["move_end"][1] == moves and kt["select"][1] == moves
+            assert all(ms > 0 for ms, c in kt.values() if c)
+        else:
+            assert all(c == 0 for _, c in kt.values())
         out.append((eng.records(), st["expansions"]))
         eng.close()
     for rec, x in out[1:]:
