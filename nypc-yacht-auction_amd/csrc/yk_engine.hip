@@ -1375,7 +1375,7 @@ int yk_engine_create(yk_engine_t** out, const yk_engine_config_t* cfg, yk_net_t*
     // forward head split: when a group's row tiles do not fill the CUs, 2 or 4
     // workgroups per tile each take a slice of the policy head (the trunk runs in each)
 #ifndef YK_FPARTS_MAX
-#define YK_FPARTS_MAX 1  // 4 once measured on the GPU (tools/fparts_ab.sh)
+#define YK_FPARTS_MAX 4
 #endif
     {
         int cus = 256, dev = 0;

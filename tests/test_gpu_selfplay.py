@@ -164,7 +164,7 @@ def test_selfplay_net_prior_at_config3_shape(Y):
     game replayed by the oracle."""
     _, E, N = Y
     st = _net_prior_sampled_games_vs_oracle(E, N, 2048, 200, 3033, 7000, 32)
-    assert st["forward_parts"] in (1, 2)
+    assert st["forward_parts"] == (2 if torch.cuda.get_device_properties(0).multi_processor_count >= 256 else 1)
 
 
 def test_selfplay_hash_prior_at_bench_size(Y):
