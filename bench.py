@@ -276,7 +276,7 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel event timing")
-    ap.add_argument("--profile-stride", type=int, default=8,
+    ap.add_argument("--profile-stride", type=int, default=20,
                     help="time the forward / expand pair of every k-th simulation (1 = all; each event "
                          "record between dependent launches costs GPU time: ~5 %% of the batch at 1)")
     ap.add_argument("--no-arena", action="store_true", help="skip the config-4 Arena leg")
