@@ -1163,6 +1163,11 @@ struct yk_engine {
     yk_engine_config_t cfg;
     yk_net_t* net = nullptr;
     yk_net_t* net2 = nullptr;  // the opponent seat's net with dual trees (default: net)
+    // dual trees, one game group, row tiles x head parts x 2 <= CUs: the opponent seat's forward
+    // runs on its own stream beside the agent's (disjoint rows), with fparts_dual head parts
+    hipStream_t dstream = nullptr;
+    hipEvent_t ev_d0 = nullptr, ev_d1 = nullptr;
+    int fparts_single = 1, fparts_dual = 0;  // fparts_dual 0: the two forwards stay in sequence
     EngDev d{};
     std::vector<void*> allocs;
     float* logits = nullptr;
@@ -1288,13 +1293,23 @@ int run_sims(yk_engine* eng, int G, const hipStream_t* st, int sims, const uint3
                 // predict row = game: no compaction; workgroups without a leaf exit at once
                 // (dual trees: the agent's leaves on its net, then the opponent's on its own)
                 const int lo = d.e_lo;
+                const bool conc = d.dual && eng->dstream && G == 1;
+                if (conc) {  // the opponent's forward waits for this stream's last expand only
+                    YK_HIP(hipEventRecord(eng->ev_d0, st[g]));
+                    YK_HIP(hipStreamWaitEvent(eng->dstream, eng->ev_d0, 0));
+                }
                 for (int side = 0; side < (d.dual ? 2 : 1); side++) {
                     const yk_net_t* net = side ? eng->net2 : eng->net;
+                    hipStream_t fs = conc && side == 1 ? eng->dstream : st[g];
                     int rc = launch_forward(net->dev, d.leaf_state + lo, nullptr, nullptr, nullptr, d.e_hi - lo,
-                                            eng->logits + (size_t)lo * PI_LD, eng->vpred + lo, st[g],
+                                            eng->logits + (size_t)lo * PI_LD, eng->vpred + lo, fs,
                                             d.leaf_flag + lo, eng->mlse + lo, true, d.dual ? (uint8_t)(1u << side) : 0xFF,
                                             d.fparts, d.E);
                     if (rc) return rc;
+                }
+                if (conc) {
+                    YK_HIP(hipEventRecord(eng->ev_d1, eng->dstream));
+                    YK_HIP(hipStreamWaitEvent(st[g], eng->ev_d1, 0));
                 }
 #ifdef YK_STAGGER
                 if (G > 1) YK_HIP(hipEventRecord(eng->ev_fwd[g], st[g]));
@@ -1383,6 +1398,11 @@ int yk_engine_create(yk_engine_t** out, const yk_engine_config_t* cfg, yk_net_t*
         const int tiles = ((cfg->n_envs + G - 1) / G + 15) / 16;
         d.fparts = 1;
         while (d.fparts * 2 <= YK_FPARTS_MAX && tiles * d.fparts * 2 <= cus) d.fparts *= 2;
+        eng->fparts_single = d.fparts;
+        if (cfg->dual_trees && G == 1 && cfg->prior == 0 && 2 * tiles <= cus) {
+            eng->fparts_dual = 1;
+            while (eng->fparts_dual * 2 <= YK_FPARTS_MAX && 2 * tiles * eng->fparts_dual * 2 <= cus) eng->fparts_dual *= 2;
+        }
     }
     const size_t R = ((size_t)cfg->n_envs + d.rec_stride - 1) / d.rec_stride;
     const size_t E = (size_t)d.E, T = (size_t)d.T;
@@ -1453,6 +1473,12 @@ int yk_engine_create(yk_engine_t** out, const yk_engine_config_t* cfg, yk_net_t*
                 hipEventCreateWithFlags(&eng->ev_fwd[g], hipEventDisableTiming) != hipSuccess)
                 rc = YK_ERR_HIP;
     }
+    if (rc == YK_OK && eng->fparts_dual > 0) {
+        if (hipStreamCreateWithFlags(&eng->dstream, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&eng->ev_d0, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&eng->ev_d1, hipEventDisableTiming) != hipSuccess)
+            rc = YK_ERR_HIP;
+    }
     if (rc != YK_OK) {
         yk_engine_destroy(eng);
         return rc;
@@ -1486,6 +1512,9 @@ int yk_engine_destroy(yk_engine_t* eng) {
         if (eng->ev_fwd[g]) (void)hipEventDestroy(eng->ev_fwd[g]);
     }
     if (eng->ev_fork) (void)hipEventDestroy(eng->ev_fork);
+    if (eng->dstream) (void)hipStreamDestroy(eng->dstream);
+    if (eng->ev_d0) (void)hipEventDestroy(eng->ev_d0);
+    if (eng->ev_d1) (void)hipEventDestroy(eng->ev_d1);
     for (void* p : eng->allocs) (void)hipFree(p);
     if (eng->host_done) (void)hipHostFree(eng->host_done);
     delete eng;
@@ -1575,10 +1604,12 @@ int yk_arena(yk_engine_t* eng, uint64_t seed, uint32_t env_base, const int32_t* 
     d.arena_opp = opponent;
     // two MCTS players each keep their own tree (and net) when the engine has dual trees
     d.dual = (d.T == 2 * d.E && agent == YK_PLAYER_MCTS && opponent == YK_PLAYER_MCTS) ? 1 : 0;
+    if (d.dual && eng->dstream) d.fparts = eng->fparts_dual;  // the two seats' forwards side by side
     eng->have_arena = false;
     const int rc = play_batch(eng, seed, env_base, s);
     d.arena = 0;
     d.dual = 0;
+    d.fparts = eng->fparts_single;
     eng->have_arena = rc == YK_OK || rc == YK_ERR_STATE;
     return rc;
 }
