@@ -143,24 +143,15 @@ def arena_leg(net, games=1000, sims=25, seed=0, reps=3):
 
 def train_leg(model_sd, eng, steps=40, batch=512, seed=0):
     """Config 5's train step on one GPU (NNetWrapper.train semantics, NNet.py:118-174): minibatches
-    of 512 replay entries drawn from the self-play records just produced (packed boards, argmax
-    of the visit counts, values), forward + backward + clip + AdamW in f32, dropout 0.3."""
-    import numpy as np
+    of 512 replay entries drawn from the self-play records just produced - the device replay
+    buffer yk_examples_from_records builds (packed boards, argmax(pi) targets as
+    NNet.py:145-146 takes them, values) - forward + backward + clip + AdamW in f32, dropout 0.3."""
     import torch
 
-    from yacht_amd import kernels as K
+    from yacht_amd.replay import examples_from_images
     from yacht_amd.train import Trainer
-    rec = eng.records()
-    E, M = rec["n_moves"].shape[0], rec["states"].shape[1]
-    ok = np.arange(M)[None, :] < rec["n_moves"][:, None]
-    states = rec["states"][ok]
-    # hard targets: the chosen action for temp-0 moves, else the first most-visited action
-    info = rec["info"][ok]
-    tg = info[:, 2].astype(np.int32)
-    vals = rec["values"][ok].astype(np.float32)
-    S = K.states_to_device(states)
-    T = torch.tensor(tg, device="cuda")
-    V = torch.tensor(vals, device="cuda")
+    shard = examples_from_images(eng.pack_records(), eng.n_envs, eng.max_moves, eng.sims)
+    S, T, V = shard.states, shard.targets, shard.values
     n = S.shape[0]
     tr = Trainer(model_sd, H, NB, max_batch=batch, dropout=0.3, seed=seed)
     g = torch.Generator(device="cuda")
@@ -207,6 +198,44 @@ def shape_leg(net, envs=2048, sims=200, seed=0):
             "forward_parts": st["forward_parts"],
             "capacity_use": {k: int(st[k]) for k in ("max_nodes", "node_cap", "max_edges", "edge_cap", "max_arena",
                                                      "arena_cap")}}
+
+
+def f16_leg(sd, envs=4096, sims=100, seed=0):
+    """The opt-in fp16 predict mode (YK_PREDICT_F16: fp16 weights and GEMM inputs, f32
+    accumulation - the arithmetic of the reference's own GPU predict under autocast('cuda'),
+    NNet.py:186-189) at the headline shape: one warm-up batch, one timed batch, the forward's
+    roofline against the f16 dense MFMA peak (one MFMA per product).  Not the headline: the
+    headline keeps the f32-equivalent products the north star's 1e-5 tolerance needs."""
+    import torch
+
+    from yacht_amd.engine import SelfPlayEngine
+    from yacht_amd.nnet import YkNet
+    net16 = YkNet(sd, H, NB, precision="f16")
+    eng = SelfPlayEngine(envs, sims, 1.5, 15, net=net16, max_moves=64)
+    eng.run(seed + 600, 0)
+    torch.cuda.synchronize()
+    eng.profile(True, stride=20)
+    t0 = time.perf_counter()
+    eng.run(seed + 601, 0)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    st, kt = eng.stats(), eng.kernel_times()
+    eng.close()
+    if st["errors"]:
+        raise SystemExit(f"fp16 leg: engine error flags {st['errors']}")
+    out = {"config": f"{envs} games x {sims} sims, full episodes, YachtNNet {H} x {NB}, predict in fp16 "
+                     f"(one fp16 MFMA per product, f32 accumulation; LayerNorm / SiLU / softmax f32)",
+           "expansions_per_s": st["expansions"] / dt, "episodes_per_s": envs / dt, "s_per_batch": dt}
+    if kt.get("forward", (0, 0))[1]:
+        f_ms = kt["forward"][0] / kt["forward"][1]
+        x_ms = kt["expand_backup_select"][0] / kt["expand_backup_select"][1]
+        exp_per_launch = st["expansions"] / max(st["sims"] * st["groups"], 1)
+        ach = PREDICT_FLOP * exp_per_launch / (f_ms * 1e-3) / 1e12
+        out["kernel_avg_ms"] = {"forward": round(f_ms, 5), "expand_backup_select": round(x_ms, 5)}
+        out["roofline"] = {"kernel": "k_forward<256, 1>", "bound": "mfma", "achieved": ach,
+                           "peak": F16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": ach / F16_MFMA_PEAK_TFLOPS,
+                           "work_per_launch": f"{exp_per_launch:.0f} expansions x {PREDICT_FLOP} FLOP"}
+    return out
 
 
 def coach_leg(model, image, n_envs, max_moves, sims, world, train_steps=60, arena_games=256, arena_sims=25,
@@ -283,6 +312,7 @@ def main():
     ap.add_argument("--no-train", action="store_true", help="skip the config-5 train-step leg")
     ap.add_argument("--no-coach", action="store_true", help="skip the config-5 Coach-iteration leg")
     ap.add_argument("--no-shape", action="store_true", help="skip the config-3 shape leg (2048 x 200)")
+    ap.add_argument("--no-f16", action="store_true", help="skip the fp16 predict-mode leg")
     ap.add_argument("--dist-backend", default=None, help="nccl (RCCL, default on GPUs) or gloo (rehearsal)")
     ap.add_argument("--groups", type=int, default=0,
                     help="game groups on their own streams (0: the engine's auto choice)")
@@ -351,6 +381,26 @@ def main():
 
     tot = torch.tensor([elapsed, float(exps), float(games)], dtype=torch.float64,
                        device="cuda" if world > 1 and dist.get_backend() == "nccl" else "cpu")
+    gather_ok = None
+    if world > 1:
+        # the all-gather delivered every rank's image byte for byte: each rank compares its slot of
+        # the pooled buffer with its own freshly packed image, and every rank's checksum of every slot
+        # must agree across ranks
+        own = eng.pack_records(stream=stream)
+        g = last_gather[0]
+        mine = bool(torch.equal(g[rank].to(own.device), own))
+        w = torch.arange(1, g.shape[1] + 1, dtype=torch.int64, device=g.device) % 1000003
+        sums = (g.to(torch.int64) * w).sum(dim=1)  # one position-weighted checksum per slot
+        if dist.get_backend() != "nccl":
+            sums = sums.cpu()
+        allsums = [torch.zeros_like(sums) for _ in range(world)]
+        dist.all_gather(allsums, sums)
+        agree = all(torch.equal(a.cpu(), allsums[0].cpu()) for a in allsums)
+        flag = torch.tensor([1 if (mine and agree) else 0], dtype=torch.int32,
+                            device="cuda" if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        gather_ok = bool(flag.item())
+        del own
     if world > 1:
         t_max = tot[:1].clone()
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
@@ -379,8 +429,11 @@ def main():
                    "envs_per_gpu": args.envs, "sims": args.sims, "cpuct": 1.5, "temp_threshold": 15,
                    "parallelism": f"games sharded over {world} GPU(s), RCCL all-gather of trajectories"},
         "episodes_per_s": games / elapsed,
-        "value_basis": "whole job: expansions of all GPUs / the slowest rank's time (the metric's per-GPU "
-                       "rate is expansions_per_s_per_gpu)",
+        "value_basis": "whole job, as the bench contract defines `value` (the driver derives scaling "
+                       "efficiency from it): expansions of all GPUs / the slowest rank's time; the metric's "
+                       "per-GPU rate is value_per_gpu (= value at N=1)",
+        "value_total": value,
+        "value_per_gpu": value / world,
         "expansions_per_s_per_gpu": value / world,
         "expansions_per_episode_batch": exps / args.steps,
         "game_groups": st["groups"],
@@ -395,7 +448,10 @@ def main():
         imgs = [unpack_record_image(last_gather[0][r].cpu().numpy(), args.envs, 64, args.sims) for r in range(world)]
         ok = all(bool((im["n_moves"] == 48).all()) for im in imgs)
         ok = ok and len({im["final"].tobytes() for im in imgs}) == world
-        out["allgather_check"] = "ok" if ok else "FAILED"
+        out["allgather_check"] = "ok" if ok and gather_ok else "FAILED"
+        out["allgather_check_basis"] = ("every rank's slot of the pooled buffer equals that rank's own packed image "
+                                        "byte for byte, the per-slot checksums agree on all ranks, every game has "
+                                        "48 moves and the ranks' final boards differ")
         out["allgather_bytes"] = gathered_bytes
         out["dist_backend"] = dist.get_backend()
     if kt:
@@ -450,6 +506,8 @@ def main():
         out["coach"] = coach
     if world == 1 and not args.no_shape:
         out["config3_shape"] = shape_leg(net, seed=args.seed)
+    if world == 1 and not args.no_f16:
+        out["predict_f16"] = f16_leg(sd, args.envs, args.sims, seed=args.seed)
     if world == 1 and not args.no_arena:
         out["arena"] = arena_leg(net, seed=args.seed)
     if world == 1 and not args.no_train:

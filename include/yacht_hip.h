@@ -132,6 +132,14 @@ int yk_net_leaf_prior(yk_net_t* net, const yk_state_t* states, float* pi, float*
 int yk_net_policy_action(yk_net_t* net, const yk_state_t* states, int32_t* actions, float* probs, int n,
                          void* stream);
 int yk_net_destroy(yk_net_t* net);
+/* Precision of every forward of this net (predict, leaf prior, the engine's expansions):
+ * YK_PREDICT_F32 (default) - f32-equivalent products (fp16 hi/lo planes, three MFMAs each; within
+ * 1e-5 of the reference's float32 CPU path); YK_PREDICT_F16 - fp16 weights and GEMM inputs with
+ * f32 accumulation, one MFMA per product, as the reference's own GPU predict runs under
+ * autocast('cuda') (yacht/NNet.py:186-189).  LayerNorm, SiLU, softmax and tanh stay f32. */
+#define YK_PREDICT_F32 0
+#define YK_PREDICT_F16 1
+int yk_net_set_precision(yk_net_t* net, int mode);
 
 /* ---------------------------------------------------------------- self-play engine
  * Batched Coach.executeEpisode (Coach.py:34-72) over n_envs games in lock-step; every game
@@ -251,11 +259,18 @@ int yk_mcts_search(yk_engine_t* eng, const yk_state_t* roots, uint64_t seed, con
 int yk_mcts_reset(yk_engine_t* eng);
 
 /* ---------------------------------------------------------------- training
- * NNetWrapper.train (yacht/NNet.py:118-174): one optimiser step per minibatch of YachtNNet in
- * float32 - loss = cross_entropy(logits, argmax(pi)) + vloss_weight * mse(v, z) (:143-148),
- * clip_grad_norm_(max_grad_norm) (:152-153), AdamW(lr, weight_decay) (:109-110).  Dropout masks
- * come from the Philox stream (seed, layer, step, element), not torch's generator.
- * Parameters, gradients and Adam moments are flat device buffers in state_dict order. */
+ * NNetWrapper.train (yacht/NNet.py:118-174): one optimiser step per minibatch of YachtNNet -
+ * loss = cross_entropy(logits, argmax(pi)) + vloss_weight * mse(v, z) (:143-148),
+ * clip_grad_norm_(max_grad_norm) (:152-153), AdamW(lr, weight_decay) (:109-110).  Two modes:
+ * amp = 0, float32 (the reference's CPU path, :157-165); amp = 1, the reference's GPU path
+ * (:113-116, 141-155): autocast('cuda') arithmetic (fp16 Linear layers with f32 accumulation,
+ * f32 LayerNorm and losses) on fp16 MFMA kernels, loss scaling with GradScaler('cuda')
+ * semantics (init_scale, x2 after growth_interval finite steps, x0.5 and the step skipped on an
+ * inf / nan gradient), unscale before the clip.  Dropout masks come from the Philox stream
+ * (seed, layer, step, row, column), not torch's generator; rows are numbered from the offset set
+ * by yk_trainer_set_row_offset (0 by default), so ranks splitting one minibatch draw the masks of
+ * the whole minibatch.  Parameters, gradients and Adam moments are flat device buffers in
+ * state_dict order. */
 typedef struct {
     int max_batch;          /* batch_size (rows per step, upper bound) */
     float lr, weight_decay; /* AdamW */
@@ -264,6 +279,9 @@ typedef struct {
     float vloss_weight;     /* 1.5 in main.py */
     float dropout;          /* 0.3 in main.py; 0 for deterministic parity tests */
     uint64_t seed;          /* dropout stream */
+    int amp;                /* 0: float32 step; 1: mixed precision (autocast + GradScaler) */
+    float init_scale;       /* GradScaler init_scale (0: 65536) */
+    int growth_interval;    /* GradScaler growth_interval (0: 2000) */
 } yk_train_config_t;
 typedef struct yk_trainer yk_trainer_t;
 /* params: HOST float32 arrays in YachtNNet.state_dict() order (as yk_net_create) */
@@ -289,6 +307,11 @@ int yk_trainer_losses(yk_trainer_t* t, double* out);
 int yk_trainer_get(yk_trainer_t* t, int which, float* const* out);
 int yk_trainer_set(yk_trainer_t* t, int which, const float* const* in, int64_t step);
 int64_t yk_trainer_step_count(yk_trainer_t* t);
+/* the global row number of the next backward's first example (dropout masks; DDP ranks pass
+ * their offset into the minibatch) */
+int yk_trainer_set_row_offset(yk_trainer_t* t, int64_t row0);
+/* HOST out[4] (amp mode): loss scale, growth tracker, optimiser steps taken, last step skipped */
+int yk_trainer_amp_state(yk_trainer_t* t, double* out);
 
 #ifdef __cplusplus
 }

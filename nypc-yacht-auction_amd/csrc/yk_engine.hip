@@ -1395,7 +1395,9 @@ int yk_engine_create(yk_engine_t** out, const yk_engine_config_t* cfg, yk_net_t*
     {
         int cus = 256, dev = 0;
         if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        const int tiles = ((cfg->n_envs + G - 1) / G + 15) / 16;
+        // the G groups' forwards run at once on their own streams: the bound counts every group's
+        // tiles (sizing from one group's tiles oversubscribed the chip at G = 4)
+        const int tiles = G * (((cfg->n_envs + G - 1) / G + 15) / 16);
         d.fparts = 1;
         while (d.fparts * 2 <= YK_FPARTS_MAX && tiles * d.fparts * 2 <= cus) d.fparts *= 2;
         eng->fparts_single = d.fparts;

@@ -26,6 +26,7 @@ struct NetDev {
     const float* vblk;   // per block b: b1 g1 be1 b2 g2 be2 ([6][H]), staged to LDS per block
     float pi_bspread;    // max - min of pi_head.2's bias over the 3226 actions
     float pi_wmax;       // max over actions of |pi_head.2 weight row|_2
+    int planes;          // 2: f32-equivalent hi/lo products (default); 1: fp16 mode (hi planes only)
 };
 // vstat offsets in units of H (b_v1 at VS_BV1*H, w_v2 right after it, b_pi at vs_bpi(H))
 enum { VS_BIN = 0, VS_GIN = 1, VS_BEIN = 2, VS_GPI = 3, VS_BEPI = 4, VS_GV = 5, VS_BEV = 6, VS_BV1 = 7 };

@@ -68,7 +68,9 @@ constexpr int PCH = 4;       // policy-head tiles per chunk
 #ifndef YK_PW
 #define YK_PW 2
 #endif
-constexpr int PW = YK_PW;    // policy-head ring depth (32-deep slices)
+// policy-head ring depth (32-deep slices): a single fp16 plane (PL = 1, the fp16 predict mode)
+// takes half the registers per slice, so its ring is twice as deep
+constexpr int pw_of(int PL) { return PL == 1 ? 2 * YK_PW : YK_PW; }
 constexpr float SPLIT = 2048.f, UNSPLIT = 1.f / 2048.f;  // lo plane scale (keeps it out of fp16 subnormals)
 constexpr int REAL_TILES = (ASIZE + 15) / 16;  // policy tiles holding an action column (202 of 204)
 constexpr float FULL_SPREAD = 80.f;  // logit spread bound above which a workgroup takes the full pass
@@ -100,8 +102,11 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 struct W2 {
     float4 h, l;
 };
+// PL = 1 (fp16 predict mode) loads the hi plane only: half the weight bytes of the stream
+template <int PL>
 __device__ __forceinline__ W2 ld_w2(const float* __restrict__ P, int KS, int nt, int ks, int lane) {
     const float* p = P + ((long)(nt * KS + ks) * 2 * 64 + lane) * 4;
+    if constexpr (PL == 1) return W2{*reinterpret_cast<const float4*>(p), make_float4(0.f, 0.f, 0.f, 0.f)};
     return W2{*reinterpret_cast<const float4*>(p), *reinterpret_cast<const float4*>(p + 256)};
 }
 
@@ -116,7 +121,20 @@ struct Acc3 {
     floatx4 m, c;
 };
 __device__ __forceinline__ void acc_zero(Acc3& a) { a.m = a.c = floatx4{0.f, 0.f, 0.f, 0.f}; }
-__device__ __forceinline__ floatx4 combine(const Acc3& a) { return a.m + a.c * UNSPLIT; }
+template <int PL>
+__device__ __forceinline__ floatx4 combine(const Acc3& a) {
+    if constexpr (PL == 1) return a.m;
+    return a.m + a.c * UNSPLIT;
+}
+// one 16x16x32 product into the accumulators: hi*hi (+ the two cross terms when PL = 2)
+template <int PL>
+__device__ __forceinline__ void mma3(Acc3& c, float4 ah, float4 al, const W2& w) {
+    c.m = mfma16(ah, w.h, c.m);
+    if constexpr (PL == 2) {
+        c.c = mfma16(ah, w.l, c.c);
+        c.c = mfma16(al, w.h, c.c);
+    }
+}
 
 // A fragment of a plane pair in LDS (row stride SA halves): lane l reads row l & 15,
 // k = 32 ks + 8 (l >> 4) .. + 7 of each plane.
@@ -132,7 +150,7 @@ __device__ __forceinline__ APtr a_ptr(const _Float16* planes, int sa) {
 __device__ __forceinline__ float4 ld_a(const _Float16* p, int ks) { return *reinterpret_cast<const float4*>(p + 32 * ks); }
 
 // x -> (hi, lo * 2^11) into row r, column c of a plane pair (row stride sa halves), VPL values
-template <int VPL>
+template <int PL, int VPL>
 __device__ __forceinline__ void put_planes(_Float16* planes, int sa, int r, int c, const float (&x)[VPL]) {
     _Float16 h[VPL], l[VPL];
 #pragma unroll
@@ -144,12 +162,12 @@ __device__ __forceinline__ void put_planes(_Float16* planes, int sa, int r, int 
     _Float16* pl = planes + ROWS * sa + r * sa + c;
     if constexpr (VPL == 4) {
         *reinterpret_cast<half4*>(ph) = half4{h[0], h[1], h[2], h[3]};
-        *reinterpret_cast<half4*>(pl) = half4{l[0], l[1], l[2], l[3]};
+        if constexpr (PL == 2) *reinterpret_cast<half4*>(pl) = half4{l[0], l[1], l[2], l[3]};
     } else {
 #pragma unroll
         for (int i = 0; i < VPL; i++) {
             ph[i] = h[i];
-            pl[i] = l[i];
+            if constexpr (PL == 2) pl[i] = l[i];
         }
     }
 }
@@ -158,7 +176,7 @@ __device__ __forceinline__ void put_planes(_Float16* planes, int sa, int r, int 
 // weight slices taken from the ring; slice ks lives in slot ks % RW.  After use, the slot is
 // refilled with slice ks + RW of this layer (cur) or, past its end, of the next layer (nxt,
 // same shape).
-template <int K, int NT, int RW, bool NEXT = true>
+template <int PL, int K, int NT, int RW, bool NEXT = true>
 __device__ __forceinline__ void mma_ring(const _Float16* A, int sa, W2 (&ring)[RW][NT], floatx4 (&acc)[NT],
                                          const float* __restrict__ cur, const float* __restrict__ nxt, int nt0) {
     constexpr int KS = K / 32;
@@ -170,26 +188,29 @@ __device__ __forceinline__ void mma_ring(const _Float16* A, int sa, W2 (&ring)[R
     float4 ah = ld_a(ap.h, 0), al = ld_a(ap.l, 0);
 #pragma unroll
     for (int ks = 0; ks < KS; ks++) {
-        const float4 ahn = ld_a(ap.h, (ks + 1) % KS), aln = ld_a(ap.l, (ks + 1) % KS);
+        const float4 ahn = ld_a(ap.h, (ks + 1) % KS);
+        const float4 aln = PL == 2 ? ld_a(ap.l, (ks + 1) % KS) : ahn;
         W2(&w)[NT] = ring[ks % RW];
 #pragma unroll
         for (int t = 0; t < NT; t++) c[t].m = mfma16(ah, w[t].h, c[t].m);
+        if constexpr (PL == 2) {
 #pragma unroll
-        for (int t = 0; t < NT; t++) c[t].c = mfma16(ah, w[t].l, c[t].c);
+            for (int t = 0; t < NT; t++) c[t].c = mfma16(ah, w[t].l, c[t].c);
 #pragma unroll
-        for (int t = 0; t < NT; t++) c[t].c = mfma16(al, w[t].h, c[t].c);
+            for (int t = 0; t < NT; t++) c[t].c = mfma16(al, w[t].h, c[t].c);
+        }
         const int g = ks + RW;
         if (g < KS || NEXT) {
 #pragma unroll
             for (int t = 0; t < NT; t++)
-                w[t] = g < KS ? ld_w2(cur, KS, nt0 + t, g, lane) : ld_w2(nxt, KS, nt0 + t, g - KS, lane);
+                w[t] = g < KS ? ld_w2<PL>(cur, KS, nt0 + t, g, lane) : ld_w2<PL>(nxt, KS, nt0 + t, g - KS, lane);
         }
         __builtin_amdgcn_sched_barrier(0);  // keep the refill here, a ring's depth ahead of its use
         ah = ahn;
         al = aln;
     }
 #pragma unroll
-    for (int t = 0; t < NT; t++) acc[t] = combine(c[t]);
+    for (int t = 0; t < NT; t++) acc[t] = combine<PL>(c[t]);
 }
 
 // D[16 x 16] tile t of the wave: lane holds rows 4(l>>4)+j, column 16(nt0 + t) + (l&15).
@@ -321,15 +342,17 @@ __device__ __forceinline__ void layernorm2(f2v (&x)[R][NP], const float* g, cons
     ln_stats2<NP, R>(x, mean, rstd, H);
     ln_apply2<NP, R>(x, mean, rstd, g, b, c0);
 }
-template <int NP>
+template <int PL, int NP>
 __device__ __forceinline__ void put_planes2(_Float16* planes, int sa, int r, int c, const f2v (&x)[NP]) {
 #pragma unroll
     for (int i = 0; i < NP; i++) {
         const h2v h = __builtin_convertvector(x[i], h2v);
-        const f2v back = __builtin_convertvector(h, f2v);
-        const h2v l = __builtin_convertvector((x[i] - back) * SPLIT, h2v);
         *reinterpret_cast<h2v*>(planes + r * sa + c + 2 * i) = h;
-        *reinterpret_cast<h2v*>(planes + ROWS * sa + r * sa + c + 2 * i) = l;
+        if constexpr (PL == 2) {
+            const f2v back = __builtin_convertvector(h, f2v);
+            const h2v l = __builtin_convertvector((x[i] - back) * SPLIT, h2v);
+            *reinterpret_cast<h2v*>(planes + ROWS * sa + r * sa + c + 2 * i) = l;
+        }
     }
 }
 
@@ -338,7 +361,7 @@ __device__ __forceinline__ void put_planes2(_Float16* planes, int sa, int r, int
 // chunk, NTL <= PCH in a wave's last chunk.  The ring (RD slices of PCH tiles) streams across
 // chunk boundaries: past the last slice it refills with the next chunk's first slices (NXT tiles).
 // Chunk shapes are template parameters, so the loop body has no branches.
-template <int KS, int NTL, int NXT, int RD = (PW < KS ? PW : KS)>
+template <int PL, int KS, int NTL, int NXT, int RD = (pw_of(PL) < KS ? pw_of(PL) : KS)>
 __device__ __forceinline__ void ring_chunk(const _Float16* A, int sa, W2 (&ring)[RD][PCH], floatx4 (&pa)[NTL],
                                            const float* __restrict__ W, const int (&tile)[PCH],
                                            const float* __restrict__ Wn, const int (&ntile)[PCH]) {
@@ -350,28 +373,31 @@ __device__ __forceinline__ void ring_chunk(const _Float16* A, int sa, W2 (&ring)
     float4 ah = ld_a(ap.h, 0), al = ld_a(ap.l, 0);
 #pragma unroll
     for (int ks = 0; ks < KS; ks++) {
-        const float4 ahn = ld_a(ap.h, (ks + 1) % KS), aln = ld_a(ap.l, (ks + 1) % KS);
+        const float4 ahn = ld_a(ap.h, (ks + 1) % KS);
+        const float4 aln = PL == 2 ? ld_a(ap.l, (ks + 1) % KS) : ahn;
         W2(&w)[PCH] = ring[ks % RD];
 #pragma unroll
         for (int t = 0; t < NTL; t++) c[t].m = mfma16(ah, w[t].h, c[t].m);
+        if constexpr (PL == 2) {
 #pragma unroll
-        for (int t = 0; t < NTL; t++) c[t].c = mfma16(ah, w[t].l, c[t].c);
+            for (int t = 0; t < NTL; t++) c[t].c = mfma16(ah, w[t].l, c[t].c);
 #pragma unroll
-        for (int t = 0; t < NTL; t++) c[t].c = mfma16(al, w[t].h, c[t].c);
+            for (int t = 0; t < NTL; t++) c[t].c = mfma16(al, w[t].h, c[t].c);
+        }
         const int g = ks + RD;
         if (g < KS) {
 #pragma unroll
-            for (int t = 0; t < NTL; t++) w[t] = ld_w2(W, KS, tile[t], g, lane);
+            for (int t = 0; t < NTL; t++) w[t] = ld_w2<PL>(W, KS, tile[t], g, lane);
         } else {
 #pragma unroll
-            for (int t = 0; t < NXT; t++) w[t] = ld_w2(Wn, KS, ntile[t], g - KS, lane);
+            for (int t = 0; t < NXT; t++) w[t] = ld_w2<PL>(Wn, KS, ntile[t], g - KS, lane);
         }
         __builtin_amdgcn_sched_barrier(0);
         ah = ahn;
         al = aln;
     }
 #pragma unroll
-    for (int t = 0; t < NTL; t++) pa[t] = combine(c[t]);
+    for (int t = 0; t < NTL; t++) pa[t] = combine<PL>(c[t]);
 }
 // Which logits of a row are stored (valid_only launches: the engine reads a leaf's logits only
 // at its valid actions, MCTS.py:87-88, so the rest never leave the CU): per row a mode nibble -
@@ -454,14 +480,14 @@ __device__ __forceinline__ void stat_merge(float& m, float& s, float m2, float s
 // one chunk of policy tiles: a row's logits (+ bias) in the tiles it keeps a column in (`allc`:
 // every real column) - a set that depends on the row alone - stored and folded into its running
 // (max, sum exp): one rescale per row and chunk.  Lane (q, c) holds rows 4 q + j, column c.
-template <int KS, int NTL, int NXT, int RD = (PW < KS ? PW : KS)>
+template <int PL, int KS, int NTL, int NXT, int RD = (pw_of(PL) < KS ? pw_of(PL) : KS)>
 __device__ __forceinline__ void pi_chunk(const _Float16* A, int sa, W2 (&ring)[RD][PCH], const float* __restrict__ W,
                                          const int (&tile)[PCH], const int (&ntile)[PCH], const float* bias,
                                          float* __restrict__ logits, int row0, int n, float (&sm)[4], float (&ss)[4],
                                          const uint16_t* trb, const bool (&allc)[4]) {
     const int lane = threadIdx.x & 63;
     floatx4 pa[NTL];
-    ring_chunk<KS, NTL, NXT, RD>(A, sa, ring, pa, W, tile, W, ntile);
+    ring_chunk<PL, KS, NTL, NXT, RD>(A, sa, ring, pa, W, tile, W, ntile);
     const int rr = lane & 15, q = lane >> 4;
 #pragma unroll
     for (int t = 0; t < NTL; t++) {
@@ -506,7 +532,10 @@ __device__ __forceinline__ void pi_chunk(const _Float16* A, int sa, W2 (&ring)[R
 }
 
 // Row passes (LayerNorm / SiLU / residual): wave w owns rows RPW w ... RPW w + RPW - 1.
-template <int H>
+// PL = 2: f32-equivalent hi/lo planes (the parity mode); PL = 1: one fp16 plane of weights and
+// GEMM inputs with f32 accumulation (the fp16 predict mode, as the reference's autocast('cuda')
+// predict, NNet.py:186-189; LayerNorm, SiLU, softmax and the value head stay f32)
+template <int H, int PL>
 __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* __restrict__ states,
                                                  const float* __restrict__ xin, const int32_t* __restrict__ rows,
                                                  const int32_t* __restrict__ count, int n,
@@ -599,13 +628,13 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
 #pragma unroll
         for (int ks = 0; ks < 2; ks++)
 #pragma unroll
-            for (int t = 0; t < NT; t++) w0[ks][t] = ld_w2(net.w_in, 2, nt0 + t, ks, lane);
+            for (int t = 0; t < NT; t++) w0[ks][t] = ld_w2<PL>(net.w_in, 2, nt0 + t, ks, lane);
     }
     if (gw && net.NB > 0) {
 #pragma unroll
         for (int ks = 0; ks < RW; ks++)
 #pragma unroll
-            for (int t = 0; t < NT; t++) ring[ks][t] = ld_w2(w_first, KS, nt0 + t, ks, lane);
+            for (int t = 0; t < NT; t++) ring[ks][t] = ld_w2<PL>(w_first, KS, nt0 + t, ks, lane);
     }
     // featurize (state_to_vec, NNet.py:65-86) straight into the input layer's planes, K = 64
     uint32_t vdk[FPT];
@@ -616,7 +645,7 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
         float val = 0.f;
         if (row < n && f < FEAT) val = xin ? xin[(long)(rows ? rows[row] : row) * FEAT + f] : feature(fs[k], f);
         const float one[1] = {val};
-        put_planes<1>(P, SA, rr, f, one);
+        put_planes<PL, 1>(P, SA, rr, f, one);
         const uint32_t vdr = row >= n || !((amask >> rr) & 1u) ? LM_NONE
                              : (valid_only && !xin) ? logit_mode(fs[k]) : LM_ALL;
         if (lane == 0) VD[rr] = vdr;
@@ -645,16 +674,13 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
         for (int t = 0; t < NT; t++) acc_zero(c[t]);
 #pragma unroll
         for (int ks = 0; ks < 2; ks++) {
-            const float4 ah = ld_a(ap.h, ks), al = ld_a(ap.l, ks);
+            const float4 ah = ld_a(ap.h, ks);
+            const float4 al = PL == 2 ? ld_a(ap.l, ks) : ah;
 #pragma unroll
-            for (int t = 0; t < NT; t++) {
-                c[t].m = mfma16(ah, w0[ks][t].h, c[t].m);
-                c[t].c = mfma16(ah, w0[ks][t].l, c[t].c);
-                c[t].c = mfma16(al, w0[ks][t].h, c[t].c);
-            }
+            for (int t = 0; t < NT; t++) mma3<PL>(c[t], ah, al, w0[ks][t]);
         }
 #pragma unroll
-        for (int t = 0; t < NT; t++) acc[t] = combine(c[t]);
+        for (int t = 0; t < NT; t++) acc[t] = combine<PL>(c[t]);
         store_acc<NT>(T, LD, nt0, acc, nullptr);
     }
     lds_barrier();  // T complete; every wave is done reading the feature planes
@@ -692,7 +718,7 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
                 x[rr][i] = silu2(x[rr][i]);
                 *reinterpret_cast<f2v*>(X + r * LD + c0 + 2 * i) = x[rr][i];
             }
-            put_planes2<VPL / 2>(P, SA, r, c0, x[rr]);
+            put_planes2<PL, VPL / 2>(P, SA, r, c0, x[rr]);
         }
     } else {
 #pragma unroll
@@ -707,7 +733,7 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
                 x[i] = silu(x[i]);
                 X[r * LD + c0 + i] = x[i];
             }
-            put_planes<VPL>(P, SA, r, c0, x);
+            put_planes<PL, VPL>(P, SA, r, c0, x);
         }
     }
     lds_barrier();
@@ -721,7 +747,7 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
         float4 vb[PB];
 #pragma unroll
         for (int k = 0; k < PB; k++) vb[k] = reinterpret_cast<const float4*>(net.vblk + (long)b * NVB)[min(tid + NTHR * k, NB4 - 1)];
-        if (gw) mma_ring<H, NT, RW>(P, SA, ring, acc, net.w1 + wo, net.w2 + wo, nt0);
+        if (gw) mma_ring<PL, H, NT, RW>(P, SA, ring, acc, net.w1 + wo, net.w2 + wo, nt0);
         if (b == 2) TSTAMP(16);
 #pragma unroll
         for (int k = 0; k < PB; k++)  // the previous block's readers passed a barrier
@@ -738,7 +764,7 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
                     x[rr][i] = silu2(ld2(T + (wave * RPW + rr) * LD + c0 + 2 * i) + ld2(VB + c0 + 2 * i));
             layernorm2<VPL / 2, RPW>(x, VB + H, VB + 2 * H, c0, H);
 #pragma unroll
-            for (int rr = 0; rr < RPW; rr++) put_planes2<VPL / 2>(P, SA, wave * RPW + rr, c0, x[rr]);  // fc2's input
+            for (int rr = 0; rr < RPW; rr++) put_planes2<PL, VPL / 2>(P, SA, wave * RPW + rr, c0, x[rr]);  // fc2's input
         } else {
 #pragma unroll
             for (int rr = 0; rr < RPW; rr++) {
@@ -747,14 +773,14 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
 #pragma unroll
                 for (int i = 0; i < VPL; i++) x[i] = silu(T[r * LD + c0 + i] + VB[c0 + i]);
                 layernorm<VPL>(x, VB + H, VB + 2 * H, c0, H);
-                put_planes<VPL>(P, SA, r, c0, x);  // fc2's input
+                put_planes<PL, VPL>(P, SA, r, c0, x);  // fc2's input
             }
         }
         lds_barrier();
         if (b == 2) TSTAMP(18);
         if (gw) {
-            if (b + 1 < net.NB) mma_ring<H, NT, RW>(P, SA, ring, acc, net.w2 + wo, after, nt0);
-            else mma_ring<H, NT, RW, false>(P, SA, ring, acc, net.w2 + wo, nullptr, nt0);
+            if (b + 1 < net.NB) mma_ring<PL, H, NT, RW>(P, SA, ring, acc, net.w2 + wo, after, nt0);
+            else mma_ring<PL, H, NT, RW, false>(P, SA, ring, acc, net.w2 + wo, nullptr, nt0);
         }
         if (b == 2) TSTAMP(19);
         if (gw) store_acc<NT>(T, LD, nt0, acc, nullptr);
@@ -776,7 +802,7 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
                     x[rr][i] = x[rr][i] + ld2(X + r * LD + c0 + 2 * i);
                     *reinterpret_cast<f2v*>(X + r * LD + c0 + 2 * i) = x[rr][i];
                 }
-                if (b + 1 < net.NB) put_planes2<VPL / 2>(P, SA, r, c0, x[rr]);  // the next fc1's input
+                if (b + 1 < net.NB) put_planes2<PL, VPL / 2>(P, SA, r, c0, x[rr]);  // the next fc1's input
             }
         } else {
 #pragma unroll
@@ -791,7 +817,7 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
                     x[i] += X[r * LD + c0 + i];
                     X[r * LD + c0 + i] = x[i];
                 }
-                if (b + 1 < net.NB) put_planes<VPL>(P, SA, r, c0, x);  // the next fc1's input
+                if (b + 1 < net.NB) put_planes<PL, VPL>(P, SA, r, c0, x);  // the next fc1's input
             }
         }
         lds_barrier();
@@ -801,12 +827,12 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
     // heads: pi_head = LN -> SiLU -> Linear; v_head = LN -> SiLU -> Linear -> SiLU -> Linear -> tanh.
     // One ring streams v_head.2 (one 16-column tile per wave, first) and then the policy head;
     // its first slices fly under the LayerNorms.  a_pi's planes go to P, a_v's to T's storage.
-    constexpr int RD = PW < KS ? PW : KS;  // policy ring depth (slices)
+    constexpr int RD = pw_of(PL) < KS ? pw_of(PL) : KS;  // policy ring depth (slices)
     static_assert(KS % RD == 0 && KS % RW == 0, "a ring's refills cross into the next chunk / layer slot-aligned");
     _Float16* PV = reinterpret_cast<_Float16*>(T);
     W2 pring[RD][PCH];
 #pragma unroll
-    for (int ks = 0; ks < RD; ks++) pring[ks][0] = ld_w2(net.w_v1, KS, wave, ks, lane);
+    for (int ks = 0; ks < RD; ks++) pring[ks][0] = ld_w2<PL>(net.w_v1, KS, wave, ks, lane);
     if constexpr (VPL % 2 == 0) {
         // both heads' LayerNorms see the same row: one set of statistics, two affine maps
         f2v x[RPW][VPL / 2], y[RPW][VPL / 2];
@@ -829,8 +855,8 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
                 y[rr][i] = silu2(y[rr][i]);  // a_v
                 a = a + x[rr][i] * x[rr][i];
             }
-            put_planes2<VPL / 2>(P, SA, r, c0, x[rr]);
-            put_planes2<VPL / 2>(PV, SA, r, c0, y[rr]);
+            put_planes2<PL, VPL / 2>(P, SA, r, c0, x[rr]);
+            put_planes2<PL, VPL / 2>(PV, SA, r, c0, y[rr]);
             h2[rr] = a.x + a.y;
         }
 #pragma unroll
@@ -852,8 +878,8 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
                 x[i] = silu(x[i]);  // a_pi
                 y[i] = silu(y[i]);  // a_v
             }
-            put_planes<VPL>(P, SA, r, c0, x);
-            put_planes<VPL>(PV, SA, r, c0, y);
+            put_planes<PL, VPL>(P, SA, r, c0, x);
+            put_planes<PL, VPL>(PV, SA, r, c0, y);
             float h2 = 0.f;
 #pragma unroll
             for (int i = 0; i < VPL; i++) h2 += x[i] * x[i];
@@ -937,11 +963,11 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
         const int vt[PCH] = {wave, 0, 0, 0};
         static_assert(PCH == 4, "chunk-shape dispatch below");
         switch (chunk_n(0)) {
-            case 0: ring_chunk<KS, 1, 0>(PV, SA, pring, av, net.w_v1, vt, net.w_pi, tcur); break;
-            case 1: ring_chunk<KS, 1, 1>(PV, SA, pring, av, net.w_v1, vt, net.w_pi, tcur); break;
-            case 2: ring_chunk<KS, 1, 2>(PV, SA, pring, av, net.w_v1, vt, net.w_pi, tcur); break;
-            case 3: ring_chunk<KS, 1, 3>(PV, SA, pring, av, net.w_v1, vt, net.w_pi, tcur); break;
-            default: ring_chunk<KS, 1, 4>(PV, SA, pring, av, net.w_v1, vt, net.w_pi, tcur); break;
+            case 0: ring_chunk<PL, KS, 1, 0>(PV, SA, pring, av, net.w_v1, vt, net.w_pi, tcur); break;
+            case 1: ring_chunk<PL, KS, 1, 1>(PV, SA, pring, av, net.w_v1, vt, net.w_pi, tcur); break;
+            case 2: ring_chunk<PL, KS, 1, 2>(PV, SA, pring, av, net.w_v1, vt, net.w_pi, tcur); break;
+            case 3: ring_chunk<PL, KS, 1, 3>(PV, SA, pring, av, net.w_v1, vt, net.w_pi, tcur); break;
+            default: ring_chunk<PL, KS, 1, 4>(PV, SA, pring, av, net.w_v1, vt, net.w_pi, tcur); break;
         }
     }
     float sm[4], ss[4];  // running max and sum exp of the lane's rows 4 q + j
@@ -953,7 +979,7 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
         allc[j] = row_allc(4 * (lane >> 4) + j);
     }
 #define YK_PI_CHUNK(NTL, NXT) \
-    pi_chunk<KS, NTL, NXT>(P, SA, pring, net.w_pi, tcur, tnxt, bpi, logits, row0, n, sm, ss, TRB, allc)
+    pi_chunk<PL, KS, NTL, NXT>(P, SA, pring, net.w_pi, tcur, tnxt, bpi, logits, row0, n, sm, ss, TRB, allc)
 #pragma unroll 1
     for (int c = 0; c < nch; c++) {
         chunk_tiles(c + 1, tnxt);
@@ -1094,13 +1120,17 @@ int launch_forward(const NetDev& net, const yk_state_t* states, const float* x, 
     if (parts < 1 || parts > 4 || (parts > 1 && (!mlse || mstride < n))) return YK_ERR_ARG;
     const dim3 grid((unsigned)((n + ROWS - 1) / ROWS * parts)), block(NTHR);
     const int vo = valid_only ? 1 : 0;
+#define YK_FWD(HH, PP) hipLaunchKernelGGL((k_forward<HH, PP>), grid, block, 0, stream, net, states, x, rows, count, n, \
+                                           logits, v, active, mlse, vo, (uint32_t)want, parts, mstride)
+    const bool f16 = net.planes == 1;
     switch (net.H) {
-        case 64: hipLaunchKernelGGL(k_forward<64>, grid, block, 0, stream, net, states, x, rows, count, n, logits, v, active, mlse, vo, (uint32_t)want, parts, mstride); break;
-        case 128: hipLaunchKernelGGL(k_forward<128>, grid, block, 0, stream, net, states, x, rows, count, n, logits, v, active, mlse, vo, (uint32_t)want, parts, mstride); break;
-        case 256: hipLaunchKernelGGL(k_forward<256>, grid, block, 0, stream, net, states, x, rows, count, n, logits, v, active, mlse, vo, (uint32_t)want, parts, mstride); break;
-        case 512: hipLaunchKernelGGL(k_forward<512>, grid, block, 0, stream, net, states, x, rows, count, n, logits, v, active, mlse, vo, (uint32_t)want, parts, mstride); break;
+        case 64: if (f16) YK_FWD(64, 1); else YK_FWD(64, 2); break;
+        case 128: if (f16) YK_FWD(128, 1); else YK_FWD(128, 2); break;
+        case 256: if (f16) YK_FWD(256, 1); else YK_FWD(256, 2); break;
+        case 512: if (f16) YK_FWD(512, 1); else YK_FWD(512, 2); break;
         default: return YK_ERR_ARG;
     }
+#undef YK_FWD
 #ifdef YK_TILESTAT
     if (valid_only) hipLaunchKernelGGL(k_tilestat_flush, dim3(1), dim3(1), 0, stream);
 #endif
@@ -1209,6 +1239,7 @@ int yk_net_create(yk_net_t** out, int H, int NB, const float* const* p, int npar
     const float* B = net->blob;
     NetDev& d = net->dev;
     d.H = H; d.NB = NB;
+    d.planes = 2;  // f32-equivalent (yk_net_set_precision switches to the fp16 mode)
     d.w_in = B + o_win; d.b_in = B + o_bin; d.g_in = B + o_gin; d.be_in = B + o_bein;
     d.w1 = B + o_w1; d.b1 = B + o_b1; d.g1 = B + o_g1; d.be1 = B + o_be1;
     d.w2 = B + o_w2; d.b2 = B + o_b2; d.g2 = B + o_g2; d.be2 = B + o_be2;
@@ -1232,6 +1263,12 @@ int yk_diag_tiles(uint64_t* out) {  // HOST out[16]; resets the counters
     return YK_OK;
 }
 #endif
+
+int yk_net_set_precision(yk_net_t* net, int mode) {
+    if (!net || (mode != YK_PREDICT_F32 && mode != YK_PREDICT_F16)) return YK_ERR_ARG;
+    net->dev.planes = mode == YK_PREDICT_F16 ? 1 : 2;
+    return YK_OK;
+}
 
 int yk_net_destroy(yk_net_t* net) {
     if (!net) return YK_OK;

@@ -19,6 +19,7 @@
 
 #include "yk_api.h"
 #include "yk_common.h"
+#include "yk_train_amp.h"
 
 using namespace yk;
 
@@ -43,6 +44,8 @@ __device__ __forceinline__ float wmax(float v) {
     return v;
 }
 // dropout keep-mask from the Philox stream: element `idx` of layer `layer` at optimiser step `step`
+// (idx = global row * H + column: the row counts from the step's row offset, so the ranks of a
+// split minibatch draw the masks one process drawing the whole minibatch would)
 __device__ __forceinline__ bool keep(uint64_t seed, int layer, uint64_t step, long idx, float p) {
     if (p <= 0.0f) return true;
     const uint64_t d = philox_draw(seed, 0x44524F50u + (uint32_t)layer, (step << 32) ^ (uint64_t)idx);
@@ -86,7 +89,7 @@ __device__ __forceinline__ void ln_row_bwd(const float (&xh)[VPL], float (&dy)[V
 // inp: Z0 += b; A = LN(Z0) (affine); H0 = dropout(silu(A)).  Saves Z0 (+bias), mu, rs, mask.
 template <int VPL>
 __global__ void k_inp_fwd(float* Z, const float* b, const float* g, const float* be, float* mu_o, float* rs_o,
-                          uint8_t* mask, float* Hout, int B, float p, uint64_t seed, uint64_t step) {
+                          uint8_t* mask, float* Hout, int B, float p, uint64_t seed, uint64_t step, int64_t row_base) {
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (row >= B) return;
     constexpr int H = VPL * 64;
@@ -108,7 +111,7 @@ __global__ void k_inp_fwd(float* Z, const float* b, const float* g, const float*
     for (int i = 0; i < VPL; i++) {
         const long idx = (long)row * H + c0 + i;
         const float a = x[i] * g[c0 + i] + be[c0 + i];
-        const bool k = keep(seed, 0, step, idx, p);
+        const bool k = keep(seed, 0, step, (row_base + row) * H + c0 + i, p);
         mask[idx] = k;
         Hout[idx] = k ? silu_f(a) * (p > 0.f ? sc : 1.0f) : 0.0f;
     }
@@ -118,7 +121,7 @@ __global__ void k_inp_fwd(float* Z, const float* b, const float* g, const float*
 template <int VPL>
 __global__ void k_blk_fwd(float* U, const float* b, const float* g, const float* be, float* mu_o, float* rs_o,
                           uint8_t* mask, float* out, const float* Hin, int B, float p, uint64_t seed, uint64_t step,
-                          int layer) {
+                          int layer, int64_t row_base) {
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (row >= B) return;
     constexpr int H = VPL * 64;
@@ -144,7 +147,7 @@ __global__ void k_blk_fwd(float* U, const float* b, const float* g, const float*
         if (Hin) {
             out[idx] = Hin[idx] + l;  // residual
         } else {
-            const bool k = keep(seed, layer, step, idx, p);
+            const bool k = keep(seed, layer, step, (row_base + row) * H + c0 + i, p);
             mask[idx] = k;
             out[idx] = k ? l * (p > 0.f ? sc : 1.0f) : 0.0f;
         }
@@ -481,6 +484,8 @@ struct yk_trainer {
     float2* lrow = nullptr;    // per-row (ce, squared value error) of the last batch
     float* lsum = nullptr;     // their column sums (k_colsums)
     double host_loss[3] = {0, 0, 0};
+    int64_t row_base = 0;        // global row of the next backward's first example (dropout)
+    yk::AmpTrain* amp = nullptr;  // mixed-precision mode (yk_train_amp.hip)
 };
 
 namespace {
@@ -528,16 +533,18 @@ int step_impl(yk_trainer* t, const yk_state_t* states, const int32_t* targets, c
     // ---- forward
     if ((rc = gemm_rm(t, false, true, B, H, FEAT, t->X, FEAT, Pt(T_WIN), FEAT, t->Z0, H, 0.f))) return rc;
     hipLaunchKernelGGL(k_inp_fwd<VPL>, rows, wave4, 0, s, t->Z0, Pt(T_BIN), Pt(T_GIN), Pt(T_BEIN), t->mu0, t->rs0,
-                       t->mask0, t->Hs[0], B, p, seed, step);
+                       t->mask0, t->Hs[0], B, p, seed, step, t->row_base);
     YK_LAUNCHED();
     for (int b = 0; b < NB; b++) {
         if ((rc = gemm_rm(t, false, true, B, H, H, t->Hs[b], H, Pt(t_blk(b, 0)), H, t->U1[b], H, 0.f))) return rc;
         hipLaunchKernelGGL(k_blk_fwd<VPL>, rows, wave4, 0, s, t->U1[b], Pt(t_blk(b, 1)), Pt(t_blk(b, 2)), Pt(t_blk(b, 3)),
-                           t->mu1[b], t->rs1[b], t->mask1[b], t->R1[b], (const float*)nullptr, B, p, seed, step, 1 + b);
+                           t->mu1[b], t->rs1[b], t->mask1[b], t->R1[b], (const float*)nullptr, B, p, seed, step, 1 + b,
+                           t->row_base);
         YK_LAUNCHED();
         if ((rc = gemm_rm(t, false, true, B, H, H, t->R1[b], H, Pt(t_blk(b, 4)), H, t->U2[b], H, 0.f))) return rc;
         hipLaunchKernelGGL(k_blk_fwd<VPL>, rows, wave4, 0, s, t->U2[b], Pt(t_blk(b, 5)), Pt(t_blk(b, 6)), Pt(t_blk(b, 7)),
-                           t->mu2[b], t->rs2[b], (uint8_t*)nullptr, t->Hs[b + 1], t->Hs[b], B, p, seed, step, -1);
+                           t->mu2[b], t->rs2[b], (uint8_t*)nullptr, t->Hs[b + 1], t->Hs[b], B, p, seed, step, -1,
+                           t->row_base);
         YK_LAUNCHED();
     }
     const float* Hh = t->Hs[NB];
@@ -700,7 +707,7 @@ int yk_trainer_create(yk_trainer_t** out, int H, int NB, const float* const* par
         (void)hipMemcpy(t->tiles, tiles.data(), sizeof(int2) * tiles.size(), hipMemcpyHostToDevice);
     }
 #undef TA
-    if (rc == YK_OK && rocblas_create_handle(&t->blas) != rocblas_status_success) rc = YK_ERR_HIP;
+    if (rc == YK_OK && !cfg->amp && rocblas_create_handle(&t->blas) != rocblas_status_success) rc = YK_ERR_HIP;
     if (rc != YK_OK) {
         yk_trainer_destroy(t);
         return rc;
@@ -715,6 +722,14 @@ int yk_trainer_create(yk_trainer_t** out, int H, int NB, const float* const* par
     (void)hipMemset(t->G, 0, sizeof(float) * o);
     (void)hipMemset(t->acc, 0, sizeof(double) * 3);
     (void)hipMemset(t->lsum, 0, sizeof(float) * 2);
+    if (cfg->amp) {
+        if ((rc = yk::amp_create(&t->amp, H, NB, t->Bmax, t->P, t->G, t->off.data(), cfg->init_scale,
+                                 cfg->growth_interval)) != YK_OK ||
+            (rc = yk::amp_pack(t->amp, 0)) != YK_OK) {
+            yk_trainer_destroy(t);
+            return rc;
+        }
+    }
     if (hipDeviceSynchronize() != hipSuccess) {
         yk_trainer_destroy(t);
         return YK_ERR_HIP;
@@ -726,6 +741,7 @@ int yk_trainer_create(yk_trainer_t** out, int H, int NB, const float* const* par
 int yk_trainer_destroy(yk_trainer_t* t) {
     if (!t) return YK_OK;
     if (t->blas) rocblas_destroy_handle(t->blas);
+    yk::amp_destroy(t->amp);
     for (void* p : t->allocs) (void)hipFree(p);
     delete t;
     return YK_OK;
@@ -744,6 +760,9 @@ int yk_trainer_backward(yk_trainer_t* t, const yk_state_t* states, const int32_t
     if (!t || !states || !targets || !values) return YK_ERR_ARG;
     if (batch <= 0 || batch > t->Bmax) return YK_ERR_ARG;
     hipStream_t s = as_stream(stream);
+    if (t->amp)
+        return yk::amp_backward(t->amp, states, targets, values, batch_idx, batch, t->cfg.dropout, t->cfg.seed, t->step,
+                                t->row_base, t->cfg.vloss_weight, t->lrow, t->lsum, s);
     if (rocblas_set_stream(t->blas, s) != rocblas_status_success) return YK_ERR_HIP;
     switch (t->H) {
         case 64: return step_impl<1>(t, states, targets, values, batch_idx, batch, s);
@@ -757,7 +776,10 @@ int yk_trainer_backward(yk_trainer_t* t, const yk_state_t* states, const int32_t
 int yk_trainer_apply(yk_trainer_t* t, void* stream) {
     if (!t) return YK_ERR_ARG;
     hipStream_t s = as_stream(stream);
-    t->step += 1;
+    t->step += 1;  // (amp: the dropout stream's step; the optimiser's count of steps taken is on the device)
+    if (t->amp)
+        return yk::amp_apply(t->amp, t->nparams, t->M, t->V, t->acc + 2, t->cfg.max_grad_norm, t->cfg.lr,
+                             t->cfg.weight_decay, t->cfg.beta1, t->cfg.beta2, t->cfg.eps, s);
     const double b1 = t->cfg.beta1, b2 = t->cfg.beta2, st = (double)t->step;
     const double bc1 = 1.0 - std::pow(b1, st), bc2 = 1.0 - std::pow(b2, st);
     const float step_size = (float)(t->cfg.lr / bc1), bc2_sqrt = (float)std::sqrt(bc2);
@@ -803,10 +825,34 @@ int yk_trainer_set(yk_trainer_t* t, int which, const float* const* in, int64_t s
     for (size_t k = 0; k < t->off.size(); k++)
         if (in[k]) YK_HIP(hipMemcpy(dst + t->off[k], in[k], sizeof(float) * t->len[k], hipMemcpyHostToDevice));
     if (step >= 0) t->step = (uint64_t)step;
+    if (t->amp) {
+        if (step >= 0) {
+            const int rc = yk::amp_set_steps(t->amp, step);
+            if (rc) return rc;
+        }
+        if (which == 0) {  // new parameters: new fp16 copies
+            const int rc = yk::amp_pack(t->amp, 0);
+            if (rc) return rc;
+        }
+    }
     YK_HIP(hipDeviceSynchronize());
     return YK_OK;
 }
 
-int64_t yk_trainer_step_count(yk_trainer_t* t) { return t ? (int64_t)t->step : YK_ERR_ARG; }
+int64_t yk_trainer_step_count(yk_trainer_t* t) {
+    if (!t) return YK_ERR_ARG;
+    return t->amp ? yk::amp_steps(t->amp) : (int64_t)t->step;
+}
+
+int yk_trainer_set_row_offset(yk_trainer_t* t, int64_t row0) {
+    if (!t || row0 < 0) return YK_ERR_ARG;
+    t->row_base = row0;
+    return YK_OK;
+}
+
+int yk_trainer_amp_state(yk_trainer_t* t, double* out) {
+    if (!t || !out || !t->amp) return YK_ERR_ARG;
+    return yk::amp_state(t->amp, out);
+}
 
 }  // extern "C"

@@ -1,0 +1,1438 @@
+// yk_train_amp.hip - NNetWrapper.train's mixed-precision step on MI355X: the reference trains on
+// the GPU under autocast('cuda') with a GradScaler (yacht/NNet.py:113-116, 141-155): fp16 Linear
+// layers (fp16 inputs, weights and outputs, f32 accumulation), LayerNorm / cross-entropy / MSE
+// in f32, the loss scaled before backward, the gradients unscaled, clip_grad_norm_(5.0), AdamW,
+// and the step skipped (scale halved) when a gradient overflows.  This file restates that
+// arithmetic - the fp16 rounding points included - on hand-written v_mfma_f32_16x16x32_f16
+// kernels instead of library GEMMs (yk_train.hip keeps the f32 rocBLAS step for the f32 mode).
+//
+// A step is ten launches (yk_train_amp.h):
+//   k_amp_fwd      one 512-thread workgroup per 16-row tile: features -> input layer -> the
+//                  residual blocks -> the heads' LayerNorms, every dense layer from a register
+//                  ring of fp16 weight fragments that streams the next layer during the row pass;
+//                  saves what the backward needs (fp16 pre-activations, LayerNorm statistics, the
+//                  GEMM inputs in the T layout the weight-gradient GEMMs read)
+//   k_amp_head     row tile x column part: the policy logits (fp16-rounded) and their per-part
+//                  softmax statistics; one more part per tile computes v_head.2
+//   k_amp_loss     one wave per example: cross-entropy, the value head's tail, the MSE and their
+//                  scaled gradients
+//   k_amp_headbwd  row tile x action slice: the scaled fp16 logits gradient, its T layout, and a
+//                  split-K slice of pi_head.2's input gradient
+//   k_amp_bwd      one workgroup per row tile: the heads' LayerNorm backward and the trunk's
+//                  backward chain (LayerNorm / SiLU / dropout backward, the dX GEMMs) to the input
+//   k_amp_dw       every weight gradient (13 + 2 GEMMs, K = the batch) in one grouped launch
+//   k_amp_vecsum   bias / LayerNorm gradients and the loss sums: fixed-order column sums
+//   k_amp_sq, k_amp_adamw, k_amp_pack  unscale + norm, clip + AdamW (or skip), GradScaler
+//                  update and the fp16 weight copies for the next step
+// Weight fragments use yk_net.h's packing (one plane): for W[N][K], the 1 KB piece (nt, ks) holds
+// W[16 nt + (l & 15)][32 ks + 8 (l >> 4) + j] for lane l, j < 8.  The T layout of an activation
+// matrix X[rows][C] is the same packing of X^T (piece (ct, rs): X[32 rs + 8 (l >> 4) + j][16 ct +
+// (l & 15)]), so dW = dU^T X is an MFMA over 32-row slices with both operands read whole.
+#include <cmath>
+#include <vector>
+
+#include "yk_api.h"
+#include "yk_common.h"
+#include "yk_train_amp.h"
+
+using namespace yk;
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+
+namespace {
+
+constexpr int TR = 16;          // rows per tile (the MFMA M)
+constexpr int TW = 8;           // waves per trunk workgroup
+constexpr int TTHR = 64 * TW;
+constexpr int TRPW = TR / TW;   // rows per wave in the row passes
+constexpr int LDL = 3264;       // logits row stride: 204 tiles of 16 columns
+constexpr int PT = LDL / 16;    // policy column tiles
+constexpr int PKS = LDL / 32;   // 32-deep action slices
+constexpr int HQ = 8;           // policy-head column parts per row tile (+1 part: v_head.2)
+constexpr int BQ = 6;           // head-backward action parts per row tile
+constexpr int VH = 128;         // v_head hidden width
+constexpr int SQ_BLOCKS = 1024;
+
+struct Scaler {  // GradScaler('cuda') state + the AdamW step count (device)
+    float scale;
+    int tracker;
+    int64_t steps;
+    int found_inf;
+    int growth_interval;
+};
+
+// Everything the kernels address: parameters (f32, state_dict order), fp16 weight fragments
+// (float4 = 8 halves), saved activations, gradients.
+struct AmpDev {
+    int H, NB, Bmax, RS, TMAX, NVEC;
+    const float* P;
+    float* G;
+    const long* off;                      // tensor offsets (device)
+    const float4 *win_f, *w1f, *w2f, *w1t, *w2t, *wpif, *wpit, *wv1f, *wv1t;
+    _Float16 *xT, *hT, *r1T, *apiT, *avT, *api_rm, *av_rm;
+    float *z0, *u1, *u2, *hF, *stats;
+    float *logits, *zv1, *lse;
+    float2* mlq;
+    _Float16 *dz1_rm, *dz1T, *dlT, *dz0T, *du1T, *du2T;
+    float *dz1f, *v2prod, *dzv2, *dpart, *dbpi_part, *colpart;
+    Scaler* sc;
+};
+// tensor indices in state_dict order (YachtNNet.py:30-52)
+enum { T_WIN = 0, T_BIN, T_GIN, T_BEIN };
+__host__ __device__ inline int t_blk(int b, int k) { return 4 + 8 * b + k; }
+__host__ __device__ inline int t_head(int NB, int k) { return 4 + 8 * NB + k; }
+// offset of tensor k in the flat buffer (closed form of the state_dict sizes: no memory load,
+// so nothing the kernels read waits behind the weight ring in the in-order vmcnt queue)
+__host__ __device__ inline long poff(int H, int NB, int k) {
+    const long h = H, hh = h * h;
+    if (k < 4) return k == 0 ? 0 : FEAT * h + (k - 1) * h;
+    const long base = (FEAT + 3) * h;
+    if (k < 4 + 8 * NB) {
+        const int b = (k - 4) / 8, s = (k - 4) % 8;
+        const long o = base + b * (2 * hh + 6 * h);
+        const long so[8] = {0, hh, hh + h, hh + 2 * h, hh + 3 * h, 2 * hh + 3 * h, 2 * hh + 4 * h, 2 * hh + 5 * h};
+        return o + so[s];
+    }
+    const int s = k - 4 - 8 * NB;
+    const long o = base + NB * (2 * hh + 6 * h), A = ASIZE;
+    const long so[10] = {0, h, 2 * h, 2 * h + A * h, 2 * h + A * h + A, 3 * h + A * h + A, 4 * h + A * h + A,
+                         4 * h + A * h + A + 128 * h, 4 * h + A * h + A + 129 * h, 4 * h + A * h + A + 130 * h};
+    return o + so[s];
+}
+enum { HP_G = 0, HP_B = 1, HP_W = 2, HP_BIAS = 3, HV_G = 4, HV_B = 5, HV_W1 = 6, HV_B1 = 7, HV_W2 = 8, HV_B2 = 9 };
+// column-partial vectors of k_amp_bwd (colpart[tile][v][H])
+enum { CV_BIN = 0, CV_GIN, CV_BEIN, CV_GPI, CV_BEPI, CV_GV, CV_BEV, CV_BLK };  // + 6 b + {b1 g1 be1 b2 g2 be2}
+
+__device__ __forceinline__ float r16(float x) { return (float)(_Float16)x; }  // an fp16 tensor's value
+__device__ __forceinline__ floatx4 mfma(float4 a, float4 b, floatx4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, a), __builtin_bit_cast(half8, b), c, 0, 0, 0);
+}
+__device__ __forceinline__ floatx4 zero4() { return floatx4{0.f, 0.f, 0.f, 0.f}; }
+__device__ __forceinline__ float wsum(float v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
+__device__ __forceinline__ float silu(float x) { return x * sigm(x); }
+__device__ __forceinline__ float silu_grad(float x) {
+    const float s = sigm(x);
+    return s * (1.0f + x * (1.0f - s));
+}
+// the f32 trainer's dropout mask (yk_train.hip keep): element idx of layer `layer` at step `step`
+__device__ __forceinline__ bool keep(uint64_t seed, int layer, uint64_t step, long idx, float p) {
+    if (p <= 0.0f) return true;
+    const uint64_t d = philox_draw(seed, 0x44524F50u + (uint32_t)layer, (step << 32) ^ (uint64_t)idx);
+    return (float)(d >> 40) * (1.0f / 16777216.0f) >= p;
+}
+// workgroup barrier that does not drain the weight ring's outstanding loads (vmcnt)
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+__device__ __forceinline__ void stat_merge(float& m, float& s, float m2, float s2) {
+    const float mm = fmaxf(m, m2);
+    if (mm == -INFINITY) return;
+    s = s * __expf(m - mm) + s2 * __expf(m2 - mm);
+    m = mm;
+}
+
+// The tile's 16 rows of an fp16 plane (LDS, row stride sa halves; columns col0 .. col0 + C) into
+// the T layout at column tile offset ct0; the last tile of an odd tile count also zeroes the
+// slice's other half (rows past the batch must not enter a weight gradient).
+__device__ __forceinline__ void write_tl(const _Float16* A, int sa, int col0, int C, _Float16* dst, int RS, int ct0,
+                                         int tile, bool zero_half) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int h = tile & 1, rs = tile >> 1, q = lane >> 4;
+    const bool mine = (q >> 1) == h;
+    for (int ct = wave; ct < C / 16; ct += nw) {
+        half8 v = {};
+        if (mine) {
+#pragma unroll
+            for (int j = 0; j < 8; j++) v[j] = A[(8 * (q - 2 * h) + j) * sa + col0 + 16 * ct + (lane & 15)];
+        }
+        if (mine || zero_half)
+            *reinterpret_cast<half8*>(dst + (((long)(ct0 + ct) * RS + rs) * 64 + lane) * 8) = v;
+    }
+}
+
+// acc[t] = A[16 x K] (fp16 plane in LDS) x W^T over this wave's NT column tiles, weights from the
+// register ring (slice ks in slot ks % RW); a consumed slot is refilled with slice ks + RW of
+// this matrix (cur) or, past its end, of the next one (nxt, same shape; none if null).
+template <int KS, int NT, int RW>
+__device__ __forceinline__ void gemm_ring(const _Float16* A, int sa, float4 (&ring)[RW][NT], floatx4 (&acc)[NT],
+                                          const float4* __restrict__ cur, const float4* __restrict__ nxt, int nt0) {
+    static_assert(KS % RW == 0, "ring slots align with layers");
+    const int lane = threadIdx.x & 63;
+    const _Float16* ap = A + (lane & 15) * sa + 8 * (lane >> 4);
+#pragma unroll
+    for (int t = 0; t < NT; t++) acc[t] = zero4();
+    float4 a = *reinterpret_cast<const float4*>(ap);
+#pragma unroll
+    for (int ks = 0; ks < KS; ks++) {
+        const float4 an = *reinterpret_cast<const float4*>(ap + 32 * ((ks + 1) % KS));
+        float4(&w)[NT] = ring[ks % RW];
+#pragma unroll
+        for (int t = 0; t < NT; t++) acc[t] = mfma(a, w[t], acc[t]);
+        const int g = ks + RW;
+        if (g < KS) {
+#pragma unroll
+            for (int t = 0; t < NT; t++) w[t] = cur[((long)(nt0 + t) * KS + g) * 64 + lane];
+        } else if (nxt) {
+#pragma unroll
+            for (int t = 0; t < NT; t++) w[t] = nxt[((long)(nt0 + t) * KS + g - KS) * 64 + lane];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        a = an;
+    }
+}
+template <int KS, int NT, int RW>
+__device__ __forceinline__ void ring_fill(float4 (&ring)[RW][NT], const float4* __restrict__ W, int nt0) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int s = 0; s < RW; s++)
+#pragma unroll
+        for (int t = 0; t < NT; t++) ring[s][t] = W[((long)(nt0 + t) * KS + s) * 64 + lane];
+}
+// accumulator tile t -> T[row][col] (+ bias16, fp16-rounded when `round`); lane holds rows
+// 4 (l >> 4) + j of column 16 (nt0 + t) + (l & 15)
+template <int NT>
+__device__ __forceinline__ void store_acc(float* T, int ld, int nt0, const floatx4 (&acc)[NT]) {
+    const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
+#pragma unroll
+    for (int t = 0; t < NT; t++)
+#pragma unroll
+        for (int j = 0; j < 4; j++) T[(4 * q + j) * ld + 16 * (nt0 + t) + r] = acc[t][j];
+}
+// LayerNorm statistics (biased variance, eps 1e-5) of a row held VPL per lane
+template <int VPL>
+__device__ __forceinline__ void ln_stats(const float (&x)[VPL], int H, float& mu, float& rs) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPL; i++) s += x[i];
+    mu = wsum(s) / (float)H;
+    float v = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPL; i++) {
+        const float d = x[i] - mu;
+        v += d * d;
+    }
+    rs = 1.0f / sqrtf(wsum(v) / (float)H + 1e-5f);
+}
+// LayerNorm input gradient from dL/dxhat (dx, in place): rs / H (H dx - sum dx - xhat sum(dx xhat))
+template <int VPL>
+__device__ __forceinline__ void ln_bwd(const float (&xh)[VPL], float (&dx)[VPL], int H, float rs) {
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPL; i++) {
+        a += dx[i];
+        b += dx[i] * xh[i];
+    }
+    a = wsum(a);
+    b = wsum(b);
+#pragma unroll
+    for (int i = 0; i < VPL; i++) dx[i] = rs / (float)H * ((float)H * dx[i] - a - xh[i] * b);
+}
+__device__ __forceinline__ float* stat_ptr(const AmpDev& d, int layer, int which) {
+    return d.stats + ((long)layer * 2 + which) * d.Bmax;
+}
+// per-wave column partials of up to 3 vectors (LDS CP[TW][3][H]) summed over the waves in wave
+// order into colpart[tile][v0 + k][H]
+template <int H>
+__device__ __forceinline__ void colpart_flush(const AmpDev& d, const float* CP, int tile, int v0, int nv) {
+    for (int i = threadIdx.x; i < nv * H; i += TTHR) {
+        float s = 0.f;
+#pragma unroll
+        for (int w = 0; w < TW; w++) s += CP[w * 3 * H + i];
+        d.colpart[((long)tile * d.NVEC + v0) * H + i] = s;
+    }
+}
+
+// ------------------------------------------------------------------ forward (trunk)
+template <int H>
+__global__ __launch_bounds__(TTHR) void k_amp_fwd(AmpDev d, const yk_state_t* __restrict__ states,
+                                                  const int32_t* __restrict__ idx, int B, float p, uint64_t seed,
+                                                  uint64_t step, int64_t row_base) {
+    constexpr int LD = H + 4, SA = H + 8, VPL = H / 64, KS = H / 32;
+    constexpr int NT = H >= 128 ? H / 128 : 1, NACT = H / (16 * NT);
+    constexpr int RW = KS * NT <= 16 ? KS : 16 / NT;
+    __shared__ __attribute__((aligned(16))) float Xs[TR * LD];
+    __shared__ __attribute__((aligned(16))) float Ts[TR * LD];
+    __shared__ __attribute__((aligned(16))) _Float16 Pa[TR * SA];
+    __shared__ __attribute__((aligned(16))) float VL[3 * H];
+    const int tile = blockIdx.x, row0 = tile * TR;
+    const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    const bool gw = wave < NACT;
+    const int nt0 = wave * NT, c0 = lane * VPL;
+    const bool zero_half = row0 + TR >= B && (tile & 1) == 0;
+    const float sc = p > 0.f ? 1.0f / (1.0f - p) : 1.0f;
+    const int NB = d.NB;
+    const long HH8 = (long)H * H / 8;  // float4 per packed H x H matrix
+
+    // the input layer's vectors, its weights (K = 64: 2 slices), the first block's ring, then features
+    for (int i = tid; i < 3 * H; i += TTHR) VL[i] = d.P[poff(H, d.NB, T_BIN + i / H) + i % H];
+    float4 w0[2][NT];
+    if (gw) {
+#pragma unroll
+        for (int s = 0; s < 2; s++)
+#pragma unroll
+            for (int t = 0; t < NT; t++) w0[s][t] = d.win_f[((long)(nt0 + t) * 2 + s) * 64 + lane];
+    }
+    float4 ring[RW][NT];
+    if (gw && NB > 0) ring_fill<KS, NT, RW>(ring, d.w1f, nt0);
+#pragma unroll
+    for (int k = 0; k < 2; k++) {  // state_to_vec (NNet.py:65-86), K padded to 64
+        const int r = wave + TW * k, row = row0 + r;
+        float x = 0.f;
+        if (row < B) {
+            const int src = __builtin_amdgcn_readfirstlane(idx ? idx[row] : row);
+            YkS s;
+            const uint64_t* q = reinterpret_cast<const uint64_t*>(states + src);
+#pragma unroll
+            for (int w = 0; w < 8; w++) s.w[w] = q[w];
+            if (lane < FEAT) x = feature(s, lane);
+        }
+        Pa[r * SA + lane] = (_Float16)x;
+    }
+    lds_barrier();
+    write_tl(Pa, SA, 0, 64, d.xT, d.RS, 0, tile, zero_half);
+    floatx4 acc[NT];
+    if (gw) {  // inp.0: Z0 = fp16(x16 W_in^T + b16)
+        const _Float16* ap = Pa + (lane & 15) * SA + 8 * (lane >> 4);
+#pragma unroll
+        for (int t = 0; t < NT; t++) acc[t] = zero4();
+#pragma unroll
+        for (int s = 0; s < 2; s++) {
+            const float4 a = *reinterpret_cast<const float4*>(ap + 32 * s);
+#pragma unroll
+            for (int t = 0; t < NT; t++) acc[t] = mfma(a, w0[s][t], acc[t]);
+        }
+        store_acc<NT>(Ts, LD, nt0, acc);
+    }
+    lds_barrier();
+    // inp.1-3: LayerNorm (f32) -> SiLU -> Dropout  YachtNNet.py:30-35
+#pragma unroll
+    for (int rr = 0; rr < TRPW; rr++) {
+        const int r = wave * TRPW + rr, row = row0 + r;
+        float x[VPL];
+        if (row < B) {
+#pragma unroll
+            for (int i = 0; i < VPL; i++) {
+                x[i] = r16(Ts[r * LD + c0 + i] + r16(VL[c0 + i]));
+                d.z0[(long)row * H + c0 + i] = x[i];
+            }
+            float mu, rs;
+            ln_stats<VPL>(x, H, mu, rs);
+            if (lane == 0) {
+                stat_ptr(d, 0, 0)[row] = mu;
+                stat_ptr(d, 0, 1)[row] = rs;
+            }
+#pragma unroll
+            for (int i = 0; i < VPL; i++) {
+                const float a = (x[i] - mu) * rs * VL[H + c0 + i] + VL[2 * H + c0 + i];
+                const bool k = keep(seed, 0, step, (row_base + row) * H + c0 + i, p);
+                x[i] = k ? silu(a) * sc : 0.f;
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < VPL; i++) x[i] = 0.f;
+        }
+#pragma unroll
+        for (int i = 0; i < VPL; i++) {
+            Xs[r * LD + c0 + i] = x[i];
+            Pa[r * SA + c0 + i] = (_Float16)x[i];
+        }
+    }
+    lds_barrier();
+    if (NB > 0) write_tl(Pa, SA, 0, H, d.hT, d.RS, 0, tile, zero_half);
+
+    // ResidualBlock x NB: h = LN1(SiLU(fc1 x)); h = Dropout(h); h = LN2(SiLU(fc2 h)); x + h  YachtNNet.py:8-21
+    for (int b = 0; b < NB; b++) {
+        for (int half = 0; half < 2; half++) {
+            const int kb = half == 0 ? 1 : 5;  // fc1.bias / fc2.bias
+            float vr[(3 * H + TTHR - 1) / TTHR];  // this layer's bias, gamma, beta (issued before the
+#pragma unroll                               // ring's refills, so the LDS copy never waits behind them)
+            for (int k = 0; k < (3 * H + TTHR - 1) / TTHR; k++) {
+                const int i = tid + TTHR * k;
+                if (i < 3 * H) vr[k] = d.P[poff(H, d.NB, t_blk(b, kb + i / H)) + i % H];
+            }
+            const float4* cur = (half == 0 ? d.w1f : d.w2f) + b * HH8;
+            const float4* nxt = half == 0 ? d.w2f + b * HH8 : (b + 1 < NB ? d.w1f + (b + 1) * HH8 : nullptr);
+            if (gw) {
+                gemm_ring<KS, NT, RW>(Pa, SA, ring, acc, cur, nxt, nt0);
+                store_acc<NT>(Ts, LD, nt0, acc);
+            }
+#pragma unroll
+            for (int k = 0; k < (3 * H + TTHR - 1) / TTHR; k++) {
+                const int i = tid + TTHR * k;
+                if (i < 3 * H) VL[i] = vr[k];
+            }
+            lds_barrier();
+            float* U = (half == 0 ? d.u1 : d.u2) + (long)b * d.Bmax * H;
+            const int L = 1 + 2 * b + half;
+#pragma unroll
+            for (int rr = 0; rr < TRPW; rr++) {
+                const int r = wave * TRPW + rr, row = row0 + r;
+                float x[VPL];
+                if (row < B) {
+                    float s[VPL];
+#pragma unroll
+                    for (int i = 0; i < VPL; i++) {
+                        const float u = r16(Ts[r * LD + c0 + i] + r16(VL[c0 + i]));  // fc out (fp16)
+                        U[(long)row * H + c0 + i] = u;
+                        s[i] = r16(silu(u));                                          // SiLU on fp16
+                    }
+                    float mu, rs;
+                    ln_stats<VPL>(s, H, mu, rs);
+                    if (lane == 0) {
+                        stat_ptr(d, L, 0)[row] = mu;
+                        stat_ptr(d, L, 1)[row] = rs;
+                    }
+#pragma unroll
+                    for (int i = 0; i < VPL; i++) {
+                        const float l = (s[i] - mu) * rs * VL[H + c0 + i] + VL[2 * H + c0 + i];
+                        if (half == 0) {
+                            const bool k = keep(seed, 1 + b, step, (row_base + row) * H + c0 + i, p);
+                            x[i] = k ? l * sc : 0.f;
+                        } else {
+                            x[i] = Xs[r * LD + c0 + i] + l;  // residual (f32)
+                        }
+                    }
+                } else {
+#pragma unroll
+                    for (int i = 0; i < VPL; i++) x[i] = 0.f;
+                }
+#pragma unroll
+                for (int i = 0; i < VPL; i++) {
+                    if (half == 1) Xs[r * LD + c0 + i] = x[i];
+                    Pa[r * SA + c0 + i] = (_Float16)x[i];
+                }
+            }
+            lds_barrier();
+            if (half == 0) write_tl(Pa, SA, 0, H, d.r1T + (long)b * (H / 16) * d.RS * 512, d.RS, 0, tile, zero_half);
+            else if (b + 1 < NB)
+                write_tl(Pa, SA, 0, H, d.hT + (long)(b + 1) * (H / 16) * d.RS * 512, d.RS, 0, tile, zero_half);
+        }
+    }
+
+    // the heads' LayerNorms (one set of statistics, two affine maps) -> SiLU: a_pi, a_v (f32),
+    // cast to fp16 for pi_head.2 / v_head.2  YachtNNet.py:40-52
+    _Float16* Pv = reinterpret_cast<_Float16*>(Ts);
+    const float* gp = d.P + poff(H, d.NB, t_head(NB, HP_G));
+    const float* bp = d.P + poff(H, d.NB, t_head(NB, HP_B));
+    const float* gv = d.P + poff(H, d.NB, t_head(NB, HV_G));
+    const float* bv = d.P + poff(H, d.NB, t_head(NB, HV_B));
+    lds_barrier();  // every wave is done reading Ts
+#pragma unroll
+    for (int rr = 0; rr < TRPW; rr++) {
+        const int r = wave * TRPW + rr, row = row0 + r;
+        float x[VPL];
+#pragma unroll
+        for (int i = 0; i < VPL; i++) x[i] = Xs[r * LD + c0 + i];
+        if (row < B) {
+            float mu, rs;
+            ln_stats<VPL>(x, H, mu, rs);
+            if (lane == 0) {
+                stat_ptr(d, 1 + 2 * NB, 0)[row] = mu;
+                stat_ptr(d, 1 + 2 * NB, 1)[row] = rs;
+            }
+#pragma unroll
+            for (int i = 0; i < VPL; i++) {
+                d.hF[(long)row * H + c0 + i] = x[i];
+                const float xh = (x[i] - mu) * rs;
+                Pa[r * SA + c0 + i] = (_Float16)silu(xh * gp[c0 + i] + bp[c0 + i]);
+                Pv[r * SA + c0 + i] = (_Float16)silu(xh * gv[c0 + i] + bv[c0 + i]);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < VPL; i++) {
+                Pa[r * SA + c0 + i] = (_Float16)0.f;
+                Pv[r * SA + c0 + i] = (_Float16)0.f;
+            }
+        }
+    }
+    lds_barrier();
+    write_tl(Pa, SA, 0, H, d.apiT, d.RS, 0, tile, zero_half);
+    write_tl(Pv, SA, 0, H, d.avT, d.RS, 0, tile, zero_half);
+    for (int i = tid; i < TR * H / 8; i += TTHR) {  // row-major copies: the head kernel's A operands
+        const int r = i / (H / 8), c8 = i % (H / 8), row = row0 + r;
+        if (row < B) {
+            reinterpret_cast<float4*>(d.api_rm + (long)row * H)[c8] = *reinterpret_cast<const float4*>(Pa + r * SA + 8 * c8);
+            reinterpret_cast<float4*>(d.av_rm + (long)row * H)[c8] = *reinterpret_cast<const float4*>(Pv + r * SA + 8 * c8);
+        }
+    }
+}
+
+// ------------------------------------------------------------------ heads
+// policy logits = fp16(a_pi16 Wpi16^T + bpi16) over this part's column tiles, and per row the
+// part's (max, sum exp); part HQ: v_head.2 z1 = fp16(a_v16 Wv1^T + bv1_16)
+template <int H>
+__global__ __launch_bounds__(TTHR) void k_amp_head(AmpDev d, int B) {
+    constexpr int SA = H + 8, KS = H / 32;
+    __shared__ __attribute__((aligned(16))) _Float16 A[TR * SA];
+    __shared__ float2 red[TW][TR];
+    const int tile = blockIdx.x, part = blockIdx.y, row0 = tile * TR;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, q = lane >> 4;
+    const bool vpart = part == HQ;
+    const _Float16* src = vpart ? d.av_rm : d.api_rm;
+    for (int i = tid; i < TR * H / 8; i += TTHR) {
+        const int r = i / (H / 8), c8 = i % (H / 8);
+        const float4 v = row0 + r < B ? reinterpret_cast<const float4*>(src + (long)(row0 + r) * H)[c8]
+                                      : make_float4(0.f, 0.f, 0.f, 0.f);
+        *reinterpret_cast<float4*>(A + r * SA + 8 * c8) = v;
+    }
+    __syncthreads();
+    const _Float16* ap = A + (lane & 15) * SA + 8 * (lane >> 4);
+    if (vpart) {  // 8 tiles of 16 columns, one per wave
+        const int nt = wave;
+        floatx4 acc = zero4();
+#pragma unroll
+        for (int ks = 0; ks < KS; ks++)
+            acc = mfma(*reinterpret_cast<const float4*>(ap + 32 * ks), d.wv1f[((long)nt * KS + ks) * 64 + lane], acc);
+        const int col = 16 * nt + (lane & 15);
+        const float bias = r16(d.P[poff(H, d.NB, t_head(d.NB, HV_B1)) + col]);
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int row = row0 + 4 * q + j;
+            if (row < B) d.zv1[(long)row * VH + col] = r16(acc[j] + bias);
+        }
+        return;
+    }
+    const int t0 = part * PT / HQ, t1 = (part + 1) * PT / HQ;
+    const float* bpi = d.P + poff(H, d.NB, t_head(d.NB, HP_BIAS));
+    float m[4], s[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        m[j] = -INFINITY;
+        s[j] = 0.f;
+    }
+    float4 w[2][KS];
+    int nt = t0 + wave;
+    if (nt < t1) {
+#pragma unroll
+        for (int ks = 0; ks < KS; ks++) w[0][ks] = d.wpif[((long)nt * KS + ks) * 64 + lane];
+    }
+    for (int it = 0; nt < t1; it ^= 1, nt += TW) {
+        const int nn = nt + TW;
+        if (nn < t1) {  // the wave's next tile streams in under this one
+#pragma unroll
+            for (int ks = 0; ks < KS; ks++) w[it ^ 1][ks] = d.wpif[((long)nn * KS + ks) * 64 + lane];
+        }
+        floatx4 acc = zero4();
+#pragma unroll
+        for (int ks = 0; ks < KS; ks++) acc = mfma(*reinterpret_cast<const float4*>(ap + 32 * ks), w[it][ks], acc);
+        const int col = 16 * nt + (lane & 15);
+        if (col < ASIZE) {
+            const float bias = r16(bpi[col]);
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int row = row0 + 4 * q + j;
+                const float x = r16(acc[j] + bias);
+                if (row < B) d.logits[(long)row * LDL + col] = x;
+                if (x > m[j]) {
+                    s[j] = s[j] * __expf(m[j] - x) + 1.0f;
+                    m[j] = x;
+                } else {
+                    s[j] += __expf(x - m[j]);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) stat_merge(m[j], s[j], __shfl_xor(m[j], o, 64), __shfl_xor(s[j], o, 64));
+    if ((lane & 15) == 0) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) red[wave][4 * q + j] = make_float2(m[j], s[j]);
+    }
+    __syncthreads();
+    if (tid < TR && row0 + tid < B) {
+        float mm = -INFINITY, ss = 0.f;
+#pragma unroll
+        for (int w2 = 0; w2 < TW; w2++) stat_merge(mm, ss, red[w2][tid].x, red[w2][tid].y);
+        d.mlq[(long)part * d.Bmax + row0 + tid] = make_float2(mm, ss);
+    }
+}
+
+// one wave per example: CE (f32, NNet.py:145-146), the value head's tail in fp16 (SiLU ->
+// Linear(128, 1) -> tanh), MSE (f32), and the scaled gradients of both: d v_head.2 output (dz1,
+// fp16) and the rows whose column sums are v_head.4's gradients.  Rows past the batch (up to the
+// last 32-row slice) only zero their dz1 T-layout entries.
+__global__ __launch_bounds__(256) void k_amp_loss(AmpDev d, const int32_t* __restrict__ tgt_all,
+                                                  const float* __restrict__ v_all, const int32_t* __restrict__ idx,
+                                                  int B, float vw, float2* __restrict__ lrow) {
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (row >= d.RS * 32) return;
+    if (row >= B) {
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            const int c = 2 * lane + k;
+            const int ct = c >> 4, rs = row >> 5, l = (c & 15) + 16 * ((row & 31) >> 3);
+            d.dz1T[(((long)ct * d.RS + rs) * 64 + l) * 8 + (row & 7)] = (_Float16)0.f;
+        }
+        return;
+    }
+    const float S = d.sc->scale, invB = 1.0f / (float)B;
+    const int src = idx ? idx[row] : row;
+    const int t = tgt_all[src];
+    const float z = v_all[src];
+    float m = -INFINITY, s = 0.f;
+    for (int qq = 0; qq < HQ; qq++) {
+        const float2 ms = d.mlq[(long)qq * d.Bmax + row];
+        stat_merge(m, s, ms.x, ms.y);
+    }
+    const float lse = m + logf(s);
+    if (lane == 0) d.lse[row] = lse;
+    const float ce = lse - d.logits[(long)row * LDL + t];
+    const float* wv2 = d.P + poff(d.H, d.NB, t_head(d.NB, HV_W2));
+    const float bv2 = r16(d.P[poff(d.H, d.NB, t_head(d.NB, HV_B2))]);
+    float z1[2], s16[2], w2[2];
+    float acc = 0.f;
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        const int c = 2 * lane + k;
+        z1[k] = d.zv1[(long)row * VH + c];
+        s16[k] = r16(silu(z1[k]));  // v_head.3 SiLU on fp16
+        w2[k] = r16(wv2[c]);
+        acc += s16[k] * w2[k];
+    }
+    const float z2 = r16(wsum(acc) + bv2);  // v_head.4 (fp16 out)
+    const float v = r16(tanhf(z2));         // tanh on fp16
+    const float e = v - z;
+    const float dv = r16(S * vw * 2.0f * e * invB);  // MSE backward (f32) -> fp16 grad of v
+    const float dz2 = r16(dv * (1.0f - v * v));      // tanh backward (fp16)
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        const int c = 2 * lane + k;
+        d.v2prod[(long)row * VH + c] = dz2 * s16[k];
+        const float ds = r16(dz2 * w2[k]);
+        const float dz1 = r16(ds * silu_grad(z1[k]));  // v_head.3 SiLU backward (fp16)
+        d.dz1_rm[(long)row * VH + c] = (_Float16)dz1;
+        d.dz1f[(long)row * VH + c] = dz1;
+        const int ct = c >> 4, rs = row >> 5, l = (c & 15) + 16 * ((row & 31) >> 3);
+        d.dz1T[(((long)ct * d.RS + rs) * 64 + l) * 8 + (row & 7)] = (_Float16)dz1;
+    }
+    if (lane == 0) {
+        d.dzv2[row] = dz2;
+        lrow[row] = make_float2(ce, e * e);
+    }
+}
+
+// dlogits = fp16(S (softmax - onehot(t)) / B) for the tile's rows over this part's action slices
+// (LDS); their T layout (pi_head.2 weight gradient), their column sums over the 16 rows (bias
+// gradient partial), and dA_pi's split-K partial = dlogits16 Wpi16 over these slices
+template <int H>
+__global__ __launch_bounds__(TTHR) void k_amp_headbwd(AmpDev d, const int32_t* __restrict__ tgt_all,
+                                                      const int32_t* __restrict__ idx, int B) {
+    constexpr int NT = H >= 128 ? H / 128 : 1, NACT = H / (16 * NT);
+    constexpr int SPMAX = (PKS + BQ - 1) / BQ;
+    constexpr int SD = SPMAX * 32 + 8;
+    constexpr int RD = 4;  // weight ring depth (slices)
+    __shared__ __attribute__((aligned(16))) _Float16 DL[TR * SD];
+    __shared__ float LSE[TR];
+    __shared__ int TG[TR];
+    const int tile = blockIdx.x, part = blockIdx.y, row0 = tile * TR;
+    const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    const int ks0 = part * PKS / BQ, ks1 = (part + 1) * PKS / BQ, ns = ks1 - ks0;
+    const bool gw = wave < NACT;
+    const int nt0 = wave * NT;
+    float4 ring[RD][NT];
+    if (gw) {  // the first slices of Wpi^T stream in while the gradient block is built
+#pragma unroll
+        for (int s = 0; s < RD; s++)
+#pragma unroll
+            for (int t = 0; t < NT; t++)
+                ring[s][t] = s < ns ? d.wpit[((long)(nt0 + t) * PKS + ks0 + s) * 64 + lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    if (tid < TR) {
+        const int row = row0 + tid;
+        LSE[tid] = row < B ? d.lse[row] : 0.f;
+        TG[tid] = row < B ? tgt_all[idx ? idx[row] : row] : -1;
+    }
+    __syncthreads();
+    const float S = d.sc->scale, invB = 1.0f / (float)B;
+    const int W = ns * 32;
+    for (int i = tid; i < TR * W; i += TTHR) {
+        const int r = i / W, c = i - r * W, a = 32 * ks0 + c, row = row0 + r;
+        float g = 0.f;
+        if (row < B && a < ASIZE)
+            g = r16(S * (expf(d.logits[(long)row * LDL + a] - LSE[r]) - (a == TG[r] ? 1.0f : 0.0f)) * invB);
+        DL[r * SD + c] = (_Float16)g;
+    }
+    lds_barrier();
+    write_tl(DL, SD, 0, W, d.dlT, d.RS, 2 * ks0, tile, row0 + TR >= B && (tile & 1) == 0);
+    for (int c = tid; c < W; c += TTHR) {  // the bias gradient's partial over these 16 rows
+        float s = 0.f;
+#pragma unroll
+        for (int r = 0; r < TR; r++) s += (float)DL[r * SD + c];
+        d.dbpi_part[(long)tile * LDL + 32 * ks0 + c] = s;
+    }
+    if (!gw) return;
+    const _Float16* ap = DL + (lane & 15) * SD + 8 * (lane >> 4);
+    floatx4 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; t++) acc[t] = zero4();
+    for (int k = 0; k < ns; k++) {
+        const float4 a = *reinterpret_cast<const float4*>(ap + 32 * k);
+        float4(&w)[NT] = ring[k % RD];
+#pragma unroll
+        for (int t = 0; t < NT; t++) acc[t] = mfma(a, w[t], acc[t]);
+        if (k + RD < ns) {
+#pragma unroll
+            for (int t = 0; t < NT; t++) w[t] = d.wpit[((long)(nt0 + t) * PKS + ks0 + k + RD) * 64 + lane];
+        }
+    }
+    const int r = lane & 15, q = lane >> 4;
+#pragma unroll
+    for (int t = 0; t < NT; t++)
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int row = row0 + 4 * q + j;
+            if (row < B) d.dpart[((long)part * d.Bmax + row) * H + 16 * (nt0 + t) + r] = acc[t][j];
+        }
+}
+
+// ------------------------------------------------------------------ backward (trunk)
+// What one row pass of k_amp_bwd reads from memory, loaded into registers BEFORE the GEMM that
+// precedes it: the GEMM's weight-ring refills are issued after these loads, and vmcnt retires in
+// order, so the row pass never waits for the next layer's weights.
+template <int VPL>
+struct RowPre {
+    float u[TRPW][VPL];  // the layer's saved pre-activation (block layers) or Z0 (input layer)
+    float mu[TRPW], rs[TRPW];
+    float g[VPL], be[VPL];
+};
+template <int H>
+__device__ __forceinline__ void row_prefetch(RowPre<H / 64>& R, const AmpDev& d, const float* U, int L, int tg, int tb,
+                                             int row0, int B) {
+    constexpr int VPL = H / 64;
+    const int wave = threadIdx.x >> 6, c0 = (threadIdx.x & 63) * VPL;
+#pragma unroll
+    for (int rr = 0; rr < TRPW; rr++) {
+        const int row = row0 + wave * TRPW + rr;
+        const int rc = row < B ? row : 0;
+#pragma unroll
+        for (int i = 0; i < VPL; i++) R.u[rr][i] = U[(long)rc * H + c0 + i];
+        R.mu[rr] = stat_ptr(d, L, 0)[rc];
+        R.rs[rr] = stat_ptr(d, L, 1)[rc];
+    }
+    const float* g = d.P + poff(H, d.NB, tg);
+    const float* be = d.P + poff(H, d.NB, tb);
+#pragma unroll
+    for (int i = 0; i < VPL; i++) {
+        R.g[i] = g[c0 + i];
+        R.be[i] = be[c0 + i];
+    }
+}
+// CP (per-wave partials, slots 0 gamma, 1 beta, 2 bias) summed over the waves into colpart
+// vectors vb (bias), vb + 1 (gamma), vb + 2 (beta)
+template <int H>
+__device__ __forceinline__ void flush_gbb(const AmpDev& d, const float* CP, int tile, int vb) {
+    for (int i = threadIdx.x; i < 3 * H; i += TTHR) {
+        const int k = i / H, c = i % H;
+        const int slot = k == 0 ? 2 : k - 1;
+        float s = 0.f;
+#pragma unroll
+        for (int w = 0; w < TW; w++) s += CP[w * 3 * H + slot * H + c];
+        d.colpart[((long)tile * d.NVEC + vb + k) * H + c] = s;
+    }
+}
+
+template <int H>
+__global__ __launch_bounds__(TTHR) void k_amp_bwd(AmpDev d, int B, float p, uint64_t seed, uint64_t step,
+                                                  int64_t row_base) {
+    constexpr int LD = H + 4, SA = H + 8, VPL = H / 64, KS = H / 32;
+    constexpr int NT = H >= 128 ? H / 128 : 1, NACT = H / (16 * NT);
+    constexpr int RW = KS * NT <= 16 ? KS : 16 / NT;
+    constexpr int SV = VH + 8;
+    static_assert(SV <= SA || H == 64, "dz1 rows fit the plane buffer");
+    __shared__ __attribute__((aligned(16))) float Xs[TR * LD];
+    __shared__ __attribute__((aligned(16))) float Ts[TR * LD];
+    __shared__ __attribute__((aligned(16))) _Float16 Pa[TR * (SA > SV ? SA : SV)];
+    __shared__ __attribute__((aligned(16))) float CP[TW * 3 * H];
+    const int tile = blockIdx.x, row0 = tile * TR;
+    const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    const bool gw = wave < NACT;
+    const int nt0 = wave * NT, c0 = lane * VPL;
+    const bool zero_half = row0 + TR >= B && (tile & 1) == 0;
+    const float sc = p > 0.f ? 1.0f / (1.0f - p) : 1.0f;
+    const int NB = d.NB;
+    const long HH8 = (long)H * H / 8;
+    const long TLH = (long)(H / 16) * d.RS * 512;  // halves per T-layout [32 RS][H] matrix
+    float* cp = CP + wave * 3 * H;
+
+    // dA_v = fp16(dz1_16 Wv1_16): K = 128 (4 slices), the dz1 rows staged in Pa
+    float4 wv[4][NT];
+    if (gw) {
+#pragma unroll
+        for (int s = 0; s < 4; s++)
+#pragma unroll
+            for (int t = 0; t < NT; t++) wv[s][t] = d.wv1t[((long)(nt0 + t) * 4 + s) * 64 + lane];
+    }
+    for (int i = tid; i < TR * VH / 8; i += TTHR) {
+        const int r = i / (VH / 8), c8 = i % (VH / 8), row = row0 + r;
+        const float4 v = row < B ? reinterpret_cast<const float4*>(d.dz1_rm + (long)row * VH)[c8]
+                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+        *reinterpret_cast<float4*>(Pa + r * SV + 8 * c8) = v;
+    }
+    lds_barrier();
+    floatx4 acc[NT];
+    if (gw) {
+        const _Float16* ap = Pa + (lane & 15) * SV + 8 * (lane >> 4);
+#pragma unroll
+        for (int t = 0; t < NT; t++) acc[t] = zero4();
+#pragma unroll
+        for (int s = 0; s < 4; s++) {
+            const float4 a = *reinterpret_cast<const float4*>(ap + 32 * s);
+#pragma unroll
+            for (int t = 0; t < NT; t++) acc[t] = mfma(a, wv[s][t], acc[t]);
+        }
+        store_acc<NT>(Ts, LD, nt0, acc);
+    }
+    // the heads pass's operands (the split-K parts of dA_pi, the trunk output, its statistics,
+    // the heads' LayerNorm affines) are loaded before the trunk ring starts streaming
+    float dapi[TRPW][VPL], hx[TRPW][VPL], hmu[TRPW], hrs[TRPW];
+    float gp[VPL], bp[VPL], gv[VPL], bv[VPL];
+#pragma unroll
+    for (int rr = 0; rr < TRPW; rr++) {
+        const int row = row0 + wave * TRPW + rr, rc = row < B ? row : 0;
+#pragma unroll
+        for (int i = 0; i < VPL; i++) {
+            float a = 0.f;
+#pragma unroll
+            for (int qq = 0; qq < BQ; qq++) a += d.dpart[((long)qq * d.Bmax + rc) * H + c0 + i];
+            dapi[rr][i] = r16(a);  // fp16(dlogits16 Wpi16)
+            hx[rr][i] = d.hF[(long)rc * H + c0 + i];
+        }
+        hmu[rr] = stat_ptr(d, 1 + 2 * NB, 0)[rc];
+        hrs[rr] = stat_ptr(d, 1 + 2 * NB, 1)[rc];
+    }
+#pragma unroll
+    for (int i = 0; i < VPL; i++) {
+        gp[i] = d.P[poff(H, NB, t_head(NB, HP_G)) + c0 + i];
+        bp[i] = d.P[poff(H, NB, t_head(NB, HP_B)) + c0 + i];
+        gv[i] = d.P[poff(H, NB, t_head(NB, HV_G)) + c0 + i];
+        bv[i] = d.P[poff(H, NB, t_head(NB, HV_B)) + c0 + i];
+    }
+    RowPre<VPL> R;
+    if (NB > 0) row_prefetch<H>(R, d, d.u2 + (long)(NB - 1) * d.Bmax * H, 2 * NB, t_blk(NB - 1, 6), t_blk(NB - 1, 7), row0, B);
+    else row_prefetch<H>(R, d, d.z0, 0, T_GIN, T_BEIN, row0, B);
+    __builtin_amdgcn_sched_barrier(0);
+    float4 ring[RW][NT];
+    if (gw && NB > 0) ring_fill<KS, NT, RW>(ring, d.w2t + (NB - 1) * HH8, nt0);
+    lds_barrier();
+    // heads backward (YachtNNet.py:40-52): dT = dA SiLU'(T) for both heads (f32), one LayerNorm
+    // backward over the shared statistics -> dh
+    {
+        float dgv[TRPW][VPL], dbev[TRPW][VPL];
+#pragma unroll
+        for (int rr = 0; rr < TRPW; rr++) {
+            const int r = wave * TRPW + rr, row = row0 + r;
+            float dx[VPL], xh[VPL];
+#pragma unroll
+            for (int i = 0; i < VPL; i++) {
+                const int c = c0 + i;
+                xh[i] = (hx[rr][i] - hmu[rr]) * hrs[rr];
+                const float dtp = row < B ? dapi[rr][i] * silu_grad(xh[i] * gp[i] + bp[i]) : 0.f;
+                const float dtv = row < B ? r16(Ts[r * LD + c]) * silu_grad(xh[i] * gv[i] + bv[i]) : 0.f;
+                cp[c] = (rr == 0 ? 0.f : cp[c]) + dtp * xh[i];  // pi_head.0.weight
+                cp[H + c] = (rr == 0 ? 0.f : cp[H + c]) + dtp;  // pi_head.0.bias
+                dgv[rr][i] = dtv * xh[i];
+                dbev[rr][i] = dtv;
+                dx[i] = dtp * gp[i] + dtv * gv[i];
+            }
+            if (row < B) ln_bwd<VPL>(xh, dx, H, hrs[rr]);
+#pragma unroll
+            for (int i = 0; i < VPL; i++) Xs[r * LD + c0 + i] = row < B ? dx[i] : 0.f;
+        }
+        lds_barrier();
+        colpart_flush<H>(d, CP, tile, CV_GPI, 2);
+        lds_barrier();
+#pragma unroll
+        for (int i = 0; i < VPL; i++) {
+            float g2 = 0.f, b2 = 0.f;
+#pragma unroll
+            for (int rr = 0; rr < TRPW; rr++) {
+                g2 += dgv[rr][i];
+                b2 += dbev[rr][i];
+            }
+            cp[c0 + i] = g2;
+            cp[H + c0 + i] = b2;
+        }
+        lds_barrier();
+        colpart_flush<H>(d, CP, tile, CV_GV, 2);
+        lds_barrier();
+    }
+
+    // the trunk, last block first: per block  LN2 bwd -> dU2 -> dR1 = dU2 W2 -> dropout, LN1 bwd ->
+    // dU1 -> dh += dU1 W1; the ring streams W2^T[b], W1^T[b], W2^T[b-1], ...
+    for (int b = NB - 1; b >= 0; b--) {
+        for (int half = 1; half >= 0; half--) {
+            // row pass: (half 1) dL2 = dh; (half 0) dL1 = Dropout'(fp16(dR1)).  LayerNorm backward on
+            // S = fp16(SiLU(U)), dU = fp16(fp16(dS) SiLU'(U)); partials: gamma, beta, bias
+#pragma unroll
+            for (int rr = 0; rr < TRPW; rr++) {
+                const int r = wave * TRPW + rr, row = row0 + r;
+                float dx[VPL], xh[VPL];
+#pragma unroll
+                for (int i = 0; i < VPL; i++) {
+                    const int c = c0 + i;
+                    xh[i] = (r16(silu(R.u[rr][i])) - R.mu[rr]) * R.rs[rr];
+                    float dl = 0.f;
+                    if (row < B) {
+                        if (half == 1) {
+                            dl = Xs[r * LD + c];
+                        } else {
+                            const bool k = keep(seed, 1 + b, step, (row_base + row) * H + c, p);
+                            dl = k ? r16(Ts[r * LD + c]) * sc : 0.f;
+                        }
+                    }
+                    cp[c] = (rr == 0 ? 0.f : cp[c]) + dl * xh[i];
+                    cp[H + c] = (rr == 0 ? 0.f : cp[H + c]) + dl;
+                    dx[i] = dl * R.g[i];
+                }
+                if (row < B) ln_bwd<VPL>(xh, dx, H, R.rs[rr]);
+#pragma unroll
+                for (int i = 0; i < VPL; i++) {
+                    dx[i] = row < B ? r16(r16(dx[i]) * silu_grad(R.u[rr][i])) : 0.f;  // dU (fp16)
+                    cp[2 * H + c0 + i] = (rr == 0 ? 0.f : cp[2 * H + c0 + i]) + dx[i];
+                    Pa[r * SA + c0 + i] = (_Float16)dx[i];
+                }
+            }
+            lds_barrier();
+            flush_gbb<H>(d, CP, tile, CV_BLK + 6 * b + (half == 0 ? 0 : 3));
+            write_tl(Pa, SA, 0, H, (half == 0 ? d.du1T : d.du2T) + b * TLH, d.RS, 0, tile, zero_half);
+            // the next row pass's operands, then dX = fp16(dU16 W16) (W2 of half 1, W1 of half 0)
+            if (half == 1)
+                row_prefetch<H>(R, d, d.u1 + (long)b * d.Bmax * H, 1 + 2 * b, t_blk(b, 2), t_blk(b, 3), row0, B);
+            else if (b > 0)
+                row_prefetch<H>(R, d, d.u2 + (long)(b - 1) * d.Bmax * H, 2 * b, t_blk(b - 1, 6), t_blk(b - 1, 7), row0, B);
+            else
+                row_prefetch<H>(R, d, d.z0, 0, T_GIN, T_BEIN, row0, B);
+            __builtin_amdgcn_sched_barrier(0);
+            const float4* cur = (half == 1 ? d.w2t : d.w1t) + b * HH8;
+            const float4* nxt = half == 1 ? d.w1t + b * HH8 : (b > 0 ? d.w2t + (b - 1) * HH8 : nullptr);
+            if (gw) {
+                gemm_ring<KS, NT, RW>(Pa, SA, ring, acc, cur, nxt, nt0);
+                store_acc<NT>(Ts, LD, nt0, acc);
+            }
+            lds_barrier();
+            if (half == 0) {  // residual: dh_b = dh_{b+1} + fp16(dU1 W1)
+#pragma unroll
+                for (int rr = 0; rr < TRPW; rr++) {
+                    const int r = wave * TRPW + rr;
+#pragma unroll
+                    for (int i = 0; i < VPL; i++) Xs[r * LD + c0 + i] += r16(Ts[r * LD + c0 + i]);
+                }
+                lds_barrier();
+            }
+        }
+    }
+    // inp (YachtNNet.py:30-35): dh0 -> Dropout' -> SiLU'(a) -> LayerNorm backward -> dZ0 (fp16)
+#pragma unroll
+    for (int rr = 0; rr < TRPW; rr++) {
+        const int r = wave * TRPW + rr, row = row0 + r;
+        float dx[VPL], xh[VPL];
+#pragma unroll
+        for (int i = 0; i < VPL; i++) {
+            const int c = c0 + i;
+            xh[i] = (R.u[rr][i] - R.mu[rr]) * R.rs[rr];
+            float ds = 0.f;
+            if (row < B) {
+                const bool k = keep(seed, 0, step, (row_base + row) * H + c, p);
+                const float da = k ? Xs[r * LD + c] * sc : 0.f;
+                ds = da * silu_grad(xh[i] * R.g[i] + R.be[i]);
+            }
+            cp[c] = (rr == 0 ? 0.f : cp[c]) + ds * xh[i];
+            cp[H + c] = (rr == 0 ? 0.f : cp[H + c]) + ds;
+            dx[i] = ds * R.g[i];
+        }
+        if (row < B) ln_bwd<VPL>(xh, dx, H, R.rs[rr]);
+#pragma unroll
+        for (int i = 0; i < VPL; i++) {
+            dx[i] = row < B ? r16(dx[i]) : 0.f;
+            cp[2 * H + c0 + i] = (rr == 0 ? 0.f : cp[2 * H + c0 + i]) + dx[i];
+            Pa[r * SA + c0 + i] = (_Float16)dx[i];
+        }
+    }
+    lds_barrier();
+    flush_gbb<H>(d, CP, tile, CV_BIN);
+    write_tl(Pa, SA, 0, H, d.dz0T, d.RS, 0, tile, zero_half);
+}
+
+// ------------------------------------------------------------------ weight gradients
+struct DwJob {
+    const float4* A;  // T layout of dU [B][N]
+    const float4* X;  // T layout of X [B][K]
+    float* dst;       // gradient [N][K] in the flat buffer
+    int N, K;
+};
+// one wave per (job, 16-row tile of W, up to 4 column tiles): sum over the batch's 32-row slices
+__global__ __launch_bounds__(256) void k_amp_dw(const DwJob* __restrict__ jobs, const int4* __restrict__ items,
+                                                int nitems, int RS, int rsn) {
+    const int w = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (w >= nitems) return;
+    const int4 it = items[w];
+    const DwJob jb = jobs[it.x];
+    const int nt = it.y, kt0 = it.z, nk = it.w;
+    floatx4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
+    for (int rs = 0; rs < rsn; rs++) {
+        const float4 a = jb.A[((long)nt * RS + rs) * 64 + lane];
+        float4 x[4];
+#pragma unroll
+        for (int t = 0; t < 4; t++)
+            x[t] = t < nk ? jb.X[((long)(kt0 + t) * RS + rs) * 64 + lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int t = 0; t < 4; t++)
+            if (t < nk) acc[t] = mfma(a, x[t], acc[t]);
+    }
+    const int q = lane >> 4, c = lane & 15;
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+        if (t >= nk) break;
+        const int k = 16 * (kt0 + t) + c;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int n = 16 * nt + 4 * q + j;
+            if (n < jb.N && k < jb.K) jb.dst[(long)n * jb.K + k] = r16(acc[t][j]);  // fp16 grad_weight
+        }
+    }
+}
+
+// fixed-order column sums: dst[c] = sum_r src[r * ld + c] over `rows` rows (tiles or examples)
+struct VsJob {
+    const float* src;
+    float* dst;
+    int ld, N, per_example, round16;
+};
+__global__ __launch_bounds__(256) void k_amp_vecsum(const VsJob* __restrict__ jobs, const int2* __restrict__ items,
+                                                    int nitems, int ntiles, int B) {
+    if ((int)blockIdx.x >= nitems) return;
+    const int2 it = items[blockIdx.x];
+    const VsJob jb = jobs[it.x];
+    const int c = it.y + threadIdx.x;
+    if (c >= jb.N) return;
+    const int rows = jb.per_example ? B : ntiles;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int r = 0;
+    for (; r + 3 < rows; r += 4) {
+        a0 += jb.src[(long)r * jb.ld + c];
+        a1 += jb.src[(long)(r + 1) * jb.ld + c];
+        a2 += jb.src[(long)(r + 2) * jb.ld + c];
+        a3 += jb.src[(long)(r + 3) * jb.ld + c];
+    }
+    for (; r < rows; r++) a0 += jb.src[(long)r * jb.ld + c];
+    const float s = (a0 + a1) + (a2 + a3);
+    jb.dst[c] = jb.round16 ? r16(s) : s;
+}
+
+// ------------------------------------------------------------------ optimiser
+// GradScaler.unscale_: the norm of the unscaled gradients (an inf / nan anywhere makes it so)
+__global__ void k_amp_sq(const float* __restrict__ g, long n, const Scaler* sc, double* __restrict__ part) {
+    __shared__ double red[4];
+    const float inv = 1.0f / sc->scale;
+    double s = 0.0;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+        const double x = (double)(g[i] * inv);
+        s += x * x;
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+__device__ __forceinline__ double sq_total(const double* part) {  // every caller sums in this order
+    double t = 0.0;
+    for (int k = 0; k < SQ_BLOCKS; k++) t += part[k];
+    return t;
+}
+// scaler.step: skipped when the gradients are not finite; else unscale, clip_grad_norm_, AdamW
+// (torch's single-tensor update, bias corrections from the step count of the steps taken)
+__global__ void k_amp_adamw(float* __restrict__ P, float* __restrict__ G, float* __restrict__ M, float* __restrict__ V,
+                            long n, const double* __restrict__ part, double* sq_out, const Scaler* sc, float max_norm,
+                            float lr, float wd, float b1, float b2, float eps) {
+    __shared__ double tot;
+    if (threadIdx.x == 0) {
+        tot = sq_total(part);
+        if (blockIdx.x == 0) *sq_out = tot;
+    }
+    __syncthreads();
+    const double total = tot;
+    if (!isfinite(total)) return;
+    const float inv = 1.0f / sc->scale;
+    const double st = (double)(sc->steps + 1);
+    const float step_size = (float)((double)lr / (1.0 - pow((double)b1, st)));
+    const float bc2_sqrt = (float)sqrt(1.0 - pow((double)b2, st));
+    const float norm = (float)sqrt(total);
+    float coef = max_norm / (norm + 1e-6f);
+    coef = coef > 1.0f ? 1.0f : coef;
+    const float decay = 1.0f - lr * wd;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+        const float gi = (G[i] * inv) * coef;
+        G[i] = gi;
+        float pi = P[i] * decay;
+        const float mi = M[i] + (gi - M[i]) * (1.0f - b1);
+        const float vi = V[i] * b2 + (1.0f - b2) * gi * gi;
+        M[i] = mi;
+        V[i] = vi;
+        const float denom = sqrtf(vi) / bc2_sqrt + eps;
+        pi -= step_size * (mi / denom);
+        P[i] = pi;
+    }
+}
+// fp16 fragments of one weight matrix W[N][K] (f32, row-major): `trans` packs W^T
+struct PackJob {
+    const float* W;
+    float4* dst;
+    int N, K, Np, Kp, trans;  // packed shape Np x Kp (of W or of W^T)
+    long first;               // first item (float4) of this job
+};
+// scaler.update (block 0, thread 0; GradScaler('cuda') defaults: growth 2, backoff 0.5) and the
+// fp16 weight copies for the next step
+__global__ void k_amp_pack(const PackJob* __restrict__ jobs, int njobs, long total, Scaler* sc,
+                           const double* __restrict__ part, int update) {
+    if (update && blockIdx.x == 0 && threadIdx.x == 0) {
+        const double t = sq_total(part);
+        if (!isfinite(t)) {
+            sc->scale *= 0.5f;
+            sc->tracker = 0;
+            sc->found_inf = 1;
+        } else {
+            sc->steps += 1;
+            sc->found_inf = 0;
+            if (++sc->tracker == sc->growth_interval) {
+                sc->scale *= 2.0f;
+                sc->tracker = 0;
+            }
+        }
+    }
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    int j = 0;
+    while (j + 1 < njobs && jobs[j + 1].first <= i) j++;
+    const PackJob jb = jobs[j];
+    const long e = i - jb.first;
+    const int KS = jb.Kp / 32;
+    const int lane = (int)(e % 64);
+    const long pc = e / 64;
+    const int nt = (int)(pc / KS), ks = (int)(pc % KS);
+    const int n = 16 * nt + (lane & 15), k0 = 32 * ks + 8 * (lane >> 4);
+    half8 v;
+#pragma unroll
+    for (int t = 0; t < 8; t++) {
+        const int k = k0 + t;
+        float x = 0.f;
+        if (!jb.trans) {
+            if (n < jb.N && k < jb.K) x = jb.W[(long)n * jb.K + k];
+        } else {  // W^T[n][k] = W[k][n]
+            if (k < jb.N && n < jb.K) x = jb.W[(long)k * jb.K + n];
+        }
+        v[t] = (_Float16)x;
+    }
+    *reinterpret_cast<half8*>(jb.dst + e) = v;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ host
+namespace yk {
+
+struct AmpTrain {
+    int H = 0, NB = 0, Bmax = 0, RS = 0, TMAX = 0;
+    AmpDev d{};
+    std::vector<void*> allocs;
+    long* off_dev = nullptr;
+    DwJob* dw_jobs = nullptr;
+    int4* dw_items = nullptr;
+    int n_dw_items = 0;
+    std::vector<int4> dw_items_host;
+    std::vector<int> dw_job_rows;  // for each item: unused (all jobs span the batch)
+    VsJob* vs_jobs = nullptr;
+    int2* vs_items = nullptr;
+    int n_vs_items = 0;
+    PackJob* pk_jobs = nullptr;
+    int n_pk_jobs = 0;
+    long pk_total = 0;
+    double* sqpart = nullptr;
+    Scaler* sc = nullptr;
+    float* lsum_src_dummy = nullptr;
+    float2* lrow = nullptr;
+    float* lsum = nullptr;
+};
+
+namespace {
+template <class T>
+int aalloc(AmpTrain* a, T** p, size_t count) {
+    void* q = nullptr;
+    if (hipMalloc(&q, sizeof(T) * (count ? count : 1)) != hipSuccess) {
+        (void)hipGetLastError();
+        return YK_ERR_NOMEM;
+    }
+    a->allocs.push_back(q);
+    *p = static_cast<T*>(q);
+    return YK_OK;
+}
+}  // namespace
+
+int amp_create(AmpTrain** out, int H, int NB, int Bmax, float* P, float* G, const long* off, float init_scale,
+               int growth_interval) {
+    if (!(H == 64 || H == 128 || H == 256 || H == 512)) return YK_ERR_ARG;
+    AmpTrain* a = new AmpTrain();
+    a->H = H;
+    a->NB = NB;
+    a->Bmax = Bmax;
+    a->RS = (Bmax + 31) / 32;
+    a->TMAX = (Bmax + TR - 1) / TR;
+    AmpDev& d = a->d;
+    d.H = H;
+    d.NB = NB;
+    d.Bmax = Bmax;
+    d.RS = a->RS;
+    d.TMAX = a->TMAX;
+    d.NVEC = CV_BLK + 6 * NB;
+    d.P = P;
+    d.G = G;
+    const int ntens = 14 + 8 * NB;
+    const size_t HH = (size_t)H * H, RS = (size_t)a->RS, Bm = (size_t)Bmax, T = (size_t)a->TMAX;
+    const size_t tlH = (size_t)(H / 16) * RS * 512;  // halves of one T-layout [32 RS][H] matrix
+    int rc = YK_OK;
+#define AA(p, n) \
+    if (rc == YK_OK) rc = aalloc(a, &(p), (n))
+    AA(a->off_dev, (size_t)ntens);
+    // fp16 weight fragments (float4 = 8 halves)
+    float4 *win_f = nullptr, *w1f = nullptr, *w2f = nullptr, *w1t = nullptr, *w2t = nullptr, *wpif = nullptr,
+           *wpit = nullptr, *wv1f = nullptr, *wv1t = nullptr;
+    AA(win_f, (size_t)H * 64 / 8);
+    AA(w1f, NB * HH / 8 + 1);
+    AA(w2f, NB * HH / 8 + 1);
+    AA(w1t, NB * HH / 8 + 1);
+    AA(w2t, NB * HH / 8 + 1);
+    AA(wpif, (size_t)LDL * H / 8);
+    AA(wpit, (size_t)LDL * H / 8);
+    AA(wv1f, (size_t)VH * H / 8);
+    AA(wv1t, (size_t)VH * H / 8);
+    d.win_f = win_f; d.w1f = w1f; d.w2f = w2f; d.w1t = w1t; d.w2t = w2t;
+    d.wpif = wpif; d.wpit = wpit; d.wv1f = wv1f; d.wv1t = wv1t;
+    AA(d.xT, (size_t)4 * RS * 512);
+    AA(d.hT, NB * tlH + 1);
+    AA(d.r1T, NB * tlH + 1);
+    AA(d.apiT, tlH);
+    AA(d.avT, tlH);
+    AA(d.api_rm, Bm * H);
+    AA(d.av_rm, Bm * H);
+    AA(d.z0, Bm * H);
+    AA(d.u1, NB * Bm * H + 1);
+    AA(d.u2, NB * Bm * H + 1);
+    AA(d.hF, Bm * H);
+    AA(d.stats, (size_t)(2 + 2 * NB) * 2 * Bm);
+    AA(d.logits, Bm * LDL);
+    AA(d.zv1, Bm * VH);
+    AA(d.lse, Bm);
+    AA(d.mlq, (size_t)HQ * Bm);
+    AA(d.dz1_rm, Bm * VH);
+    AA(d.dz1T, (size_t)(VH / 16) * RS * 512);
+    AA(d.dlT, (size_t)PT * RS * 512);
+    AA(d.dz0T, tlH);
+    AA(d.du1T, NB * tlH + 1);
+    AA(d.du2T, NB * tlH + 1);
+    AA(d.dz1f, Bm * VH);
+    AA(d.v2prod, Bm * VH);
+    AA(d.dzv2, Bm);
+    AA(d.dpart, (size_t)BQ * Bm * H);
+    AA(d.dbpi_part, T * LDL);
+    AA(d.colpart, T * d.NVEC * H);
+    AA(a->sqpart, (size_t)SQ_BLOCKS);
+    AA(a->sc, 1);
+    if (rc != YK_OK) {
+        amp_destroy(a);
+        return rc;
+    }
+    d.off = a->off_dev;
+    d.sc = a->sc;
+    std::vector<long> offv(off, off + ntens);
+    YK_HIP(hipMemcpy(a->off_dev, offv.data(), sizeof(long) * ntens, hipMemcpyHostToDevice));
+    Scaler s0{init_scale > 0.f ? init_scale : 65536.0f, 0, 0, 0, growth_interval > 0 ? growth_interval : 2000};
+    YK_HIP(hipMemcpy(a->sc, &s0, sizeof(Scaler), hipMemcpyHostToDevice));
+    // weight-gradient jobs: (dU T layout, X T layout, gradient, N, K)
+    std::vector<DwJob> jobs;
+    auto tl4 = [](const _Float16* p) { return reinterpret_cast<const float4*>(p); };
+    jobs.push_back({tl4(d.dz0T), tl4(d.xT), G + off[T_WIN], H, FEAT});
+    for (int b = 0; b < NB; b++) {
+        jobs.push_back({tl4(d.du1T + b * tlH), tl4(d.hT + b * tlH), G + off[t_blk(b, 0)], H, H});
+        jobs.push_back({tl4(d.du2T + b * tlH), tl4(d.r1T + b * tlH), G + off[t_blk(b, 4)], H, H});
+    }
+    jobs.push_back({tl4(d.dlT), tl4(d.apiT), G + off[t_head(NB, HP_W)], ASIZE, H});
+    jobs.push_back({tl4(d.dz1T), tl4(d.avT), G + off[t_head(NB, HV_W1)], VH, H});
+    std::vector<int4> items;
+    for (size_t j = 0; j < jobs.size(); j++) {
+        const int ntn = (jobs[j].N + 15) / 16, ntk = (jobs[j].K + 15) / 16;
+        for (int nt = 0; nt < ntn; nt++)
+            for (int k0 = 0; k0 < ntk; k0 += 4) items.push_back(make_int4((int)j, nt, k0, std::min(4, ntk - k0)));
+    }
+    a->n_dw_items = (int)items.size();
+    // column-sum jobs: bias / LayerNorm gradients and the two loss sums
+    std::vector<VsJob> vj;
+    const int ldc = d.NVEC * H;
+    auto colv = [&](int v) { return d.colpart + (size_t)v * H; };
+    vj.push_back({colv(CV_BIN), G + off[T_BIN], ldc, H, 0, 1});
+    vj.push_back({colv(CV_GIN), G + off[T_GIN], ldc, H, 0, 0});
+    vj.push_back({colv(CV_BEIN), G + off[T_BEIN], ldc, H, 0, 0});
+    for (int b = 0; b < NB; b++) {
+        const int vb = CV_BLK + 6 * b;
+        vj.push_back({colv(vb + 0), G + off[t_blk(b, 1)], ldc, H, 0, 1});
+        vj.push_back({colv(vb + 1), G + off[t_blk(b, 2)], ldc, H, 0, 0});
+        vj.push_back({colv(vb + 2), G + off[t_blk(b, 3)], ldc, H, 0, 0});
+        vj.push_back({colv(vb + 3), G + off[t_blk(b, 5)], ldc, H, 0, 1});
+        vj.push_back({colv(vb + 4), G + off[t_blk(b, 6)], ldc, H, 0, 0});
+        vj.push_back({colv(vb + 5), G + off[t_blk(b, 7)], ldc, H, 0, 0});
+    }
+    vj.push_back({colv(CV_GPI), G + off[t_head(NB, HP_G)], ldc, H, 0, 0});
+    vj.push_back({colv(CV_BEPI), G + off[t_head(NB, HP_B)], ldc, H, 0, 0});
+    vj.push_back({colv(CV_GV), G + off[t_head(NB, HV_G)], ldc, H, 0, 0});
+    vj.push_back({colv(CV_BEV), G + off[t_head(NB, HV_B)], ldc, H, 0, 0});
+    vj.push_back({d.dbpi_part, G + off[t_head(NB, HP_BIAS)], LDL, ASIZE, 0, 1});
+    vj.push_back({d.dz1f, G + off[t_head(NB, HV_B1)], VH, VH, 1, 1});
+    vj.push_back({d.v2prod, G + off[t_head(NB, HV_W2)], VH, VH, 1, 1});
+    vj.push_back({d.dzv2, G + off[t_head(NB, HV_B2)], 1, 1, 1, 1});
+    const size_t loss_job = vj.size();  // (the trainer's lrow / lsum: filled in per call)
+    vj.push_back({nullptr, nullptr, 2, 2, 1, 0});
+    std::vector<int2> vitems;
+    for (size_t j = 0; j < vj.size(); j++)
+        for (int c = 0; c < vj[j].N; c += 256) vitems.push_back(make_int2((int)j, c));
+    a->n_vs_items = (int)vitems.size();
+    // fp16 pack jobs
+    std::vector<PackJob> pj;
+    long first = 0;
+    auto pack = [&](const float* W, float4* dst, int N, int K, int Np, int Kp, int trans) {
+        pj.push_back({W, dst, N, K, Np, Kp, trans, first});
+        first += (long)Np * Kp / 8;
+    };
+    pack(P + off[T_WIN], win_f, H, FEAT, H, 64, 0);
+    for (int b = 0; b < NB; b++) {
+        pack(P + off[t_blk(b, 0)], w1f + b * HH / 8, H, H, H, H, 0);
+        pack(P + off[t_blk(b, 4)], w2f + b * HH / 8, H, H, H, H, 0);
+        pack(P + off[t_blk(b, 0)], w1t + b * HH / 8, H, H, H, H, 1);
+        pack(P + off[t_blk(b, 4)], w2t + b * HH / 8, H, H, H, H, 1);
+    }
+    pack(P + off[t_head(NB, HP_W)], wpif, ASIZE, H, LDL, H, 0);
+    pack(P + off[t_head(NB, HP_W)], wpit, ASIZE, H, H, LDL, 1);
+    pack(P + off[t_head(NB, HV_W1)], wv1f, VH, H, VH, H, 0);
+    pack(P + off[t_head(NB, HV_W1)], wv1t, VH, H, H, VH, 1);
+    a->n_pk_jobs = (int)pj.size();
+    a->pk_total = first;
+    if (aalloc(a, &a->dw_jobs, jobs.size()) || aalloc(a, &a->dw_items, items.size()) ||
+        aalloc(a, &a->vs_jobs, vj.size()) || aalloc(a, &a->vs_items, vitems.size()) ||
+        aalloc(a, &a->pk_jobs, pj.size())) {
+        amp_destroy(a);
+        return YK_ERR_NOMEM;
+    }
+    YK_HIP(hipMemcpy(a->dw_jobs, jobs.data(), sizeof(DwJob) * jobs.size(), hipMemcpyHostToDevice));
+    YK_HIP(hipMemcpy(a->dw_items, items.data(), sizeof(int4) * items.size(), hipMemcpyHostToDevice));
+    YK_HIP(hipMemcpy(a->vs_items, vitems.data(), sizeof(int2) * vitems.size(), hipMemcpyHostToDevice));
+    YK_HIP(hipMemcpy(a->pk_jobs, pj.data(), sizeof(PackJob) * pj.size(), hipMemcpyHostToDevice));
+    // the loss-sum job's buffers are the trainer's; amp_backward patches them in on first use
+    YK_HIP(hipMemcpy(a->vs_jobs, vj.data(), sizeof(VsJob) * vj.size(), hipMemcpyHostToDevice));
+    a->lsum_src_dummy = nullptr;
+    (void)loss_job;
+    *out = a;
+    return YK_OK;
+}
+
+void amp_destroy(AmpTrain* a) {
+    if (!a) return;
+    for (void* p : a->allocs) (void)hipFree(p);
+    delete a;
+}
+
+int amp_pack(AmpTrain* a, hipStream_t s) {
+    hipLaunchKernelGGL(k_amp_pack, dim3((unsigned)((a->pk_total + 255) / 256)), dim3(256), 0, s, a->pk_jobs,
+                       a->n_pk_jobs, a->pk_total, a->sc, a->sqpart, 0);
+    YK_LAUNCHED();
+    return YK_OK;
+}
+
+int amp_backward(AmpTrain* a, const yk_state_t* states, const int32_t* targets, const float* values,
+                 const int32_t* idx, int B, float dropout, uint64_t seed, uint64_t step, int64_t row_base,
+                 float vloss_weight, float2* lrow, float* lsum, hipStream_t s) {
+    if (B <= 0 || B > a->Bmax) return YK_ERR_ARG;
+    AmpDev& d = a->d;
+    if (a->lrow != lrow || a->lsum != lsum) {  // the loss-sum job reads the trainer's row losses
+        const int j = 3 + 6 * a->NB + 4 + 4;
+        VsJob jb{reinterpret_cast<const float*>(lrow), lsum, 2, 2, 1, 0};
+        YK_HIP(hipMemcpy(a->vs_jobs + j, &jb, sizeof(VsJob), hipMemcpyHostToDevice));
+        a->lrow = lrow;
+        a->lsum = lsum;
+    }
+    const int T = (B + TR - 1) / TR, rsn = (B + 31) / 32;
+    switch (a->H) {
+#define YK_AMP_FWD(HH)                                                                                              \
+    case HH:                                                                                                        \
+        hipLaunchKernelGGL(k_amp_fwd<HH>, dim3(T), dim3(TTHR), 0, s, d, states, idx, B, dropout, seed, step, row_base); \
+        YK_LAUNCHED();                                                                                              \
+        hipLaunchKernelGGL(k_amp_head<HH>, dim3(T, HQ + 1), dim3(TTHR), 0, s, d, B);                               \
+        YK_LAUNCHED();                                                                                              \
+        hipLaunchKernelGGL(k_amp_loss, dim3((rsn * 32 + 3) / 4), dim3(256), 0, s, d, targets, values, idx, B,      \
+                           vloss_weight, lrow);                                                                     \
+        YK_LAUNCHED();                                                                                              \
+        hipLaunchKernelGGL(k_amp_headbwd<HH>, dim3(T, BQ), dim3(TTHR), 0, s, d, targets, idx, B);                  \
+        YK_LAUNCHED();                                                                                              \
+        hipLaunchKernelGGL(k_amp_bwd<HH>, dim3(T), dim3(TTHR), 0, s, d, B, dropout, seed, step, row_base);         \
+        YK_LAUNCHED();                                                                                              \
+        break;
+        YK_AMP_FWD(64)
+        YK_AMP_FWD(128)
+        YK_AMP_FWD(256)
+        YK_AMP_FWD(512)
+#undef YK_AMP_FWD
+        default: return YK_ERR_ARG;
+    }
+    hipLaunchKernelGGL(k_amp_dw, dim3((unsigned)((a->n_dw_items + 3) / 4)), dim3(256), 0, s, a->dw_jobs, a->dw_items,
+                       a->n_dw_items, a->RS, rsn);
+    YK_LAUNCHED();
+    hipLaunchKernelGGL(k_amp_vecsum, dim3((unsigned)a->n_vs_items), dim3(256), 0, s, a->vs_jobs, a->vs_items,
+                       a->n_vs_items, T, B);
+    YK_LAUNCHED();
+    return YK_OK;
+}
+
+int amp_apply(AmpTrain* a, long nparams, float* M, float* V, double* sq_out, float max_norm, float lr, float wd,
+              float b1, float b2, float eps, hipStream_t s) {
+    hipLaunchKernelGGL(k_amp_sq, dim3(SQ_BLOCKS), dim3(256), 0, s, a->d.G, nparams, a->sc, a->sqpart);
+    YK_LAUNCHED();
+    hipLaunchKernelGGL(k_amp_adamw, dim3(2048), dim3(256), 0, s, const_cast<float*>(a->d.P), a->d.G, M, V, nparams,
+                       a->sqpart, sq_out, a->sc, max_norm, lr, wd, b1, b2, eps);
+    YK_LAUNCHED();
+    hipLaunchKernelGGL(k_amp_pack, dim3((unsigned)((a->pk_total + 255) / 256)), dim3(256), 0, s, a->pk_jobs,
+                       a->n_pk_jobs, a->pk_total, a->sc, a->sqpart, 1);
+    YK_LAUNCHED();
+    return YK_OK;
+}
+
+int amp_state(AmpTrain* a, double* out) {
+    Scaler sc;
+    YK_HIP(hipDeviceSynchronize());
+    YK_HIP(hipMemcpy(&sc, a->sc, sizeof(Scaler), hipMemcpyDeviceToHost));
+    out[0] = sc.scale;
+    out[1] = sc.tracker;
+    out[2] = (double)sc.steps;
+    out[3] = sc.found_inf;
+    return YK_OK;
+}
+
+int64_t amp_steps(AmpTrain* a) {
+    Scaler sc;
+    if (hipDeviceSynchronize() != hipSuccess) return YK_ERR_HIP;
+    if (hipMemcpy(&sc, a->sc, sizeof(Scaler), hipMemcpyDeviceToHost) != hipSuccess) return YK_ERR_HIP;
+    return sc.steps;
+}
+
+int amp_set_steps(AmpTrain* a, int64_t steps) {
+    Scaler sc;
+    YK_HIP(hipDeviceSynchronize());
+    YK_HIP(hipMemcpy(&sc, a->sc, sizeof(Scaler), hipMemcpyDeviceToHost));
+    sc.steps = steps;
+    YK_HIP(hipMemcpy(a->sc, &sc, sizeof(Scaler), hipMemcpyHostToDevice));
+    return YK_OK;
+}
+
+}  // namespace yk

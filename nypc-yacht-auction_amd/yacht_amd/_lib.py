@@ -62,6 +62,7 @@ SIGNATURES = {
     "yk_net_leaf_prior": [P, P, P, P, I, P],
     "yk_net_policy_action": [P, P, P, P, I, P],
     "yk_net_destroy": [P],
+    "yk_net_set_precision": [P, I],
     "yk_engine_create": [C.POINTER(P), C.POINTER(YkEngineConfig), P],
     "yk_engine_destroy": [P],
     "yk_selfplay": [P, U64, U32, P],
@@ -77,6 +78,8 @@ SIGNATURES = {
     "yk_trainer_get": [P, I, P],
     "yk_trainer_set": [P, I, P, C.c_int64],
     "yk_trainer_step_count": [P],
+    "yk_trainer_set_row_offset": [P, C.c_int64],
+    "yk_trainer_amp_state": [P, P],
     "yk_arena_results": [P, P, P, P, P, P, P],
     "yk_engine_set_opponent_net": [P, P],
     "yk_engine_stats": [P, P],

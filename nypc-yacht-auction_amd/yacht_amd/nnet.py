@@ -68,10 +68,17 @@ class YachtNNet(nn.Module):  # YachtNNet.py:24-70
         return self.pi_head(h), torch.tanh(self.v_head(h))
 
 
-class YkNet:
-    """Owns a device copy of the weights in the kernels' layout (yk_net_create)."""
+PRECISIONS = {"f32": 0, "f16": 1}  # YK_PREDICT_F32 / YK_PREDICT_F16 (include/yacht_hip.h)
 
-    def __init__(self, state_dict, hidden: int, nblocks: int):
+
+class YkNet:
+    """Owns a device copy of the weights in the kernels' layout (yk_net_create).
+
+    precision "f32" (default): f32-equivalent products, within 1e-5 of the reference's float32
+    predict.  "f16": fp16 weights / GEMM inputs with f32 accumulation - the arithmetic of the
+    reference's own GPU predict under autocast('cuda') (NNet.py:186-189), an opt-in perf mode."""
+
+    def __init__(self, state_dict, hidden: int, nblocks: int, precision: str = "f32"):
         arrs = [np.ascontiguousarray(t.detach().to("cpu", torch.float32).numpy() if torch.is_tensor(t)
                                      else np.asarray(t, dtype=np.float32)) for t in state_dict.values()]
         if len(arrs) != 14 + 8 * nblocks:
@@ -81,6 +88,10 @@ class YkNet:
         call("yk_net_create", C.byref(h), hidden, nblocks, ptrs, len(arrs))
         self.handle = h.value
         self.hidden, self.nblocks = hidden, nblocks
+        if precision not in PRECISIONS:
+            raise ValueError(f"precision must be one of {sorted(PRECISIONS)}")
+        self.precision = precision
+        call("yk_net_set_precision", self.handle, PRECISIONS[precision])
 
     def predict_states(self, states: torch.Tensor):
         """states int64[n, 8] (device) -> pi f32[n, 3226], v f32[n]."""
@@ -164,12 +175,14 @@ class NNetWrapper:
             a = self.args
             self._tr = Trainer(self.nnet.state_dict(), a.hidden, a.nblocks, lr=a.lr, weight_decay=a.weight_decay,
                                max_batch=a.batch_size, vloss_weight=a.get("vloss_weight", 1.0),
-                               dropout=a.dropout, seed=a.get("seed", 0))
+                               dropout=a.dropout, seed=a.get("seed", 0), amp=bool(a.get("amp", False)))
         return self._tr
 
     def train(self, examples, verbose=True):
         """The reference loop: `epochs` passes over shuffled minibatches of `batch_size`
-        (drop_last False), one CE(argmax pi) + vloss_weight * MSE step each, clip 5.0, AdamW.
+        (drop_last False), one CE(argmax pi) + vloss_weight * MSE step each, clip 5.0, AdamW -
+        in float32 (the reference's CPU path), or with args.amp the reference's GPU path
+        (autocast('cuda') + GradScaler, NNet.py:113-116, 141-155) on fp16 MFMA kernels.
         Shuffles come from a torch generator seeded per call (the reference uses the global
         torch RNG); dropout masks from the trainer's Philox stream.
 
@@ -200,10 +213,12 @@ class NNetWrapper:
                     tr.step(states, targets, values, idx=idx)
                     b = idx.numel()
                 else:
-                    loc = torch.tensor_split(idx, world)[rank]
+                    parts = torch.tensor_split(idx, world)
+                    loc = parts[rank]
                     b = loc.numel()
+                    row0 = sum(int(x.numel()) for x in parts[:rank])  # this rank's rows in the minibatch
                     if b:
-                        tr.backward(states, targets, values, idx=loc)
+                        tr.backward(states, targets, values, idx=loc, row0=row0)
                     else:
                         tr.grads().zero_()
                     D.allreduce_grads(tr, weight=b / idx.numel())

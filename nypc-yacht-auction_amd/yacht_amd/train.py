@@ -29,18 +29,26 @@ class _DevView:
 class YkTrainConfig(C.Structure):
     _fields_ = [("max_batch", C.c_int), ("lr", C.c_float), ("weight_decay", C.c_float), ("beta1", C.c_float),
                 ("beta2", C.c_float), ("eps", C.c_float), ("max_grad_norm", C.c_float),
-                ("vloss_weight", C.c_float), ("dropout", C.c_float), ("seed", C.c_uint64)]
+                ("vloss_weight", C.c_float), ("dropout", C.c_float), ("seed", C.c_uint64), ("amp", C.c_int),
+                ("init_scale", C.c_float), ("growth_interval", C.c_int)]
 
 
 class Trainer:
+    """amp=False: the float32 step (the reference's CPU path, NNet.py:157-165).  amp=True: the
+    reference's GPU path (NNet.py:113-116, 141-155) - autocast('cuda') arithmetic on fp16 MFMA
+    kernels, GradScaler('cuda') loss scaling (init_scale, growth_interval; a step whose gradients
+    overflow is skipped and the scale halved)."""
+
     def __init__(self, state_dict, hidden: int, nblocks: int, lr=2e-3, weight_decay=1e-4, max_batch=512,
-                 vloss_weight=1.5, dropout=0.3, seed=0, betas=(0.9, 0.999), eps=1e-8, max_grad_norm=5.0):
+                 vloss_weight=1.5, dropout=0.3, seed=0, betas=(0.9, 0.999), eps=1e-8, max_grad_norm=5.0,
+                 amp=False, init_scale=65536.0, growth_interval=2000):
         self.names = list(state_dict.keys())
         self.shapes = [tuple(t.shape) for t in state_dict.values()]
         arrs = [np.ascontiguousarray(t.detach().to("cpu", torch.float32).numpy()) for t in state_dict.values()]
         ptrs = (C.c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])
         self.cfg = YkTrainConfig(max_batch, lr, weight_decay, betas[0], betas[1], eps, max_grad_norm, vloss_weight,
-                                 dropout, seed & (2**64 - 1))
+                                 dropout, seed & (2**64 - 1), 1 if amp else 0, init_scale, growth_interval)
+        self.amp = bool(amp)
         h = C.c_void_p()
         call("yk_trainer_create", C.byref(h), hidden, nblocks, ptrs, len(arrs), C.byref(self.cfg))
         self.handle = h.value
@@ -58,8 +66,10 @@ class Trainer:
         return torch.as_tensor(_DevView(self._gptr, self.nparams), device="cuda")
 
     # ---- steps
-    def backward(self, states, targets, values, idx=None, batch=None, stream=None):
+    def backward(self, states, targets, values, idx=None, batch=None, stream=None, row0=0):
+        """row0: the global row of this batch's first example in the minibatch (dropout masks)."""
         n = int(batch if batch is not None else (idx.numel() if idx is not None else states.shape[0]))
+        call("yk_trainer_set_row_offset", self.handle, int(row0))
         call("yk_trainer_backward", self.handle, ptr(states), ptr(targets), ptr(values),
              ptr(idx) if idx is not None else None, n, stream_ptr(stream))
 
@@ -68,6 +78,7 @@ class Trainer:
 
     def step(self, states, targets, values, idx=None, batch=None, stream=None):
         n = int(batch if batch is not None else (idx.numel() if idx is not None else states.shape[0]))
+        call("yk_trainer_set_row_offset", self.handle, 0)
         call("yk_trainer_step", self.handle, ptr(states), ptr(targets), ptr(values),
              ptr(idx) if idx is not None else None, n, stream_ptr(stream))
 
@@ -79,7 +90,15 @@ class Trainer:
 
     @property
     def step_count(self) -> int:
+        """Optimiser steps taken (amp: skipped steps are not counted, as torch's AdamW state)."""
         return int(lib().yk_trainer_step_count(self.handle))
+
+    def amp_state(self) -> dict:
+        """GradScaler state (amp mode): scale, growth tracker, steps taken, last step skipped."""
+        out = np.zeros(4, dtype=np.float64)
+        call("yk_trainer_amp_state", self.handle, out.ctypes.data)
+        return {"scale": float(out[0]), "growth_tracker": int(out[1]), "steps": int(out[2]),
+                "found_inf": bool(out[3])}
 
     # ---- host copies in state_dict order
     def _get(self, which):

@@ -169,7 +169,7 @@ def test_nnetwrapper_train_and_checkpoint(T, tmp_path):
     assert w2._trainer().step_count == steps
 
 
-def _ddp_worker(rank, world, port, H, NB, B, W, tg, vv, out):
+def _ddp_worker(rank, world, port, H, NB, B, W, tg, vv, out, dropout=0.0):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -178,10 +178,10 @@ def _ddp_worker(rank, world, port, H, NB, B, W, tg, vv, out):
     from yacht_amd import kernels as K
     from yacht_amd.dist import allreduce_grads
     from yacht_amd.train import Trainer
-    tr = Trainer(_sd(H, NB), H, NB, max_batch=B, dropout=0.0)
+    tr = Trainer(_sd(H, NB), H, NB, max_batch=B, dropout=dropout, seed=5)
     sl = slice(rank * B, (rank + 1) * B)
     S = K.states_to_device(W[sl])
-    tr.backward(S, torch.tensor(tg[sl], device="cuda"), torch.tensor(vv[sl], device="cuda"))
+    tr.backward(S, torch.tensor(tg[sl], device="cuda"), torch.tensor(vv[sl], device="cuda"), row0=rank * B)
     allreduce_grads(tr)
     out["g%d" % rank] = tr.grads().cpu().numpy().copy()
     tr.apply()
@@ -189,7 +189,10 @@ def _ddp_worker(rank, world, port, H, NB, B, W, tg, vv, out):
     dist.destroy_process_group()
 
 
-def test_ddp_gradient_average_equals_union_batch(T, golden):
+@pytest.mark.parametrize("dropout", [0.0, 0.3])
+def test_ddp_gradient_average_equals_union_batch(T, golden, dropout):
+    """With dropout on, each rank draws the masks of its rows of the whole minibatch (row offset =
+    the rank's start), so the averaged gradient is still the single-process one."""
     import torch.multiprocessing as mp
     K, N, TR = T
     H, NB, B = 64, 1, 32
@@ -199,8 +202,9 @@ def test_ddp_gradient_average_equals_union_batch(T, golden):
     vv = (rng.rand(2 * B) * 2 - 1).astype(np.float32)
     mgr = mp.get_context("spawn").Manager()
     out = mgr.dict()
-    mp.start_processes(_ddp_worker, args=(2, 29577, H, NB, B, W, tg, vv, out), nprocs=2, start_method="spawn")
-    ref = TR.Trainer(_sd(H, NB), H, NB, max_batch=2 * B, dropout=0.0)
+    mp.start_processes(_ddp_worker, args=(2, 29577 + int(dropout * 10), H, NB, B, W, tg, vv, out, dropout), nprocs=2,
+                       start_method="spawn")
+    ref = TR.Trainer(_sd(H, NB), H, NB, max_batch=2 * B, dropout=dropout, seed=5)
     ref.backward(K.states_to_device(W), torch.tensor(tg, device="cuda"), torch.tensor(vv, device="cuda"))
     single = ref.grads().cpu().numpy()
     # every rank steps on the same averaged gradient, equal to the union batch's gradient up to
@@ -236,3 +240,131 @@ def test_coach_learn_iteration_and_resume(T, tmp_path):
     c3.loadTrainExamples()
     a, b = c2.trainExamplesHistory[0][5], c3.trainExamplesHistory[0][5]
     assert a[0] == b[0] and a[1] == b[1] and a[2] == b[2]
+
+
+@pytest.mark.parametrize("amp", [False, True])
+def test_dropout_rows_split_over_calls_equal_the_whole_batch(T, golden, amp):
+    """Two backwards of half a minibatch each (row offsets 0 and B/2, gradients averaged) take the
+    whole minibatch's dropout masks: the gradient equals one backward over all B rows."""
+    K, N, TR = T
+    H, NB, B = 64, 2, 64
+    W = golden("states.npz")["states"][:B]
+    rng = np.random.RandomState(2)
+    S = K.states_to_device(W)
+    tg = torch.tensor(rng.randint(0, 3226, B), dtype=torch.int32, device="cuda")
+    vv = torch.tensor(rng.rand(B) * 2 - 1, dtype=torch.float32, device="cuda")
+    whole = TR.Trainer(_sd(H, NB), H, NB, max_batch=B, dropout=0.3, seed=9, amp=amp)
+    whole.backward(S, tg, vv)
+    g_whole = whole.grads().cpu().numpy().copy()
+    half = TR.Trainer(_sd(H, NB), H, NB, max_batch=B, dropout=0.3, seed=9, amp=amp)
+    acc = 0
+    for k in range(2):
+        idx = torch.arange(k * B // 2, (k + 1) * B // 2, dtype=torch.int32, device="cuda")
+        half.backward(S, tg, vv, idx=idx, row0=k * B // 2)
+        acc = acc + 0.5 * half.grads().cpu().numpy().astype(np.float64)
+    # f32 (or fp16-rounded, amp) sums in another grouping
+    assert _relnorm(acc, g_whole) < (2e-3 if amp else 1e-5)
+    other = TR.Trainer(_sd(H, NB), H, NB, max_batch=B, dropout=0.3, seed=9, amp=amp)
+    other.backward(S, tg, vv, idx=torch.arange(B // 2, B, dtype=torch.int32, device="cuda"), row0=0)
+    g_wrong = other.grads().cpu().numpy()
+    half.backward(S, tg, vv, idx=torch.arange(B // 2, B, dtype=torch.int32, device="cuda"), row0=B // 2)
+    assert not np.allclose(g_wrong, half.grads().cpu().numpy())  # the offset selects other masks
+
+
+def _torch_train_steps(sd0, H, NB, X, tg, vv, B, steps, amp, vw=1.5):
+    """The reference's train() inner loop (NNet.py:132-165) on the GPU: autocast('cuda') +
+    GradScaler('cuda') (amp) or float32, AdamW(2e-3, 1e-4), clip 5.0; dropout 0."""
+    import torch.nn.functional as F
+    from yacht_amd.nnet import YachtNNet
+    model = YachtNNet(hidden=H, nblocks=NB, dropout=0.0).cuda().float()
+    model.load_state_dict(sd0)
+    model.train()
+    opt = torch.optim.AdamW(model.parameters(), lr=2e-3, weight_decay=1e-4)
+    scaler = torch.amp.GradScaler("cuda") if amp else None
+    losses, grads1 = [], None
+    for k in range(steps):
+        sl = slice(k * B, (k + 1) * B)
+        opt.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", enabled=amp):
+            out_pi, out_v = model(X[sl])
+            lp = F.cross_entropy(out_pi, tg[sl].long())
+            lv = F.mse_loss(out_v, vv[sl].reshape(-1, 1))
+            loss = lp + vw * lv
+        if amp:
+            scaler.scale(loss).backward()
+            scaler.unscale_(opt)
+        else:
+            loss.backward()
+        if k == 0:
+            grads1 = {n: p.grad.detach().float().cpu().numpy().copy() for n, p in model.named_parameters()}
+        torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=5.0)
+        if amp:
+            scaler.step(opt)
+            scaler.update()
+        else:
+            opt.step()
+        losses.append((float(lp), float(lv)))
+    params = {n: p.detach().cpu().numpy().copy() for n, p in model.named_parameters()}
+    return params, losses, grads1, (scaler.get_scale() if amp else None)
+
+
+@pytest.mark.parametrize("H,NB,B", [(256, 6, 512), (64, 1, 128)])
+def test_amp_steps_vs_torch_autocast_gradscaler(T, golden, H, NB, B):
+    """The mixed-precision mode against the reference's own GPU train step: torch autocast('cuda')
+    + GradScaler('cuda') (NNet.py:141-155) on the same weights and minibatches, 3 steps.
+    Stated tolerance, per quantity: the amp trainer may be no further from torch-AMP than torch's
+    float32 step is (the gap the fp16 rounding itself opens), x1.5 plus a floor: losses (each
+    step), step-1 gradients (per tensor, unscaled, before the clip), parameters after 3 steps
+    (the update p - p0 per tensor).  And the GradScaler state (scale, steps taken) is torch's."""
+    K, N, TR = T
+    torch.manual_seed(11)
+    model = N.YachtNNet(hidden=H, nblocks=NB, dropout=0.0)
+    with torch.no_grad():
+        for m in model.modules():
+            if isinstance(m, torch.nn.LayerNorm):
+                m.weight.uniform_(0.5, 1.5)
+                m.bias.uniform_(-0.2, 0.2)
+    sd0 = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    W = golden("states.npz")["states"]
+    W = np.concatenate([W] * (3 * B // len(W) + 1))[:3 * B]
+    rng = np.random.RandomState(4)
+    S = K.states_to_device(W)
+    X = K.featurize(S)
+    tg = torch.tensor(rng.randint(0, 3226, 3 * B), dtype=torch.int32, device="cuda")
+    vv = torch.tensor(rng.rand(3 * B) * 2 - 1, dtype=torch.float32, device="cuda")
+    torch.backends.cuda.matmul.allow_tf32 = False
+    p_amp, l_amp, g_amp, scale_amp = _torch_train_steps(sd0, H, NB, X, tg, vv, B, 3, True)
+    p_f32, l_f32, g_f32, _ = _torch_train_steps(sd0, H, NB, X, tg, vv, B, 3, False)
+    tr = TR.Trainer(sd0, H, NB, lr=2e-3, weight_decay=1e-4, max_batch=B, vloss_weight=1.5, dropout=0.0, amp=True)
+    ours_l = []
+    g1 = None
+    for k in range(3):
+        idx = torch.arange(k * B, (k + 1) * B, dtype=torch.int32, device="cuda")
+        tr.backward(S, tg, vv, idx=idx)
+        if k == 0:
+            scale = tr.amp_state()["scale"]
+            g1 = {n: v.numpy() / scale for n, v in tr.gradients().items()}
+        tr.apply()
+        ce, se, _ = tr.losses()
+        ours_l.append((ce / B, se / B))
+    tol = lambda ref_gap, ref: 1.5 * ref_gap + 1e-4 * abs(ref) + 1e-7
+    for k in range(3):
+        for j in range(2):
+            gap = abs(l_f32[k][j] - l_amp[k][j])
+            print(f"step {k} loss[{j}]: ours {ours_l[k][j]:.7f} torch-amp {l_amp[k][j]:.7f} torch-f32 {l_f32[k][j]:.7f}")
+            assert abs(ours_l[k][j] - l_amp[k][j]) <= tol(gap, l_amp[k][j]), (k, j)
+    worst = []
+    for name in g_amp:
+        d_ours = _relnorm(g1[name], g_amp[name])
+        d_f32 = _relnorm(g_f32[name], g_amp[name])
+        worst.append((d_ours / max(d_f32, 1e-12), name, d_ours, d_f32))
+        assert d_ours <= 1.5 * d_f32 + 2e-3, ("grad", name, d_ours, d_f32)
+    print("worst grad ratios:", sorted(worst)[-3:])
+    params = tr.state_dict()
+    for name in p_amp:
+        p0 = sd0[name].numpy()
+        d_ours = _relnorm(params[name].numpy() - p0, p_amp[name] - p0)
+        d_f32 = _relnorm(p_f32[name] - p0, p_amp[name] - p0)
+        assert d_ours <= 1.5 * d_f32 + 2e-2, ("update", name, d_ours, d_f32)
+    st = tr.amp_state()
+    assert st["scale"] == scale_amp and tr.step_count == st["steps"]
