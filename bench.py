@@ -145,7 +145,8 @@ def train_leg(model_sd, eng, steps=40, batch=512, seed=0):
     """Config 5's train step on one GPU (NNetWrapper.train semantics, NNet.py:118-174): minibatches
     of 512 replay entries drawn from the self-play records just produced - the device replay
     buffer yk_examples_from_records builds (packed boards, argmax(pi) targets as
-    NNet.py:145-146 takes them, values) - forward + backward + clip + AdamW in f32, dropout 0.3."""
+    NNet.py:145-146 takes them, values) - forward + backward + clip + AdamW, dropout 0.3, in both
+    modes: f32 and the amp trainer (the reference's GPU path)."""
     import torch
 
     from yacht_amd.replay import examples_from_images
@@ -153,26 +154,37 @@ def train_leg(model_sd, eng, steps=40, batch=512, seed=0):
     shard = examples_from_images(eng.pack_records(), eng.n_envs, eng.max_moves, eng.sims)
     S, T, V = shard.states, shard.targets, shard.values
     n = S.shape[0]
-    tr = Trainer(model_sd, H, NB, max_batch=batch, dropout=0.3, seed=seed)
-    g = torch.Generator(device="cuda")
-    g.manual_seed(seed)
-    perm = torch.randperm(n, generator=g, device="cuda").to(torch.int32)
-    for i in range(3):  # warm-up (rocBLAS kernel selection)
-        tr.step(S, T, V, idx=perm[i * batch:(i + 1) * batch])
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(steps):
-        j = (i * batch) % (n - batch)
-        tr.step(S, T, V, idx=perm[j:j + batch])
-    torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / steps
-    ce, se, _ = tr.losses()
-    tr.close()
-    flop = 3 * PREDICT_FLOP * batch  # forward + backward (2x) per example
-    return {"config": f"minibatch {batch} of {n} self-play examples, YachtNNet hidden {H} x {NB}, f32, "
-                      f"AdamW + clip 5.0, dropout 0.3 (rocBLAS GEMMs + fused HIP row kernels)",
-            "ms_per_step": 1000.0 * dt, "examples_per_s": batch / dt, "achieved_tflops": flop / dt / 1e12,
-            "last_loss": ce / batch + 1.5 * se / batch}
+    out = {}
+    for amp in (False, True):
+        tr = Trainer(model_sd, H, NB, max_batch=batch, dropout=0.3, seed=seed, amp=amp)
+        g = torch.Generator(device="cuda")
+        g.manual_seed(seed)
+        perm = torch.randperm(n, generator=g, device="cuda").to(torch.int32)
+        for i in range(3):  # warm-up (rocBLAS kernel selection)
+            tr.step(S, T, V, idx=perm[i * batch:(i + 1) * batch])
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            j = (i * batch) % (n - batch)
+            tr.step(S, T, V, idx=perm[j:j + batch])
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / steps
+        ce, se, _ = tr.losses()
+        st = tr.amp_state() if amp else None
+        tr.close()
+        flop = 3 * PREDICT_FLOP * batch  # forward + backward (2x) per example
+        key = "amp" if amp else "f32"
+        out[key] = {"config": f"minibatch {batch} of {n} self-play examples, YachtNNet hidden {H} x {NB}, " +
+                              ("autocast('cuda') + GradScaler arithmetic on hand-written fp16 MFMA kernels (10 launches)"
+                               if amp else "f32 (rocBLAS GEMMs + fused HIP row kernels)") +
+                              ", AdamW + clip 5.0, dropout 0.3",
+                    "ms_per_step": 1000.0 * dt, "examples_per_s": batch / dt, "achieved_tflops": flop / dt / 1e12,
+                    "last_loss": ce / batch + 1.5 * se / batch}
+        if st:
+            out[key]["grad_scaler"] = st
+    out["ms_per_step"] = out["amp"]["ms_per_step"]
+    out["basis"] = "ms_per_step is the amp mode's (the reference's GPU train path, NNet.py:113-116, 141-155)"
+    return out
 
 
 def shape_leg(net, envs=2048, sims=200, seed=0):
@@ -235,6 +247,50 @@ def f16_leg(sd, envs=4096, sims=100, seed=0):
         out["roofline"] = {"kernel": "k_forward<256, 1>", "bound": "mfma", "achieved": ach,
                            "peak": F16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": ach / F16_MFMA_PEAK_TFLOPS,
                            "work_per_launch": f"{exp_per_launch:.0f} expansions x {PREDICT_FLOP} FLOP"}
+    return out
+
+
+def coach_iter_leg(model, world, games_per_gpu=8192, seed=0, amp=True):
+    """Config 5 at its per-GPU shape: ONE whole Coach.learn iteration (Coach.py:74-139) with
+    main.py's args (main.py:17-43: 25 sims, tempThreshold 15, maxlenOfQueue 200,000, 15 epochs of
+    batch 512, dropout 0.3, arenaCompare 10, updateThreshold 0.55) over numEps = games_per_gpu x
+    N games sharded over the N ranks (65,536 on 8 GPUs = config 5), the reference's GPU train
+    path (autocast + GradScaler: the amp trainer) unless amp=False.  Per-phase wall times."""
+    import shutil
+    import tempfile
+
+    from yacht_amd.coach import Coach
+    from yacht_amd import dist as D
+    from yacht_amd.game import YachtGame
+    from yacht_amd.nnet import NNetWrapper
+    from yacht_amd.utils import dotdict
+    rank, _ = D.rank_world()
+    tmp = tempfile.mkdtemp(prefix="yk_coach_") if rank == 0 else None
+    if world > 1:
+        import torch.distributed as dist
+        box = [tmp]
+        dist.broadcast_object_list(box, src=0)
+        tmp = box[0]
+    args = dotdict(numIters=1, numEps=games_per_gpu * world, tempThreshold=15, updateThreshold=0.55,
+                   maxlenOfQueue=200000, numMCTSSims=25, arenaCompare=10, cpuct=1.5, checkpoint=tmp,
+                   load_folder_file=(tmp, "best.pth.tar"), numItersForTrainExamplesHistory=5, lr=2e-3,
+                   weight_decay=1e-4, epochs=15, batch_size=512, vloss_weight=1.5, cuda=True, hidden=H,
+                   nblocks=NB, dropout=0.3, amp=amp, examples_format="npz", seed=seed)
+    game = YachtGame(seed=seed + 99, env_id=2 * 10**6)
+    nn = NNetWrapper(game, args)
+    nn.nnet.load_state_dict(model.state_dict())
+    c = Coach(game, nn, args)
+    c.learn()
+    n = len(c.trainExamplesHistory[0])
+    steps = 15 * -(-n // 512)
+    out = {"config": f"one Coach.learn iteration, main.py args: numEps {args.numEps} ({games_per_gpu}/GPU x {world}), "
+                     f"25 sims, maxlenOfQueue 200000, 15 epochs x batch 512 "
+                     f"({'autocast + GradScaler on fp16 MFMA' if amp else 'f32'}), dropout 0.3, arenaCompare 10",
+           "examples_kept": n, "train_steps": steps, "gate_tally_prev_new_draws": list(c.last_pit)}
+    out.update({k: round(v, 4) for k, v in c.phase_times.items()})
+    out["train_ms_per_step"] = 1000.0 * c.phase_times["train_s"] / max(steps, 1)
+    if rank == 0:
+        shutil.rmtree(tmp, ignore_errors=True)
     return out
 
 
@@ -310,7 +366,7 @@ def main():
                          "record between dependent launches costs GPU time: ~5 %% of the batch at 1)")
     ap.add_argument("--no-arena", action="store_true", help="skip the config-4 Arena leg")
     ap.add_argument("--no-train", action="store_true", help="skip the config-5 train-step leg")
-    ap.add_argument("--no-coach", action="store_true", help="skip the config-5 Coach-iteration leg")
+    ap.add_argument("--no-coach", action="store_true", help="skip the config-5 Coach-iteration legs")
     ap.add_argument("--no-shape", action="store_true", help="skip the config-3 shape leg (2048 x 200)")
     ap.add_argument("--no-f16", action="store_true", help="skip the fp16 predict-mode leg")
     ap.add_argument("--dist-backend", default=None, help="nccl (RCCL, default on GPUs) or gloo (rehearsal)")
@@ -412,6 +468,7 @@ def main():
         img = last_gather[0] if world > 1 else eng.pack_records(stream=stream)
         coach = coach_leg(model, img, args.envs, 64, args.sims, world, seed=args.seed)
         del img
+        coach["iteration"] = coach_iter_leg(model, world, seed=args.seed)
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()

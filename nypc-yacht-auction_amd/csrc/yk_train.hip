@@ -43,14 +43,9 @@ __device__ __forceinline__ float wmax(float v) {
     for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
     return v;
 }
-// dropout keep-mask from the Philox stream: element `idx` of layer `layer` at optimiser step `step`
-// (idx = global row * H + column: the row counts from the step's row offset, so the ranks of a
-// split minibatch draw the masks one process drawing the whole minibatch would)
-__device__ __forceinline__ bool keep(uint64_t seed, int layer, uint64_t step, long idx, float p) {
-    if (p <= 0.0f) return true;
-    const uint64_t d = philox_draw(seed, 0x44524F50u + (uint32_t)layer, (step << 32) ^ (uint64_t)idx);
-    return (float)(d >> 40) * (1.0f / 16777216.0f) >= p;
-}
+// dropout masks: dropout_keep (yk_common.h) of element global row * H + column; the row counts
+// from the step's row offset, so the ranks of a split minibatch draw the masks one process
+// drawing the whole minibatch would
 
 // LayerNorm of one row held VPL-per-lane (biased variance, eps 1e-5); returns x_hat, mean, rstd
 template <int VPL>
@@ -107,11 +102,12 @@ __global__ void k_inp_fwd(float* Z, const float* b, const float* g, const float*
         rs_o[row] = rs;
     }
     const float sc = 1.0f / (1.0f - p);
+    KeepCache kc;
 #pragma unroll
     for (int i = 0; i < VPL; i++) {
         const long idx = (long)row * H + c0 + i;
         const float a = x[i] * g[c0 + i] + be[c0 + i];
-        const bool k = keep(seed, 0, step, (row_base + row) * H + c0 + i, p);
+        const bool k = dropout_keep(kc, seed, 0, step, (row_base + row) * H + c0 + i, p);
         mask[idx] = k;
         Hout[idx] = k ? silu_f(a) * (p > 0.f ? sc : 1.0f) : 0.0f;
     }
@@ -140,6 +136,7 @@ __global__ void k_blk_fwd(float* U, const float* b, const float* g, const float*
         rs_o[row] = rs;
     }
     const float sc = 1.0f / (1.0f - p);
+    KeepCache kc;
 #pragma unroll
     for (int i = 0; i < VPL; i++) {
         const long idx = (long)row * H + c0 + i;
@@ -147,7 +144,7 @@ __global__ void k_blk_fwd(float* U, const float* b, const float* g, const float*
         if (Hin) {
             out[idx] = Hin[idx] + l;  // residual
         } else {
-            const bool k = keep(seed, layer, step, (row_base + row) * H + c0 + i, p);
+            const bool k = dropout_keep(kc, seed, layer, step, (row_base + row) * H + c0 + i, p);
             mask[idx] = k;
             out[idx] = k ? l * (p > 0.f ? sc : 1.0f) : 0.0f;
         }

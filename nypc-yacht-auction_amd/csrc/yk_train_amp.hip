@@ -97,7 +97,8 @@ __host__ __device__ inline long poff(int H, int NB, int k) {
     const int s = k - 4 - 8 * NB;
     const long o = base + NB * (2 * hh + 6 * h), A = ASIZE;
     const long so[10] = {0, h, 2 * h, 2 * h + A * h, 2 * h + A * h + A, 3 * h + A * h + A, 4 * h + A * h + A,
-                         4 * h + A * h + A + 128 * h, 4 * h + A * h + A + 129 * h, 4 * h + A * h + A + 130 * h};
+                         4 * h + A * h + A + 128 * h, 4 * h + A * h + A + 128 * h + 128,
+                         4 * h + A * h + A + 128 * h + 256};
     return o + so[s];
 }
 enum { HP_G = 0, HP_B = 1, HP_W = 2, HP_BIAS = 3, HV_G = 4, HV_B = 5, HV_W1 = 6, HV_B1 = 7, HV_W2 = 8, HV_B2 = 9 };
@@ -114,17 +115,27 @@ __device__ __forceinline__ float wsum(float v) {
     for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
 }
+// two full-wave sums at once on the DPP path (quad / row shuffles, row broadcasts, lane 63 read):
+// the row passes' reductions, whose latency is on every layer's critical path
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ float dpp(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, ROW_MASK, 0xF, false));
+}
+__device__ __forceinline__ void wsum2(float& a, float& b) {
+    a += dpp<0xB1, 0xF>(a);   b += dpp<0xB1, 0xF>(b);    // quad_perm [1,0,3,2]
+    a += dpp<0x4E, 0xF>(a);   b += dpp<0x4E, 0xF>(b);    // quad_perm [2,3,0,1]
+    a += dpp<0x141, 0xF>(a);  b += dpp<0x141, 0xF>(b);   // row_half_mirror
+    a += dpp<0x140, 0xF>(a);  b += dpp<0x140, 0xF>(b);   // row_mirror: 16-lane row sums
+    a += dpp<0x142, 0xA>(a);  b += dpp<0x142, 0xA>(b);   // row_bcast15
+    a += dpp<0x143, 0xC>(a);  b += dpp<0x143, 0xC>(b);   // row_bcast31
+    a = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, a), 63));
+    b = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, b), 63));
+}
 __device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
 __device__ __forceinline__ float silu(float x) { return x * sigm(x); }
 __device__ __forceinline__ float silu_grad(float x) {
     const float s = sigm(x);
     return s * (1.0f + x * (1.0f - s));
-}
-// the f32 trainer's dropout mask (yk_train.hip keep): element idx of layer `layer` at step `step`
-__device__ __forceinline__ bool keep(uint64_t seed, int layer, uint64_t step, long idx, float p) {
-    if (p <= 0.0f) return true;
-    const uint64_t d = philox_draw(seed, 0x44524F50u + (uint32_t)layer, (step << 32) ^ (uint64_t)idx);
-    return (float)(d >> 40) * (1.0f / 16777216.0f) >= p;
 }
 // workgroup barrier that does not drain the weight ring's outstanding loads (vmcnt)
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
@@ -202,20 +213,22 @@ __device__ __forceinline__ void store_acc(float* T, int ld, int nt0, const float
 #pragma unroll
         for (int j = 0; j < 4; j++) T[(4 * q + j) * ld + 16 * (nt0 + t) + r] = acc[t][j];
 }
-// LayerNorm statistics (biased variance, eps 1e-5) of a row held VPL per lane
+// LayerNorm statistics (biased variance, eps 1e-5) of a row held VPL per lane: one pass of sums
+// shifted by the row's first value (so E[(x-k)^2] - E[x-k]^2 does not cancel), one reduction
 template <int VPL>
 __device__ __forceinline__ void ln_stats(const float (&x)[VPL], int H, float& mu, float& rs) {
-    float s = 0.f;
-#pragma unroll
-    for (int i = 0; i < VPL; i++) s += x[i];
-    mu = wsum(s) / (float)H;
-    float v = 0.f;
+    const float k = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, x[0])));
+    float s = 0.f, q = 0.f;
 #pragma unroll
     for (int i = 0; i < VPL; i++) {
-        const float d = x[i] - mu;
-        v += d * d;
+        const float d = x[i] - k;
+        s += d;
+        q += d * d;
     }
-    rs = 1.0f / sqrtf(wsum(v) / (float)H + 1e-5f);
+    wsum2(s, q);
+    const float m = s / (float)H;
+    mu = k + m;
+    rs = 1.0f / sqrtf(fmaxf(q / (float)H - m * m, 0.f) + 1e-5f);
 }
 // LayerNorm input gradient from dL/dxhat (dx, in place): rs / H (H dx - sum dx - xhat sum(dx xhat))
 template <int VPL>
@@ -226,8 +239,7 @@ __device__ __forceinline__ void ln_bwd(const float (&xh)[VPL], float (&dx)[VPL],
         a += dx[i];
         b += dx[i] * xh[i];
     }
-    a = wsum(a);
-    b = wsum(b);
+    wsum2(a, b);
 #pragma unroll
     for (int i = 0; i < VPL; i++) dx[i] = rs / (float)H * ((float)H * dx[i] - a - xh[i] * b);
 }
@@ -266,6 +278,7 @@ __global__ __launch_bounds__(TTHR) void k_amp_fwd(AmpDev d, const yk_state_t* __
     const float sc = p > 0.f ? 1.0f / (1.0f - p) : 1.0f;
     const int NB = d.NB;
     const long HH8 = (long)H * H / 8;  // float4 per packed H x H matrix
+    KeepCache kc;  // dropout masks (yk_common.h), one Philox draw per 4 elements
 
     // the input layer's vectors, its weights (K = 64: 2 slices), the first block's ring, then features
     for (int i = tid; i < 3 * H; i += TTHR) VL[i] = d.P[poff(H, d.NB, T_BIN + i / H) + i % H];
@@ -328,7 +341,7 @@ __global__ __launch_bounds__(TTHR) void k_amp_fwd(AmpDev d, const yk_state_t* __
 #pragma unroll
             for (int i = 0; i < VPL; i++) {
                 const float a = (x[i] - mu) * rs * VL[H + c0 + i] + VL[2 * H + c0 + i];
-                const bool k = keep(seed, 0, step, (row_base + row) * H + c0 + i, p);
+                const bool k = dropout_keep(kc, seed, 0, step, (row_base + row) * H + c0 + i, p);
                 x[i] = k ? silu(a) * sc : 0.f;
             }
         } else {
@@ -390,7 +403,7 @@ __global__ __launch_bounds__(TTHR) void k_amp_fwd(AmpDev d, const yk_state_t* __
                     for (int i = 0; i < VPL; i++) {
                         const float l = (s[i] - mu) * rs * VL[H + c0 + i] + VL[2 * H + c0 + i];
                         if (half == 0) {
-                            const bool k = keep(seed, 1 + b, step, (row_base + row) * H + c0 + i, p);
+                            const bool k = dropout_keep(kc, seed, 1 + b, step, (row_base + row) * H + c0 + i, p);
                             x[i] = k ? l * sc : 0.f;
                         } else {
                             x[i] = Xs[r * LD + c0 + i] + l;  // residual (f32)
@@ -504,22 +517,15 @@ __global__ __launch_bounds__(TTHR) void k_amp_head(AmpDev d, int B) {
         m[j] = -INFINITY;
         s[j] = 0.f;
     }
-    float4 w[2][KS];
-    int nt = t0 + wave;
-    if (nt < t1) {
+    auto load = [&](float4(&w)[KS], int n) {
 #pragma unroll
-        for (int ks = 0; ks < KS; ks++) w[0][ks] = d.wpif[((long)nt * KS + ks) * 64 + lane];
-    }
-    for (int it = 0; nt < t1; it ^= 1, nt += TW) {
-        const int nn = nt + TW;
-        if (nn < t1) {  // the wave's next tile streams in under this one
-#pragma unroll
-            for (int ks = 0; ks < KS; ks++) w[it ^ 1][ks] = d.wpif[((long)nn * KS + ks) * 64 + lane];
-        }
+        for (int ks = 0; ks < KS; ks++) w[ks] = d.wpif[((long)n * KS + ks) * 64 + lane];
+    };
+    auto do_tile = [&](const float4(&w)[KS], int n) {
         floatx4 acc = zero4();
 #pragma unroll
-        for (int ks = 0; ks < KS; ks++) acc = mfma(*reinterpret_cast<const float4*>(ap + 32 * ks), w[it][ks], acc);
-        const int col = 16 * nt + (lane & 15);
+        for (int ks = 0; ks < KS; ks++) acc = mfma(*reinterpret_cast<const float4*>(ap + 32 * ks), w[ks], acc);
+        const int col = 16 * n + (lane & 15);
         if (col < ASIZE) {
             const float bias = r16(bpi[col]);
 #pragma unroll
@@ -535,6 +541,17 @@ __global__ __launch_bounds__(TTHR) void k_amp_head(AmpDev d, int B) {
                 }
             }
         }
+    };
+    float4 wa[KS], wb[KS];  // two tiles' slices: the wave's next tile streams in under this one
+    int nt = t0 + wave;
+    if (nt < t1) load(wa, nt);
+    for (; nt < t1; nt += 2 * TW) {
+        const int n2 = nt + TW;
+        if (n2 < t1) load(wb, n2);
+        do_tile(wa, nt);
+        if (n2 >= t1) break;
+        if (n2 + TW < t1) load(wa, n2 + TW);
+        do_tile(wb, n2);
     }
 #pragma unroll
     for (int j = 0; j < 4; j++)
@@ -671,14 +688,19 @@ __global__ __launch_bounds__(TTHR) void k_amp_headbwd(AmpDev d, const int32_t* _
     floatx4 acc[NT];
 #pragma unroll
     for (int t = 0; t < NT; t++) acc[t] = zero4();
-    for (int k = 0; k < ns; k++) {
-        const float4 a = *reinterpret_cast<const float4*>(ap + 32 * k);
-        float4(&w)[NT] = ring[k % RD];
+    for (int k0 = 0; k0 < ns; k0 += RD) {
 #pragma unroll
-        for (int t = 0; t < NT; t++) acc[t] = mfma(a, w[t], acc[t]);
-        if (k + RD < ns) {
+        for (int j = 0; j < RD; j++) {  // static ring slots
+            const int k = k0 + j;
+            if (k < ns) {
+                const float4 a = *reinterpret_cast<const float4*>(ap + 32 * k);
 #pragma unroll
-            for (int t = 0; t < NT; t++) w[t] = d.wpit[((long)(nt0 + t) * PKS + ks0 + k + RD) * 64 + lane];
+                for (int t = 0; t < NT; t++) acc[t] = mfma(a, ring[j][t], acc[t]);
+                if (k + RD < ns) {
+#pragma unroll
+                    for (int t = 0; t < NT; t++) ring[j][t] = d.wpit[((long)(nt0 + t) * PKS + ks0 + k + RD) * 64 + lane];
+                }
+            }
         }
     }
     const int r = lane & 15, q = lane >> 4;
@@ -757,6 +779,7 @@ __global__ __launch_bounds__(TTHR) void k_amp_bwd(AmpDev d, int B, float p, uint
     const float sc = p > 0.f ? 1.0f / (1.0f - p) : 1.0f;
     const int NB = d.NB;
     const long HH8 = (long)H * H / 8;
+    KeepCache kc;
     const long TLH = (long)(H / 16) * d.RS * 512;  // halves per T-layout [32 RS][H] matrix
     float* cp = CP + wave * 3 * H;
 
@@ -882,7 +905,7 @@ __global__ __launch_bounds__(TTHR) void k_amp_bwd(AmpDev d, int B, float p, uint
                         if (half == 1) {
                             dl = Xs[r * LD + c];
                         } else {
-                            const bool k = keep(seed, 1 + b, step, (row_base + row) * H + c, p);
+                            const bool k = dropout_keep(kc, seed, 1 + b, step, (row_base + row) * H + c, p);
                             dl = k ? r16(Ts[r * LD + c]) * sc : 0.f;
                         }
                     }
@@ -938,7 +961,7 @@ __global__ __launch_bounds__(TTHR) void k_amp_bwd(AmpDev d, int B, float p, uint
             xh[i] = (R.u[rr][i] - R.mu[rr]) * R.rs[rr];
             float ds = 0.f;
             if (row < B) {
-                const bool k = keep(seed, 0, step, (row_base + row) * H + c, p);
+                const bool k = dropout_keep(kc, seed, 0, step, (row_base + row) * H + c, p);
                 const float da = k ? Xs[r * LD + c] * sc : 0.f;
                 ds = da * silu_grad(xh[i] * R.g[i] + R.be[i]);
             }
@@ -998,7 +1021,8 @@ __global__ __launch_bounds__(256) void k_amp_dw(const DwJob* __restrict__ jobs, 
     }
 }
 
-// fixed-order column sums: dst[c] = sum_r src[r * ld + c] over `rows` rows (tiles or examples)
+// fixed-order column sums: dst[c] = sum_r src[r * ld + c] over `rows` rows (tiles or examples).
+// Block = one job's 16 columns x 16 row groups (row r to group r % 16), the groups added in order.
 struct VsJob {
     const float* src;
     float* dst;
@@ -1006,23 +1030,29 @@ struct VsJob {
 };
 __global__ __launch_bounds__(256) void k_amp_vecsum(const VsJob* __restrict__ jobs, const int2* __restrict__ items,
                                                     int nitems, int ntiles, int B) {
+    __shared__ float part[16][17];
     if ((int)blockIdx.x >= nitems) return;
     const int2 it = items[blockIdx.x];
     const VsJob jb = jobs[it.x];
-    const int c = it.y + threadIdx.x;
-    if (c >= jb.N) return;
+    const int c = it.y + (threadIdx.x & 15), g = threadIdx.x >> 4;
     const int rows = jb.per_example ? B : ntiles;
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-    int r = 0;
-    for (; r + 3 < rows; r += 4) {
-        a0 += jb.src[(long)r * jb.ld + c];
-        a1 += jb.src[(long)(r + 1) * jb.ld + c];
-        a2 += jb.src[(long)(r + 2) * jb.ld + c];
-        a3 += jb.src[(long)(r + 3) * jb.ld + c];
+    float a0 = 0.f, a1 = 0.f;
+    if (c < jb.N) {
+        int r = g;
+        for (; r + 16 < rows; r += 32) {
+            a0 += jb.src[(long)r * jb.ld + c];
+            a1 += jb.src[(long)(r + 16) * jb.ld + c];
+        }
+        for (; r < rows; r += 16) a0 += jb.src[(long)r * jb.ld + c];
     }
-    for (; r < rows; r++) a0 += jb.src[(long)r * jb.ld + c];
-    const float s = (a0 + a1) + (a2 + a3);
-    jb.dst[c] = jb.round16 ? r16(s) : s;
+    part[g][threadIdx.x & 15] = a0 + a1;
+    __syncthreads();
+    if (g == 0 && c < jb.N) {
+        float s = 0.f;
+#pragma unroll
+        for (int k = 0; k < 16; k++) s += part[k][threadIdx.x];
+        jb.dst[c] = jb.round16 ? r16(s) : s;
+    }
 }
 
 // ------------------------------------------------------------------ optimiser
@@ -1041,23 +1071,29 @@ __global__ void k_amp_sq(const float* __restrict__ g, long n, const Scaler* sc, 
     __syncthreads();
     if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
 }
-__device__ __forceinline__ double sq_total(const double* part) {  // every caller sums in this order
+// the SQ_BLOCKS partials summed by a 256-thread block in one fixed order (every caller gets the
+// same bits): 4 per thread, the wave butterflies, the 4 waves in order
+__device__ __forceinline__ double sq_total(const double* part) {
+    __shared__ double red[4];
+    static_assert(SQ_BLOCKS == 4 * 256, "4 partials per thread");
     double t = 0.0;
-    for (int k = 0; k < SQ_BLOCKS; k++) t += part[k];
-    return t;
+#pragma unroll
+    for (int k = 0; k < 4; k++) t += part[threadIdx.x + 256 * k];
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) t += __shfl_xor(t, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = t;
+    __syncthreads();
+    const double tot = (red[0] + red[1]) + (red[2] + red[3]);
+    __syncthreads();
+    return tot;
 }
 // scaler.step: skipped when the gradients are not finite; else unscale, clip_grad_norm_, AdamW
 // (torch's single-tensor update, bias corrections from the step count of the steps taken)
 __global__ void k_amp_adamw(float* __restrict__ P, float* __restrict__ G, float* __restrict__ M, float* __restrict__ V,
                             long n, const double* __restrict__ part, double* sq_out, const Scaler* sc, float max_norm,
                             float lr, float wd, float b1, float b2, float eps) {
-    __shared__ double tot;
-    if (threadIdx.x == 0) {
-        tot = sq_total(part);
-        if (blockIdx.x == 0) *sq_out = tot;
-    }
-    __syncthreads();
-    const double total = tot;
+    const double total = sq_total(part);
+    if (blockIdx.x == 0 && threadIdx.x == 0) *sq_out = total;
     if (!isfinite(total)) return;
     const float inv = 1.0f / sc->scale;
     const double st = (double)(sc->steps + 1);
@@ -1091,8 +1127,8 @@ struct PackJob {
 // fp16 weight copies for the next step
 __global__ void k_amp_pack(const PackJob* __restrict__ jobs, int njobs, long total, Scaler* sc,
                            const double* __restrict__ part, int update) {
+    const double t = (update && blockIdx.x == 0) ? sq_total(part) : 0.0;
     if (update && blockIdx.x == 0 && threadIdx.x == 0) {
-        const double t = sq_total(part);
         if (!isfinite(t)) {
             sc->scale *= 0.5f;
             sc->tracker = 0;
@@ -1247,6 +1283,11 @@ int amp_create(AmpTrain** out, int H, int NB, int Bmax, float* P, float* G, cons
         amp_destroy(a);
         return rc;
     }
+    for (int k = 0; k < ntens; k++)  // the kernels' closed-form offsets are the trainer's
+        if (poff(H, NB, k) != off[k]) {
+            amp_destroy(a);
+            return YK_ERR_ARG;
+        }
     d.off = a->off_dev;
     d.sc = a->sc;
     std::vector<long> offv(off, off + ntens);
@@ -1298,7 +1339,7 @@ int amp_create(AmpTrain** out, int H, int NB, int Bmax, float* P, float* G, cons
     vj.push_back({nullptr, nullptr, 2, 2, 1, 0});
     std::vector<int2> vitems;
     for (size_t j = 0; j < vj.size(); j++)
-        for (int c = 0; c < vj[j].N; c += 256) vitems.push_back(make_int2((int)j, c));
+        for (int c = 0; c < vj[j].N; c += 16) vitems.push_back(make_int2((int)j, c));
     a->n_vs_items = (int)vitems.size();
     // fp16 pack jobs
     std::vector<PackJob> pj;

@@ -121,12 +121,22 @@ class Coach:
         writes the files; every rank reads the checkpoints back, so all ranks stay identical."""
         from . import dist as D
         from .arena import GatingArena
+        import time
+
+        import torch
         a = self.args
         rank, _world = D.rank_world()
+
+        def clock():
+            if torch.cuda.is_available():
+                torch.cuda.synchronize()
+            return time.perf_counter()
         for i in range(1, a.numIters + 1):
             log.info(f"Starting Iter #{i} ...")
+            t = {"t0": clock()}  # phase wall times of this iteration (self.phase_times)
             if not self.skipFirstSelfPlay or i > 1:
                 self.trainExamplesHistory.append(self.selfPlayExamples(a.numEps, maxlen=a.maxlenOfQueue))
+            t["selfplay"] = clock()
             if len(self.trainExamplesHistory) > a.numItersForTrainExamplesHistory:
                 log.warning(f"Removing the oldest entry in trainExamples. len(trainExamplesHistory) = "
                             f"{len(self.trainExamplesHistory)}")
@@ -136,13 +146,16 @@ class Coach:
                 self.nnet.save_checkpoint(folder=a.checkpoint, filename="temp.pth.tar")
             D.barrier()
             self.pnet.load_checkpoint(folder=a.checkpoint, filename="temp.pth.tar")
+            t["save"] = clock()
             # the reference shuffles the pooled examples here (Coach.py:104-108) and its
             # DataLoader(shuffle=True) reshuffles every epoch; train's per-epoch permutation is
             # that reshuffle
             self.nnet.train(self.trainExamplesHistory)
+            t["train"] = clock()
             log.info("PITTING AGAINST PREVIOUS VERSION")
             pwins, nwins, draws = GatingArena(self.game, self.pnet, self.nnet, a).playGames(
                 a.arenaCompare, env_base=self._streams(2 * int(a.arenaCompare / 2)))
+            t["arena"] = clock()
             log.info("NEW/PREV WINS : %d / %d ; DRAWS : %d" % (nwins, pwins, draws))
             D.barrier()  # every rank has read temp.pth.tar before it can be rewritten
             if pwins + nwins == 0 or float(nwins) / (pwins + nwins) < a.updateThreshold:
@@ -155,6 +168,10 @@ class Coach:
                     self.nnet.save_checkpoint(folder=a.checkpoint, filename="best.pth.tar")
             self.last_pit = (pwins, nwins, draws)
             D.barrier()
+            t["gate"] = clock()
+            keys = ["t0", "selfplay", "save", "train", "arena", "gate"]
+            self.phase_times = {k + "_s": t[k] - t[p] for p, k in zip(keys, keys[1:])}
+            self.phase_times["iteration_s"] = t["gate"] - t["t0"]
 
     def getCheckpointFile(self, iteration):
         return "checkpoint_" + str(iteration) + ".pth.tar"

@@ -42,14 +42,31 @@ class ExampleShard:
     def host(self) -> dict:
         """Host arrays of the shard with the full policies (sparse CSR, float64 as
         MCTS.getActionProb returns them): states u64[n, 8], pi_indptr i64[n+1], pi_cols i32,
-        pi_vals f64, values f64[n], targets i32[n]."""
+        pi_vals f64, values f64[n], targets i32[n].  Built once: only the rank images holding
+        the kept tail of the deque are copied to the host, and the device images are released
+        afterwards (the shard keeps its compact device examples and these host arrays)."""
         if self._host is None:
             if self._source is None:
                 raise ValueError("this shard has no record images to rebuild policies from")
             images, E, M, sims, n_games, skip = self._source
-            h = host_examples(images.cpu().numpy(), E, M, sims, n_games)
-            n = len(self)
-            self._host = _tail(h, skip, n)
+            R = images.shape[0]
+            total_games = R * E if n_games is None or n_games < 0 else min(n_games, R * E)
+            # examples per rank image (from the images' move counts), so the images entirely before
+            # the kept tail are never copied
+            L = record_layout(E, M, sims)
+            nm_off, nm_bytes = L["n_moves"]
+            per = []
+            for r in range(R):
+                g = min(max(total_games - r * E, 0), E)
+                nm = images[r, nm_off:nm_off + nm_bytes].view(torch.int32)[:g] if g else None
+                per.append(int(nm.clamp(0, M).sum().item()) if g else 0)
+            r0, before = 0, 0
+            while r0 < R - 1 and before + per[r0] <= skip:
+                before += per[r0]
+                r0 += 1
+            h = host_examples(images[r0:].cpu().numpy(), E, M, sims, total_games - r0 * E)
+            self._host = _tail(h, skip - before, len(self))
+            self._source = None
         return self._host
 
     def __iter__(self):
@@ -95,6 +112,19 @@ def examples_from_images(images: torch.Tensor, n_envs: int, max_moves: int, sims
     if int(cnt.value) != n:
         raise RuntimeError(f"yk_examples_from_records wrote {cnt.value} examples, expected {n}")
     return ExampleShard(states[:n], targets[:n], values[:n], source=(imgs, n_envs, max_moves, sims, n_games, skip))
+
+
+def record_layout(n_envs: int, max_moves: int, sims: int) -> dict:
+    """(byte offset, bytes) of each part of one rank's record image (yk_engine_pack_records)."""
+    E, M = n_envs, max_moves
+    vcap = _vcap(M, sims)
+    parts = [("states", 8 * E * M * 8), ("info", 4 * E * M * 8), ("ctr", 8 * E * M * 2), ("values", 8 * E * M),
+             ("visits_raw", 4 * E * vcap), ("voff", 4 * E * (M + 1)), ("n_moves", 4 * E), ("final", 8 * E * 8)]
+    out, off = {}, 0
+    for name, nb in parts:
+        out[name] = (off, nb)
+        off += (nb + 15) & ~15
+    return out
 
 
 # ---------------------------------------------------------------- host side (numpy)

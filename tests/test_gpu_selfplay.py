@@ -116,7 +116,24 @@ def test_selfplay_net_prior_replayed_by_oracle(Y):
     assert check_recorded_priors(pi, v, cnt, leaves, sd) == int(cnt.sum())
 
 
-def _net_prior_sampled_games_vs_oracle(E, N, n, sims, seed, base, stride):
+def _divergence_vs_independent_f32(rec, pick, sd, sims, seed, base):
+    """How often the search outcome of an independently computed f32 predict differs: the oracle
+    plays the sampled games with its own float32 YachtNNet (C, the reference's CPU arithmetic,
+    MODE_MLP, no replay), and each game is compared move by move with the engine's (action and
+    visit counts).  Returns (fraction of games that diverge, first diverging move per game or -1)."""
+    orc = O.selfplay(base + pick, seed, sims, 1.5, 15, O.MODE_MLP, net=O.Net(sd, 256, 6), max_moves=48, threads=16)
+    assert orc["nerr"] == 0
+    first = np.full(len(pick), -1)
+    for r, e in enumerate(pick):
+        M = min(int(orc["stats"][r, 0]), int(rec["n_moves"][e]))
+        for m in range(M):
+            if rec["info"][e, m, 2] != orc["mv"][r, m, 2] or not np.array_equal(_dense_counts(rec, e, m), orc["counts"][r, m]):
+                first[r] = m
+                break
+    return float((first >= 0).mean()), first
+
+
+def _net_prior_sampled_games_vs_oracle(E, N, n, sims, seed, base, stride, divergence=False):
     """n games x sims with the production forward (valid-only head) and the expand's prior branch,
     every stride-th game's predictions recorded: the oracle replays those games bit for bit
     (visit counts of every move, actions, counters, values, final boards), and the recorded
@@ -146,6 +163,14 @@ def _net_prior_sampled_games_vs_oracle(E, N, n, sims, seed, base, stride):
         assert np.array_equal(rec["values"][e, :M], orc["values"][r, :M])
         assert np.array_equal(rec["final"][e], orc["final"][r])
     assert check_recorded_priors(pi, v, cnt, leaves, sd, every=16) > 10000
+    if divergence:
+        frac, first = _divergence_vs_independent_f32(rec, pick, sd, sims, seed, base)
+        d = first[first >= 0]
+        print(f"\nindependent f32 predict (oracle MODE_MLP) vs the engine over {len(pick)} games x {sims} sims: "
+              f"{frac:.3f} of the games diverge; first diverging move: median "
+              f"{np.median(d) if len(d) else -1:.0f}, min {d.min() if len(d) else -1}, max {d.max() if len(d) else -1}; "
+              f"histogram by 8 moves {np.bincount(d // 8, minlength=6).tolist() if len(d) else []}")
+        st["divergence"] = (frac, first)
     eng.close()
     return st
 
@@ -154,7 +179,7 @@ def test_selfplay_net_prior_at_bench_size(Y):
     """Config 2 (4096 games x 100 sims, YachtNNet 256 x 6) exactly as bench.py runs it (one
     forward workgroup per 16-row tile), every 64th game replayed by the oracle."""
     _, E, N = Y
-    st = _net_prior_sampled_games_vs_oracle(E, N, 4096, 100, 2024, 0, 64)
+    st = _net_prior_sampled_games_vs_oracle(E, N, 4096, 100, 2024, 0, 64, divergence=True)
     assert st["forward_parts"] == 1
 
 

@@ -253,18 +253,20 @@ def test_dropout_rows_split_over_calls_equal_the_whole_batch(T, golden, amp):
     S = K.states_to_device(W)
     tg = torch.tensor(rng.randint(0, 3226, B), dtype=torch.int32, device="cuda")
     vv = torch.tensor(rng.rand(B) * 2 - 1, dtype=torch.float32, device="cuda")
-    whole = TR.Trainer(_sd(H, NB), H, NB, max_batch=B, dropout=0.3, seed=9, amp=amp)
+    # (amp: a small loss scale - 65536 / 32 rows would overflow fp16 gradients, a step GradScaler skips)
+    kw = dict(max_batch=B, dropout=0.3, seed=9, amp=amp, init_scale=256.0)
+    whole = TR.Trainer(_sd(H, NB), H, NB, **kw)
     whole.backward(S, tg, vv)
     g_whole = whole.grads().cpu().numpy().copy()
-    half = TR.Trainer(_sd(H, NB), H, NB, max_batch=B, dropout=0.3, seed=9, amp=amp)
+    half = TR.Trainer(_sd(H, NB), H, NB, **kw)
     acc = 0
     for k in range(2):
         idx = torch.arange(k * B // 2, (k + 1) * B // 2, dtype=torch.int32, device="cuda")
         half.backward(S, tg, vv, idx=idx, row0=k * B // 2)
         acc = acc + 0.5 * half.grads().cpu().numpy().astype(np.float64)
     # f32 (or fp16-rounded, amp) sums in another grouping
-    assert _relnorm(acc, g_whole) < (2e-3 if amp else 1e-5)
-    other = TR.Trainer(_sd(H, NB), H, NB, max_batch=B, dropout=0.3, seed=9, amp=amp)
+    assert _relnorm(acc, g_whole) < (2e-3 if amp else 1e-4)  # wrong masks would be O(1) off
+    other = TR.Trainer(_sd(H, NB), H, NB, **kw)
     other.backward(S, tg, vv, idx=torch.arange(B // 2, B, dtype=torch.int32, device="cuda"), row0=0)
     g_wrong = other.grads().cpu().numpy()
     half.backward(S, tg, vv, idx=torch.arange(B // 2, B, dtype=torch.int32, device="cuda"), row0=B // 2)
