@@ -172,6 +172,7 @@ class Coach:
             keys = ["t0", "selfplay", "save", "train", "arena", "gate"]
             self.phase_times = {k + "_s": t[k] - t[p] for p, k in zip(keys, keys[1:])}
             self.phase_times["iteration_s"] = t["gate"] - t["t0"]
+        self.wait_saves()
 
     def getCheckpointFile(self, iteration):
         return "checkpoint_" + str(iteration) + ".pth.tar"
@@ -179,7 +180,12 @@ class Coach:
     # ---- the replay buffer on disk (Coach.py:144-170): this framework's npz and, when asked
     # for (examples_format "reference" / "both"), the reference's pickle next to it
     def saveTrainExamples(self, iteration):
-        from .examples_io import save_examples, save_reference_examples
+        """Coach.py:144-152.  The npz's arrays are copied to the host here; the compressed write
+        runs on a background thread (joined before the next write, a load, and at the end of
+        learn), so the iteration's training does not wait for the disk."""
+        import threading
+
+        from .examples_io import examples_payload, save_reference_examples, write_examples
         folder = self.args.checkpoint
         os.makedirs(folder, exist_ok=True)
         base = os.path.join(folder, self.getCheckpointFile(iteration) + ".examples")
@@ -187,10 +193,21 @@ class Coach:
         if fmt in ("both", "reference"):
             save_reference_examples(base, self.trainExamplesHistory)
         if fmt in ("both", "npz"):
-            save_examples(base + ".npz", self.trainExamplesHistory)
+            payload = examples_payload(self.trainExamplesHistory)
+            self.wait_saves()
+            self._saver = threading.Thread(target=write_examples, args=(base + ".npz", payload))
+            self._saver.start()
+
+    def wait_saves(self):
+        """Join the background examples write, if one is running."""
+        t = getattr(self, "_saver", None)
+        if t is not None:
+            t.join()
+            self._saver = None
 
     def loadTrainExamples(self):
         from .examples_io import load_examples, load_reference_examples
+        self.wait_saves()
         modelFile = os.path.join(self.args.load_folder_file[0], self.args.load_folder_file[1])
         examplesFile = modelFile + ".examples"
         if os.path.isfile(examplesFile + ".npz"):

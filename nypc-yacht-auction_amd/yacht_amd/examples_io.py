@@ -28,6 +28,15 @@ from .state import ACTION_SIZE, PlayerState, YachtState, pack_many, unpack
 # ---------------------------------------------------------------- native format
 def save_examples(path: str, history) -> None:
     """history: list (iterations) of iterables of (YachtState, pi, v)."""
+    write_examples(path, examples_payload(history))
+
+
+def write_examples(path: str, payload: dict) -> None:
+    np.savez_compressed(path, **payload)
+
+
+def examples_payload(history) -> dict:
+    """The arrays save_examples writes (host copies: the history may change after this returns)."""
     from .replay import ExampleShard
     sizes, chunks, rows, cols, vals, values = [], [], [], [], [], []
     k = 0
@@ -41,7 +50,7 @@ def save_examples(path: str, history) -> None:
             cols.append(h["pi_cols"].astype(np.int16))
             vals.append(h["pi_vals"].astype(np.float64))
             chunks.append(np.asarray(h["states"], dtype=np.uint64).reshape(-1, 8))
-            values.extend(float(v) for v in h["values"])
+            values.append(np.asarray(h["values"], dtype=np.float64))
             k += n
             continue
         it = list(it)
@@ -54,14 +63,14 @@ def save_examples(path: str, history) -> None:
             rows.append(np.full(len(nz), k, dtype=np.int32))
             cols.append(nz.astype(np.int16))
             vals.append(p[nz])
-            values.append(float(v))
+            values.append(np.array([float(v)], dtype=np.float64))
             k += 1
-    np.savez_compressed(path, format=np.array("yacht_amd.examples.v1"), sizes=np.array(sizes, dtype=np.int64),
-                        states=np.concatenate(chunks) if chunks else np.zeros((0, 8), np.uint64),
-                        pi_rows=np.concatenate(rows) if rows else np.zeros(0, np.int32),
-                        pi_cols=np.concatenate(cols) if cols else np.zeros(0, np.int16),
-                        pi_vals=np.concatenate(vals) if vals else np.zeros(0),
-                        values=np.array(values, dtype=np.float64))
+    return dict(format=np.array("yacht_amd.examples.v1"), sizes=np.array(sizes, dtype=np.int64),
+                states=np.concatenate(chunks) if chunks else np.zeros((0, 8), np.uint64),
+                pi_rows=np.concatenate(rows) if rows else np.zeros(0, np.int32),
+                pi_cols=np.concatenate(cols) if cols else np.zeros(0, np.int16),
+                pi_vals=np.concatenate(vals) if vals else np.zeros(0),
+                values=np.concatenate(values) if values else np.zeros(0, np.float64))
 
 
 def load_examples(path: str, boards: bool = True):

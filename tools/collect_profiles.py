@@ -20,7 +20,7 @@ src, dst = os.path.join(REPO, "gpurun_out"), os.path.join(REPO, "profiles")
 cfg = {"envs": envs, "sims": sims, "hidden": 256, "nblocks": 6}
 cmd = (f"tools/profile_bench.sh {tag}: rocprofv3 --kernel-include-regex 'k_forward|k_expand_backup' --pmc "
        "FETCH_SIZE|WRITE_SIZE (separate passes) -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline "
-       "--no-arena --no-coach --no-shape --no-profile")
+       "--no-arena --no-coach --no-shape --no-f16 --no-train --no-profile")
 
 
 def copy(a, b):
@@ -44,7 +44,7 @@ if os.path.exists(summ):
         if kind is None:
             continue
         avg = next((x["avg_us"] for n, x in stats.items() if n == kname), None)
-        short = "k_forward<256>" if kind == "forward" else "k_expand_backup"
+        short = "k_forward<256, 2>" if kind == "forward" else "k_expand_backup"
         if "hbm_bytes_per_launch" in v:
             out = {"kernel": short, "config": cfg, "command": cmd, "launches": v["launches"],
                    "FETCH_SIZE_KiB_mean": v["FETCH_SIZE_KiB_mean"], "WRITE_SIZE_KiB_mean": v["WRITE_SIZE_KiB_mean"],
@@ -58,7 +58,7 @@ if os.path.exists(summ):
                    "command": f"tools/profile_bench.sh {tag}: rocprofv3 --kernel-include-regex k_forward --pmc "
                               "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE -- python3 "
                               "bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-arena --no-coach --no-shape "
-                              "--no-profile --no-train",
+                              "--no-f16 --no-train --no-profile",
                    "counters_mean_per_launch": {c: v[c + "_mean"] for c in ("SQ_VALU_MFMA_BUSY_CYCLES", "SQ_BUSY_CYCLES",
                                                                           "SQ_WAVE_CYCLES", "GRBM_GUI_ACTIVE")},
                    "busy_frac": v["mfma_busy_frac"],

@@ -4,7 +4,7 @@
 cd "$(dirname "$0")/.." || exit 2
 set -e
 mkdir -p /tmp/yk_diag
-for f in yk_env yk_net yk_engine yk_train yk_replay; do
+for f in yk_env yk_net yk_engine yk_train yk_train_amp yk_replay; do
   /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -fPIC -std=c++17 -ffp-contract=off -DYK_SEL_TIMING $YK_EXTRA \
      -Iinclude -Inypc-yacht-auction_amd/csrc -c nypc-yacht-auction_amd/csrc/$f.hip -o /tmp/yk_diag/$f.o
 done

@@ -8,13 +8,13 @@ export TMPDIR=/tmp
 tag=${1:-r01}
 out=gpurun_out/prof_$tag
 mkdir -p $out
-args="--steps 1 --warmup 1 --no-cpu-baseline --no-arena --no-coach --no-shape"
+args="--steps 1 --warmup 1 --no-cpu-baseline --no-arena --no-coach --no-shape --no-f16 --no-train"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/trace -o bench --output-format csv -- python3 bench.py $args > $out/bench_trace.json
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 400 rocprofv3 --kernel-include-regex 'k_forward|k_expand_backup' --pmc $c -d $out/$c -o $c --output-format csv -- python3 bench.py $args --no-profile > $out/bench_$c.json
 done
 # MFMA utilisation of k_forward: busy cycles of the matrix pipes against the kernel's cycles
 timeout -k 10 400 rocprofv3 --kernel-include-regex 'k_forward' --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE \
-  -d $out/MFMA -o MFMA --output-format csv -- python3 bench.py $args --no-profile --no-train > $out/bench_MFMA.json
+  -d $out/MFMA -o MFMA --output-format csv -- python3 bench.py $args --no-profile > $out/bench_MFMA.json
 python3 tools/summarize_prof.py $out > $out/summary.json
 cat $out/summary.json

@@ -10,7 +10,7 @@ src=nypc-yacht-auction_amd/csrc
 case $name in base*) src=ab_base/csrc ;; esac
 out=/tmp/yk_$name
 mkdir -p $out
-for f in yk_env yk_net yk_engine yk_train yk_replay; do
+for f in yk_env yk_net yk_engine yk_train yk_train_amp yk_replay; do
   [ -f $src/$f.hip ] || continue
   /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -fPIC -std=c++17 -ffp-contract=off -w "$@" \
      -Iinclude -I$src -c $src/$f.hip -o $out/$f.o &
