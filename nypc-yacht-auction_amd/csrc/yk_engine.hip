@@ -559,22 +559,11 @@ __device__ __forceinline__ void select_game(const EngDev& d, int e, int lane, co
         }
         // UCB argmax, MCTS.py:117-135: float32 arithmetic, strict '>' => lowest action wins
         const uint32_t Ns = nd.Ns;
-        float sq, sqe;
-#ifdef YK_SQRT_DIRECT
-        // the table's own expressions, evaluated here: no dependent load after the node record
-        // (f64 sqrt is correctly rounded, so these are the table's bits)
-        if (true) {
-            sq = (float)sqrt((double)Ns);
-            sqe = (float)sqrt((double)Ns + 1e-8);
-        } else
-#endif
-        if (Ns < (uint32_t)LUT_N) {
-            sq = d.lut_sq[Ns];
-            sqe = d.lut_sqe[Ns];
-        } else {
-            sq = (float)sqrt((double)Ns);
-            sqe = (float)sqrt((double)Ns + 1e-8);
-        }
+        // f32(sqrt(Ns)), f32(sqrt(Ns + 1e-8)) (MCTS.py:125-129 under NEP 50): f64 sqrt is correctly
+        // rounded, so these are the bits numpy gets; computed here rather than read from a table,
+        // which saves a dependent load per level (expand 53.35 -> 53.02 us, profiles/r03_expand_ab.log)
+        const float sq = (float)sqrt((double)Ns);
+        const float sqe = (float)sqrt((double)Ns + 1e-8);
         SEL_T0(t_sc);
         const float* P = Pbase + p_off;
         const uint16_t* S = Sbase + p_off;
@@ -703,20 +692,6 @@ __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int l
     const int t = tree_of(d, e);
     const int g = d.gen[t];
     PyV res{d.res_v[e], d.res_t[e]};
-#ifdef YK_BACKUP_HOIST
-    // The backup's reads do not depend on the expansion (the path holds existing nodes; the new
-    // node's record, slots and P are fresh storage), so the path entries and their edge slots are
-    // read first and resolve under the prior pass (the edges and Ns are read at the backup, in
-    // one round trip instead of three)
-    const int bdepth = d.path_len[e];
-    uint64_t b_pe = 0;
-    uint32_t b_sl = 0;
-    if (lane < bdepth) {
-        b_pe = d.path[(long)e * MAXD + lane];
-        b_sl = d.arenaS[(long)t * d.AE + (b_pe >> 32)];
-    }
-    const uint32_t b_ne0 = d.edge_count[g * d.T + t];
-#endif
     if (d.leaf_flag[e]) {
         SEL_T0(t_x0);
         const YkS s = ld_state(d.leaf_state + e);
@@ -763,39 +738,6 @@ __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int l
             // most two categories, a's and a + 2's (category starts are 202 + 252 c = 2 mod 4)
             static_assert(NBID % 4 == 2 && NCOMB % 4 == 0, "category starts are 2 mod 4");
             const bool score10 = valid.mode == 0 && valid.n >= 10;
-#ifdef YK_PRIOR_BATCH
-            // validity first (VALU only), then every group's load in flight at once - one round
-            // trip to the logits instead of one per group; a group with no valid action reads the
-            // row's first 16 bytes instead (one line, never used), so no load is conditional
-            uint64_t vb = 0;  // 4 validity bits per group
-#pragma unroll
-            for (int j = 0; j < PW_GMAX; j++) {
-                const int a = st + 8 * j + 4 * h;
-                uint32_t m;
-                if (score10) {
-                    const int b0 = a - NBID, b2 = a + 2 - NBID;
-                    const bool lo = j < G && b0 >= 0 && !((valid.used >> ((unsigned)b0 / NCOMB)) & 1u);
-                    const bool hi = j < G && b2 >= 0 && !((valid.used >> ((unsigned)b2 / NCOMB)) & 1u);
-                    m = (lo ? 3u : 0u) | (hi ? 12u : 0u);
-                } else {
-                    m = (j < G && valid(a) ? 1u : 0u) | (j < G && valid(a + 1) ? 2u : 0u) |
-                        (j < G && valid(a + 2) ? 4u : 0u) | (j < G && valid(a + 3) ? 8u : 0u);
-                }
-                vb |= (uint64_t)m << (4 * j);
-            }
-            float4 x4[PW_GMAX];
-#pragma unroll
-            for (int j = 0; j < PW_GMAX; j++) {
-                const int o = ((vb >> (4 * j)) & 0xFull) ? 8 * j + 4 * h : -st;
-                x4[j] = *reinterpret_cast<const float4*>(x + o);
-            }
-#pragma unroll
-            for (int j = 0; j < PW_GMAX; j++) {
-                const uint32_t m = (uint32_t)(vb >> (4 * j)) & 0xFu;
-                q[j] = make_float4((m & 1u) ? softmax_p(x4[j].x, mx, lse) : 0.f, (m & 2u) ? softmax_p(x4[j].y, mx, lse) : 0.f,
-                                   (m & 4u) ? softmax_p(x4[j].z, mx, lse) : 0.f, (m & 8u) ? softmax_p(x4[j].w, mx, lse) : 0.f);
-            }
-#else
 #pragma unroll
             for (int j = 0; j < PW_GMAX; j++) {
                 const int a = st + 8 * j + 4 * h;
@@ -817,7 +759,6 @@ __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int l
                 q[j] = make_float4(v0 ? softmax_p(x4.x, mx, lse) : 0.f, v1 ? softmax_p(x4.y, mx, lse) : 0.f,
                                    v2 ? softmax_p(x4.z, mx, lse) : 0.f, v3 ? softmax_p(x4.w, mx, lse) : 0.f);
             }
-#endif
 #pragma unroll
             for (int r = 0; r < PW_TMAX; r++)
                 qt[r] = (h == 0 && r < R && valid(st + 8 * G + r)) ? softmax_p(x[8 * G + r], mx, lse) : 0.f;
@@ -962,20 +903,11 @@ __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int l
     // ---- backup (MCTS.py:154-164): the path's nodes are distinct, so every level updates in
     // parallel; level k receives v * (-1)^(depth-1-k) ("return -v" per level).
     SEL_T0(t_bk);
-#ifdef YK_BACKUP_HOIST
-    const int depth = bdepth;
-#else
     const int depth = d.path_len[e];
-#endif
     if (depth > 0) {
         NodeRec* nodes = d.nodes[g] + (long)t * d.NCAP;
         Edge* edges = d.edges[g] + (long)t * d.ECAP;
         uint16_t* Sb = d.arenaS + (long)t * d.AE;
-#ifdef YK_BACKUP_HOIST
-        const uint32_t ne0 = b_ne0;
-        const uint64_t pe = b_pe;
-        const uint16_t sl = (uint16_t)b_sl;
-#else
         const uint64_t* path = d.path + (long)e * MAXD;
         const uint32_t ne0 = d.edge_count[g * d.T + t];
         uint64_t pe = 0;
@@ -984,44 +916,26 @@ __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int l
             pe = path[lane];
             sl = Sb[pe >> 32];
         }
-#endif
         const bool is_new = lane < depth && sl == 0;
         const uint64_t bal = __ballot(is_new);
         const uint32_t eid = ne0 + (uint32_t)__popcll(bal & ((1ull << lane) - 1));
         const uint32_t ne1 = ne0 + (uint32_t)__popcll(bal);
-#ifdef YK_BACKUP_HOIST
-        Edge b_ed{0.0, 0u, 0u};
-        uint32_t b_ns = 0;
-        if (lane < depth) {
-            b_ns = nodes[(uint32_t)pe].Ns;
-            if (sl) b_ed = edges[sl - 1];
-        }
-#endif
         if (lane < depth) {
             PyV v = res;
             if ((depth - 1 - lane) & 1) v.v = -v.v;
             if (sl) {
                 Edge& ed = edges[sl - 1];
-#ifdef YK_BACKUP_HOIST
-                const PyV q = pv_update(PyV{b_ed.Q, b_ed.tag}, b_ed.N, v);
-                ed = Edge{q.v, b_ed.N + 1, q.t};
-#else
                 const PyV q = pv_update(PyV{ed.Q, ed.tag}, ed.N, v);
                 ed.Q = q.v;
                 ed.tag = q.t;
                 ed.N += 1;
-#endif
             } else if (eid < (uint32_t)d.ECAP && eid < 65535u) {
                 edges[eid] = Edge{v.v, 1u, v.t};
                 Sb[pe >> 32] = (uint16_t)(eid + 1);
             } else {
                 atomicOr(d.err, ERR_EDGES);
             }
-#ifdef YK_BACKUP_HOIST
-            nodes[(uint32_t)pe].Ns = b_ns + 1;
-#else
             nodes[(uint32_t)pe].Ns += 1;
-#endif
         }
         if (lane == 0) {
             d.edge_count[g * d.T + t] = ne1;
