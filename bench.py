@@ -369,6 +369,8 @@ def main():
     ap.add_argument("--no-coach", action="store_true", help="skip the config-5 Coach-iteration legs")
     ap.add_argument("--no-shape", action="store_true", help="skip the config-3 shape leg (2048 x 200)")
     ap.add_argument("--no-f16", action="store_true", help="skip the fp16 predict-mode leg")
+    ap.add_argument("--coach-games", type=int, default=8192,
+                    help="games per GPU of the whole-iteration config-5 leg (config 5: 65,536 / 8 = 8192)")
     ap.add_argument("--dist-backend", default=None, help="nccl (RCCL, default on GPUs) or gloo (rehearsal)")
     ap.add_argument("--groups", type=int, default=0,
                     help="game groups on their own streams (0: the engine's auto choice)")
@@ -468,7 +470,7 @@ def main():
         img = last_gather[0] if world > 1 else eng.pack_records(stream=stream)
         coach = coach_leg(model, img, args.envs, 64, args.sims, world, seed=args.seed)
         del img
-        coach["iteration"] = coach_iter_leg(model, world, seed=args.seed)
+        coach["iteration"] = coach_iter_leg(model, world, games_per_gpu=args.coach_games, seed=args.seed)
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()
