@@ -250,12 +250,16 @@ def f16_leg(sd, envs=4096, sims=100, seed=0):
     return out
 
 
-def coach_iter_leg(model, world, games_per_gpu=8192, seed=0, amp=True):
+def coach_iter_leg(model, world, games_per_gpu=8192, seed=0, amp=True, warm=True):
     """Config 5 at its per-GPU shape: ONE whole Coach.learn iteration (Coach.py:74-139) with
     main.py's args (main.py:17-43: 25 sims, tempThreshold 15, maxlenOfQueue 200,000, 15 epochs of
     batch 512, dropout 0.3, arenaCompare 10, updateThreshold 0.55) over numEps = games_per_gpu x
     N games sharded over the N ranks (65,536 on 8 GPUs = config 5), the reference's GPU train
-    path (autocast + GradScaler: the amp trainer) unless amp=False.  Per-phase wall times."""
+    path (autocast + GradScaler: the amp trainer) unless amp=False.  Per-phase wall times of a
+    steady-state iteration: warm=True first runs a 512-game iteration untimed (the first torch.save
+    / zipfile / allocator use of the process cost about 1.5 s once, profiles/r03c_coach_profile.log)."""
+    if warm:
+        coach_iter_leg(model, world, games_per_gpu=min(512, games_per_gpu), seed=seed + 1, amp=amp, warm=False)
     import shutil
     import tempfile
 

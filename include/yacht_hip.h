@@ -224,6 +224,17 @@ int yk_engine_pack_records(yk_engine_t* eng, void* dst, int64_t capacity, void* 
 int yk_examples_from_records(const void* images, int n_images, int n_envs, int max_moves, int sims,
                              int64_t n_games, int64_t skip, int64_t capacity, yk_state_t* states, int32_t* targets,
                              float* values, int64_t* n_examples, void* stream);
+/* The full policies of the same examples (Coach.py:57-61: MCTS.getActionProb's pi, MCTS.py:44-54 -
+ * one-hot at the played action at temp 0, N / sum N at temp 1) as a sparse CSR of their nonzero
+ * entries, for the examples file (Coach.py:144-151) and code that iterates the reference's tuples.
+ * Examples skip .. skip + n_examples - 1 (as yk_examples_from_records numbers them; n_examples <=
+ * the examples after skip).  DEVICE pi_indptr[n_examples + 1] (always written: example k's entries
+ * are pi_indptr[k] .. pi_indptr[k+1]-1), pi_cols[nnz] (actions, ascending), pi_vals[nnz] (float64),
+ * values[n_examples] (float64 v, may be NULL).  pi_cols = NULL: count only.  HOST *nnz = the
+ * entries (YK_ERR_CAPACITY if more than nnz_capacity).  Synchronises `stream`. */
+int yk_examples_policies(const void* images, int n_images, int n_envs, int max_moves, int sims, int64_t n_games,
+                         int64_t skip, int64_t n_examples, int64_t* pi_indptr, int32_t* pi_cols, double* pi_vals,
+                         int64_t nnz_capacity, double* values, int64_t* nnz, void* stream);
 
 /* ---------------------------------------------------------------- Arena
  * Batched Arena.playGame (Arena.py:30-93), n_envs games in lock-step: `agent` in seat

@@ -92,6 +92,7 @@ SIGNATURES = {
     "yk_mcts_search": [P, P, U64, P, P, I, P, P],
     "yk_mcts_reset": [P],
     "yk_examples_from_records": [P, I, I, I, I, C.c_int64, C.c_int64, C.c_int64, P, P, P, P, P],
+    "yk_examples_policies": [P, I, I, I, I, C.c_int64, C.c_int64, C.c_int64, P, P, P, C.c_int64, P, P, P],
 }
 _RESTYPE = {"yk_version": C.c_char_p, "yk_rng_draw64": C.c_uint64, "yk_engine_record_bytes": C.c_int64,
             "yk_trainer_step_count": C.c_int64}

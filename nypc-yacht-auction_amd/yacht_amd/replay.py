@@ -5,9 +5,9 @@ iteration.  At config 5's scale (65536 games x 48 moves per iteration) those Pyt
 not fit (a dense pi is 3226 floats), and NNetWrapper.train only uses ``argmax(pi)`` of them
 (NNet.py:145-146).  So an iteration's examples are an ``ExampleShard``: device arrays of
 packed boards (64 B), argmax targets and float32 values, built by ``yk_examples_from_records``
-straight from the (all-gathered) trajectory record images.  The record image stays on the
-device as the shard's source, so the full visit policies - for the examples file
-(Coach.py:144-151) or for code that iterates the reference's tuples - are recovered on demand.
+straight from the (all-gathered) trajectory record images, plus the full visit policies as a
+device CSR (``yk_examples_policies``) for the examples file (Coach.py:144-151) and for code that
+iterates the reference's tuples.  The record images are not kept.
 """
 from __future__ import annotations
 
@@ -28,45 +28,30 @@ def _vcap(max_moves: int, sims: int) -> int:
 class ExampleShard:
     """One iteration's examples (``iterationTrainExamples``, Coach.py:86-90) on the device:
     ``states`` int64[n, 8] (packed canonical boards), ``targets`` int32[n] (argmax pi),
-    ``values`` float32[n].  ``len`` and iteration behave like the reference's deque of
-    ``(YachtState, pi list, v)`` tuples (built lazily from the record images)."""
+    ``values`` float32[n], and - when built from record images - ``policies``: the full visit
+    policies as a device CSR (``pi_indptr`` int64[n+1], ``pi_cols`` int32, ``pi_vals`` float64,
+    ``values64`` float64[n]; yk_examples_policies).  ``len`` and iteration behave like the
+    reference's deque of ``(YachtState, pi list, v)`` tuples."""
 
-    def __init__(self, states, targets, values, source=None):
+    def __init__(self, states, targets, values, policies=None):
         self.states, self.targets, self.values = states, targets, values
-        self._source = source  # (images u8 [R, nbytes] device, n_envs, max_moves, sims, n_games, skip)
+        self.policies = policies
         self._host = None
 
     def __len__(self):
         return int(self.targets.numel())
 
     def host(self) -> dict:
-        """Host arrays of the shard with the full policies (sparse CSR, float64 as
-        MCTS.getActionProb returns them): states u64[n, 8], pi_indptr i64[n+1], pi_cols i32,
-        pi_vals f64, values f64[n], targets i32[n].  Built once: only the rank images holding
-        the kept tail of the deque are copied to the host, and the device images are released
-        afterwards (the shard keeps its compact device examples and these host arrays)."""
+        """Host arrays of the shard with the full policies (float64 as MCTS.getActionProb returns
+        them): states u64[n, 8], pi_indptr i64[n+1], pi_cols i32, pi_vals f64, values f64[n],
+        targets i32[n].  One device-to-host copy of the compact arrays, cached."""
         if self._host is None:
-            if self._source is None:
-                raise ValueError("this shard has no record images to rebuild policies from")
-            images, E, M, sims, n_games, skip = self._source
-            R = images.shape[0]
-            total_games = R * E if n_games is None or n_games < 0 else min(n_games, R * E)
-            # examples per rank image (from the images' move counts), so the images entirely before
-            # the kept tail are never copied
-            L = record_layout(E, M, sims)
-            nm_off, nm_bytes = L["n_moves"]
-            per = []
-            for r in range(R):
-                g = min(max(total_games - r * E, 0), E)
-                nm = images[r, nm_off:nm_off + nm_bytes].view(torch.int32)[:g] if g else None
-                per.append(int(nm.clamp(0, M).sum().item()) if g else 0)
-            r0, before = 0, 0
-            while r0 < R - 1 and before + per[r0] <= skip:
-                before += per[r0]
-                r0 += 1
-            h = host_examples(images[r0:].cpu().numpy(), E, M, sims, total_games - r0 * E)
-            self._host = _tail(h, skip - before, len(self))
-            self._source = None
+            if self.policies is None:
+                raise ValueError("this shard was not built from record images: it has no policies")
+            P = self.policies
+            self._host = dict(states=self.states.cpu().numpy().view(np.uint64), values=P["values64"].cpu().numpy(),
+                              targets=self.targets.cpu().numpy(), pi_indptr=P["pi_indptr"].cpu().numpy(),
+                              pi_cols=P["pi_cols"].cpu().numpy(), pi_vals=P["pi_vals"].cpu().numpy())
         return self._host
 
     def __iter__(self):
@@ -94,7 +79,8 @@ def examples_from_images(images: torch.Tensor, n_envs: int, max_moves: int, sims
                          maxlen: int = None, stream=None) -> ExampleShard:
     """Record images (device uint8 [R, nbytes]: every rank's yk_engine_pack_records after the
     all-gather) -> ExampleShard of the first n_games games, keeping the last `maxlen` examples
-    (the maxlenOfQueue deque, Coach.py:86-90)."""
+    (the maxlenOfQueue deque, Coach.py:86-90).  The shard holds only compact arrays (examples and
+    the policies' CSR, about a third of the images' bytes); the images can be released."""
     imgs = images.reshape(images.shape[0] if images.dim() > 1 else 1, -1).contiguous()
     R = imgs.shape[0]
     cnt = C.c_int64()
@@ -111,20 +97,18 @@ def examples_from_images(images: torch.Tensor, n_envs: int, max_moves: int, sims
          states.data_ptr(), targets.data_ptr(), values.data_ptr(), C.byref(cnt), sp)
     if int(cnt.value) != n:
         raise RuntimeError(f"yk_examples_from_records wrote {cnt.value} examples, expected {n}")
-    return ExampleShard(states[:n], targets[:n], values[:n], source=(imgs, n_envs, max_moves, sims, n_games, skip))
-
-
-def record_layout(n_envs: int, max_moves: int, sims: int) -> dict:
-    """(byte offset, bytes) of each part of one rank's record image (yk_engine_pack_records)."""
-    E, M = n_envs, max_moves
-    vcap = _vcap(M, sims)
-    parts = [("states", 8 * E * M * 8), ("info", 4 * E * M * 8), ("ctr", 8 * E * M * 2), ("values", 8 * E * M),
-             ("visits_raw", 4 * E * vcap), ("voff", 4 * E * (M + 1)), ("n_moves", 4 * E), ("final", 8 * E * 8)]
-    out, off = {}, 0
-    for name, nb in parts:
-        out[name] = (off, nb)
-        off += (nb + 15) & ~15
-    return out
+    indptr = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+    nnz = C.c_int64()
+    call("yk_examples_policies", imgs.data_ptr(), R, n_envs, max_moves, sims, n_games, skip, n, indptr.data_ptr(),
+         None, None, 0, None, C.byref(nnz), sp)
+    k = int(nnz.value)
+    cols = torch.empty(max(k, 1), dtype=torch.int32, device="cuda")
+    vals = torch.empty(max(k, 1), dtype=torch.float64, device="cuda")
+    v64 = torch.empty(max(n, 1), dtype=torch.float64, device="cuda")
+    call("yk_examples_policies", imgs.data_ptr(), R, n_envs, max_moves, sims, n_games, skip, n, indptr.data_ptr(),
+         cols.data_ptr(), vals.data_ptr(), k, v64.data_ptr(), C.byref(nnz), sp)
+    pol = dict(pi_indptr=indptr, pi_cols=cols[:k], pi_vals=vals[:k], values64=v64[:n])
+    return ExampleShard(states[:n], targets[:n], values[:n], policies=pol)
 
 
 # ---------------------------------------------------------------- host side (numpy)
@@ -132,7 +116,8 @@ def host_examples(images: np.ndarray, n_envs: int, max_moves: int, sims: int, n_
     """The same examples from host copies of the record images, with the full policies
     (Coach.py:57-61: MCTS.getActionProb's pi per move - one-hot at the played action at temp 0,
     N / sum(N) at temp 1, MCTS.py:44-54) as a sparse CSR.  Used for the examples file and as an
-    independent restatement of yk_examples_from_records in tests."""
+    independent restatement of yk_examples_from_records / yk_examples_policies (tests, the 2-rank
+    CPU rehearsal).  Not on the product path."""
     imgs = np.ascontiguousarray(images).reshape(images.shape[0] if images.ndim > 1 else 1, -1)
     total_games = imgs.shape[0] * n_envs
     n_games = total_games if n_games is None or n_games < 0 else min(n_games, total_games)
@@ -186,15 +171,6 @@ def host_examples(images: np.ndarray, n_envs: int, max_moves: int, sims: int, n_
                 pi_indptr=np.concatenate([[0], np.cumsum(lens)]).astype(np.int64),
                 pi_cols=cat["cols"] if n else np.zeros(0, np.int32),
                 pi_vals=cat["vals"] if n else np.zeros(0))
-
-
-def _tail(h: dict, skip: int, n: int) -> dict:
-    """Examples skip .. skip+n of host_examples' output."""
-    ip = h["pi_indptr"]
-    a0, a1 = int(ip[skip]), int(ip[skip + n])
-    return dict(states=h["states"][skip:skip + n], values=h["values"][skip:skip + n],
-                targets=h["targets"][skip:skip + n], pi_indptr=ip[skip:skip + n + 1] - a0,
-                pi_cols=h["pi_cols"][a0:a1], pi_vals=h["pi_vals"][a0:a1])
 
 
 # ---------------------------------------------------------------- what NNetWrapper.train takes

@@ -82,6 +82,20 @@ def test_examples_kernel_matches_host_restatements(Y):
     assert torch.equal(tail.targets, shard.targets[-1000:]) and torch.equal(tail.states, shard.states[-1000:])
     part = R.examples_from_images(img, n, 48, sims, n_games=7)
     assert len(part) == 7 * 48 and torch.equal(part.targets, shard.targets[:7 * 48])
+    # the device policy CSR (yk_examples_policies) is the host restatement's, bit for bit, for the
+    # whole batch and for a maxlen tail
+    def _same_csr(got, want, skip=0):
+        n = len(got["targets"])
+        ip = want["pi_indptr"]
+        a0, a1 = int(ip[skip]), int(ip[skip + n])
+        assert np.array_equal(got["pi_indptr"], ip[skip:skip + n + 1] - a0)
+        assert np.array_equal(got["pi_cols"], want["pi_cols"][a0:a1])
+        assert np.array_equal(got["pi_vals"], want["pi_vals"][a0:a1])
+        assert np.array_equal(got["values"], want["values"][skip:skip + n])
+        assert np.array_equal(got["states"], want["states"][skip:skip + n])
+    _same_csr(shard.host(), h)
+    _same_csr(tail.host(), h, skip=len(ref) - 1000)
+    _same_csr(part.host(), h)
     # lazy reference tuples of a shard
     b, pi, v = tail[0]
     assert pi == ref[len(ref) - 1000][1] and v == ref[len(ref) - 1000][2]
@@ -200,10 +214,14 @@ def test_coach_iteration_two_ranks_sharing_gpu0(Y, tmp_path):
     a = np.concatenate([pr0[0][k].reshape(-1) for k in pr0[0]]).astype(np.float64)
     b = np.concatenate([wide.nnet.state_dict()[k].numpy().reshape(-1) for k in pr0[0]]).astype(np.float64)
     assert np.linalg.norm(a - b) / np.linalg.norm(b) < 1e-4 and (np.abs(a - b) > 1e-5).mean() < 1e-3
-    # the sharded gating arena's tally is the single-GPU arena's
-    pit = GatingArena(game, net0, coach.nnet, args).playGames(args.arenaCompare, env_base=900)
+    # the sharded gating arena's tally is the single-GPU arena's on the same two nets: the
+    # ranks' previous net (the initial weights, net0) against their DDP-trained p0
+    newnet = NNetWrapper(game, args)
+    newnet.nnet.load_state_dict({k: torch.from_numpy(v) for k, v in p0.items()})
+    pit = GatingArena(game, net0, newnet, args).playGames(args.arenaCompare, env_base=900)
     assert out["pit0"] == out["pit1"]
-    assert sum(out["pit0"]) == 6 and sum(pit) == 6
+    assert sum(out["pit0"]) == 6
+    assert tuple(pit) == tuple(out["pit0"])
     # Coach.learn on two ranks: same verdict, examples and parameters on both
     l0, l1 = out["learn0"], out["learn1"]
     assert l0[0] == l1[0] and l0[1] == l1[1] == 6 * 48
