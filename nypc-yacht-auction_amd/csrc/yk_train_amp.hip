@@ -1125,8 +1125,10 @@ struct PackJob {
 };
 // scaler.update (block 0, thread 0; GradScaler('cuda') defaults: growth 2, backoff 0.5) and the
 // fp16 weight copies for the next step
-__global__ void k_amp_pack(const PackJob* __restrict__ jobs, int njobs, long total, Scaler* sc,
-                           const double* __restrict__ part, int update) {
+// blk_job[b]: the job of block b (every job's item count is a multiple of the block size, so a
+// block lies in one job; checked in amp_create)
+__global__ void k_amp_pack(const PackJob* __restrict__ jobs, const uint8_t* __restrict__ blk_job, long total,
+                           Scaler* sc, const double* __restrict__ part, int update) {
     const double t = (update && blockIdx.x == 0) ? sq_total(part) : 0.0;
     if (update && blockIdx.x == 0 && threadIdx.x == 0) {
         if (!isfinite(t)) {
@@ -1144,9 +1146,7 @@ __global__ void k_amp_pack(const PackJob* __restrict__ jobs, int njobs, long tot
     }
     const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= total) return;
-    int j = 0;
-    while (j + 1 < njobs && jobs[j + 1].first <= i) j++;
-    const PackJob jb = jobs[j];
+    const PackJob jb = jobs[blk_job[blockIdx.x]];
     const long e = i - jb.first;
     const int KS = jb.Kp / 32;
     const int lane = (int)(e % 64);
@@ -1187,6 +1187,7 @@ struct AmpTrain {
     int2* vs_items = nullptr;
     int n_vs_items = 0;
     PackJob* pk_jobs = nullptr;
+    uint8_t* pk_blk = nullptr;  // per pack block: its job
     int n_pk_jobs = 0;
     long pk_total = 0;
     double* sqpart = nullptr;
@@ -1361,9 +1362,18 @@ int amp_create(AmpTrain** out, int H, int NB, int Bmax, float* P, float* G, cons
     pack(P + off[t_head(NB, HV_W1)], wv1t, VH, H, H, VH, 1);
     a->n_pk_jobs = (int)pj.size();
     a->pk_total = first;
+    std::vector<uint8_t> pblk;
+    for (size_t j = 0; j < pj.size(); j++) {
+        const long n = (j + 1 < pj.size() ? pj[j + 1].first : first) - pj[j].first;
+        if (n % 256 != 0 || pj.size() > 255) {  // a block would straddle two jobs
+            amp_destroy(a);
+            return YK_ERR_ARG;
+        }
+        pblk.insert(pblk.end(), (size_t)(n / 256), (uint8_t)j);
+    }
     if (aalloc(a, &a->dw_jobs, jobs.size()) || aalloc(a, &a->dw_items, items.size()) ||
         aalloc(a, &a->vs_jobs, vj.size()) || aalloc(a, &a->vs_items, vitems.size()) ||
-        aalloc(a, &a->pk_jobs, pj.size())) {
+        aalloc(a, &a->pk_jobs, pj.size()) || aalloc(a, &a->pk_blk, pblk.size())) {
         amp_destroy(a);
         return YK_ERR_NOMEM;
     }
@@ -1371,6 +1381,7 @@ int amp_create(AmpTrain** out, int H, int NB, int Bmax, float* P, float* G, cons
     YK_HIP(hipMemcpy(a->dw_items, items.data(), sizeof(int4) * items.size(), hipMemcpyHostToDevice));
     YK_HIP(hipMemcpy(a->vs_items, vitems.data(), sizeof(int2) * vitems.size(), hipMemcpyHostToDevice));
     YK_HIP(hipMemcpy(a->pk_jobs, pj.data(), sizeof(PackJob) * pj.size(), hipMemcpyHostToDevice));
+    YK_HIP(hipMemcpy(a->pk_blk, pblk.data(), pblk.size(), hipMemcpyHostToDevice));
     // the loss-sum job's buffers are the trainer's; amp_backward patches them in on first use
     YK_HIP(hipMemcpy(a->vs_jobs, vj.data(), sizeof(VsJob) * vj.size(), hipMemcpyHostToDevice));
     a->lsum_src_dummy = nullptr;
@@ -1387,7 +1398,7 @@ void amp_destroy(AmpTrain* a) {
 
 int amp_pack(AmpTrain* a, hipStream_t s) {
     hipLaunchKernelGGL(k_amp_pack, dim3((unsigned)((a->pk_total + 255) / 256)), dim3(256), 0, s, a->pk_jobs,
-                       a->n_pk_jobs, a->pk_total, a->sc, a->sqpart, 0);
+                       a->pk_blk, a->pk_total, a->sc, a->sqpart, 0);
     YK_LAUNCHED();
     return YK_OK;
 }
@@ -1444,7 +1455,7 @@ int amp_apply(AmpTrain* a, long nparams, float* M, float* V, double* sq_out, flo
                        a->sqpart, sq_out, a->sc, max_norm, lr, wd, b1, b2, eps);
     YK_LAUNCHED();
     hipLaunchKernelGGL(k_amp_pack, dim3((unsigned)((a->pk_total + 255) / 256)), dim3(256), 0, s, a->pk_jobs,
-                       a->n_pk_jobs, a->pk_total, a->sc, a->sqpart, 1);
+                       a->pk_blk, a->pk_total, a->sc, a->sqpart, 1);
     YK_LAUNCHED();
     return YK_OK;
 }
