@@ -493,6 +493,14 @@ __device__ unsigned long long g_sel[16384 * 16];
 #define SEL_T0(v)
 #define SEL_ACC(k, t0)
 #endif
+// Diagnostic builds only (-DYK_XSPAN, tools/diag_xspan.py): for 16 sampled k_expand_backup launches,
+// per game: start, end of expand + backup, end, the expanded node's valid count, descent levels, and
+// the wave's hardware ids - how a launch's time relates to its games' own times.
+#ifdef YK_XSPAN
+constexpr int XS_SAMPLES = 16, XS_GAMES = 4096;
+__device__ unsigned long long g_xs[XS_SAMPLES][XS_GAMES][8];
+__device__ int g_xs_slot = -1;
+#endif
 
 // One simulation's descent (MCTS.search, MCTS.py:56-152 up to the recursion).
 // All 64 lanes of the game's wave call it together.
@@ -678,7 +686,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(YK_EXPAND_W
 #ifdef YK_SEL_TIMING
     const unsigned long long t_ex = __builtin_amdgcn_s_memtime();
 #endif
+#ifdef YK_XSPAN
+    const int xs = g_xs_slot;
+    const unsigned long long xs0 = __builtin_amdgcn_s_memtime(), xr0 = __builtin_amdgcn_s_memrealtime();
+    const uint32_t xs_v = d.leaf_flag[e] ? (uint32_t)valid_info(ld_state(d.leaf_state + e), 1).V : 0xFFFFFFFFu;
+#endif
     expand_backup_game(d, e, lane);
+#ifdef YK_XSPAN
+    const unsigned long long xs1 = __builtin_amdgcn_s_memtime();
+#endif
 #ifdef YK_SEL_TIMING
     if (lane == 0) g_sel[(long)e * 16 + 6] += __builtin_amdgcn_s_memtime() - t_ex;
 #endif
@@ -686,6 +702,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(YK_EXPAND_W
         wave_sync();  // this wave's backup writes (edges, slots, Ns) precede its descent's reads
         select_game(d, e, lane, env_ids, ctr_arr);
     }
+#ifdef YK_XSPAN
+    if (xs >= 0 && xs < XS_SAMPLES && e < XS_GAMES && lane == 0) {
+        const unsigned long long xs2 = __builtin_amdgcn_s_memtime(), xr2 = __builtin_amdgcn_s_memrealtime();
+        const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID
+        const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
+        unsigned long long* o = g_xs[xs][e];
+        o[0] = xs0;
+        o[1] = xs1;
+        o[2] = xs2;
+        o[3] = xs_v;
+        o[4] = d.path_len[e];
+        o[5] = ((unsigned long long)xcc << 32) | hw;
+        o[6] = xr0;  // s_memrealtime (100 MHz, one clock for the device): the launch's span
+        o[7] = xr2;
+    }
+#endif
 }
 
 __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int lane) {
@@ -1313,6 +1345,15 @@ int run_sims(yk_engine* eng, int G, const hipStream_t* st, int sims, const uint3
 #endif
             }
             if (timed) prof_mark(eng, g, KC_EXPAND, st[g]);
+#ifdef YK_XSPAN
+            {
+                static long xs_launch = 0;
+                const long q = xs_launch++;
+                const int slot = (q % 300 == 150 && q / 300 < XS_SAMPLES) ? (int)(q / 300) : -1;
+                YK_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_xs_slot), &slot, sizeof(int), 0, hipMemcpyHostToDevice, st[g]));
+                YK_HIP(hipStreamSynchronize(st[g]));  // the host value must outlive the copy
+            }
+#endif
             hipLaunchKernelGGL(k_expand_backup, game_grid(d), bb, 0, st[g], d, k + 1 < sims ? 1 : 0, env_ids, ctr);
             YK_LAUNCHED();
             if (timed && eng->prof_stride > 1) prof_mark(eng, g, -1, st[g]);  // untimed sims follow
@@ -1325,6 +1366,13 @@ int run_sims(yk_engine* eng, int G, const hipStream_t* st, int sims, const uint3
 
 extern "C" {
 
+#ifdef YK_XSPAN
+int yk_diag_xspan(uint64_t* out) {  // HOST out[16][4096][8]
+    YK_HIP(hipDeviceSynchronize());
+    YK_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_xs), sizeof(uint64_t) * XS_SAMPLES * XS_GAMES * 8));
+    return YK_OK;
+}
+#endif
 #ifdef YK_SEL_TIMING
 int yk_diag_select(uint64_t* out, int n) {  // HOST out[n][16]; resets the accumulators
     YK_HIP(hipDeviceSynchronize());
