@@ -37,6 +37,7 @@ def lib():
         _lib.or_net_create.restype = C.c_void_p
         _lib.or_net_create.argtypes = [C.c_int, C.c_int, C.POINTER(C.c_void_p)]
         _lib.or_net_destroy.argtypes = [C.c_void_p]
+        _lib.or_net_set_order.argtypes = [C.c_void_p, C.c_int]
         _lib.or_net_predict.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
         _lib.or_net_forward_x.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
         _lib.or_draw64.restype = C.c_uint64
@@ -172,10 +173,14 @@ def pairwise_sum(a):
 class Net:
     """C restatement of YachtNNet.forward + exp(log_softmax) (NNet.py:177-195)."""
 
-    def __init__(self, state_dict, hidden, nblocks):
+    def __init__(self, state_dict, hidden, nblocks, reverse_sums=False):
+        """reverse_sums: every Linear adds its inputs last to first - another valid float32
+        evaluation order, for measuring how much float32 rounding alone changes a search."""
         self._keep = [np.ascontiguousarray(np.asarray(v, dtype=np.float32)) for v in state_dict.values()]
         arr = (C.c_void_p * len(self._keep))(*[a.ctypes.data for a in self._keep])
         self.h = lib().or_net_create(hidden, nblocks, arr)
+        if reverse_sums:
+            lib().or_net_set_order(C.c_void_p(self.h), 1)
         self.hidden, self.nblocks = hidden, nblocks
 
     def predict_states(self, states):

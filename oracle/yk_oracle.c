@@ -393,6 +393,7 @@ float or_pairwise_sum(const float* a, long n) { return pw_sum(a, n); }
  * transposed ([in][out]) so the f32 loops vectorise without reassociation. */
 typedef struct {
     int H, NB;
+    int rev; /* 1: every Linear sums its inputs last to first - another valid f32 order (tests only) */
     float *w_in, *b_in, *g_in, *be_in;                       /* [59][H] */
     float **w1, **b1, **g1, **be1, **w2, **b2, **g2, **be2;  /* per block [H][H] */
     float *g_pi, *be_pi, *w_pi, *b_pi;                        /* w_pi [H][3226] */
@@ -434,6 +435,7 @@ void* or_net_create(int H, int NB, const float* const* p) {
     n->w_v2 = dup(p[k++], 128); n->b_v2 = dup(p[k++], 1);
     return n;
 }
+void or_net_set_order(void* h, int rev) { ((net_t*)h)->rev = rev ? 1 : 0; }
 void or_net_destroy(void* h) {
     net_t* n = (net_t*)h;
     if (!n) return;
@@ -447,9 +449,10 @@ void or_net_destroy(void* h) {
     free(n->g_v); free(n->be_v); free(n->w_v1); free(n->b_v1); free(n->w_v2); free(n->b_v2);
     free(n);
 }
-static void linear(const float* wt, const float* b, const float* x, int in, int out, float* y) {
+static void linear(const float* wt, const float* b, const float* x, int in, int out, float* y, int rev) {
     for (int o = 0; o < out; o++) y[o] = 0.0f;
-    for (int i = 0; i < in; i++) {
+    for (int k = 0; k < in; k++) {
+        const int i = rev ? in - 1 - k : k;
         const float xi = x[i];
         const float* row = wt + (size_t)i * out;
         for (int o = 0; o < out; o++) y[o] += row[o] * xi;
@@ -470,14 +473,14 @@ static inline float silu(float x) { return x / (1.0f + expf(-x)); }
 static void net_forward(const net_t* n, const float* x, float* pi, float* v) {
     int H = n->H;
     float h[1024], t[1024], u[1024];
-    linear(n->w_in, n->b_in, x, FEAT, H, h);
+    linear(n->w_in, n->b_in, x, FEAT, H, h, n->rev);
     layernorm(h, H, n->g_in, n->be_in);
     for (int i = 0; i < H; i++) h[i] = silu(h[i]);
     for (int b = 0; b < n->NB; b++) {
-        linear(n->w1[b], n->b1[b], h, H, H, t);
+        linear(n->w1[b], n->b1[b], h, H, H, t, n->rev);
         for (int i = 0; i < H; i++) t[i] = silu(t[i]);
         layernorm(t, H, n->g1[b], n->be1[b]);
-        linear(n->w2[b], n->b2[b], t, H, H, u);
+        linear(n->w2[b], n->b2[b], t, H, H, u, n->rev);
         for (int i = 0; i < H; i++) u[i] = silu(u[i]);
         layernorm(u, H, n->g2[b], n->be2[b]);
         for (int i = 0; i < H; i++) h[i] += u[i];
@@ -485,11 +488,11 @@ static void net_forward(const net_t* n, const float* x, float* pi, float* v) {
     memcpy(t, h, sizeof(float) * H);
     layernorm(t, H, n->g_pi, n->be_pi);
     for (int i = 0; i < H; i++) t[i] = silu(t[i]);
-    linear(n->w_pi, n->b_pi, t, H, ASIZE, pi);
+    linear(n->w_pi, n->b_pi, t, H, ASIZE, pi, n->rev);
     memcpy(t, h, sizeof(float) * H);
     layernorm(t, H, n->g_v, n->be_v);
     for (int i = 0; i < H; i++) t[i] = silu(t[i]);
-    linear(n->w_v1, n->b_v1, t, H, 128, u);
+    linear(n->w_v1, n->b_v1, t, H, 128, u, n->rev);
     double acc = n->b_v2[0];
     for (int i = 0; i < 128; i++) acc += (double)n->w_v2[i] * silu(u[i]);
     *v = tanhf((float)acc);

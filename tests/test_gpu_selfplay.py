@@ -116,21 +116,38 @@ def test_selfplay_net_prior_replayed_by_oracle(Y):
     assert check_recorded_priors(pi, v, cnt, leaves, sd) == int(cnt.sum())
 
 
+def _first_divergence(a_moves, a_counts, b_moves, b_counts, n):
+    """First move where two plays of game r differ (action or visit counts), or -1."""
+    first = np.full(n, -1)
+    for r in range(n):
+        for m in range(min(len(a_moves[r]), len(b_moves[r]))):
+            if a_moves[r][m] != b_moves[r][m] or not np.array_equal(a_counts(r, m), b_counts(r, m)):
+                first[r] = m
+                break
+    return first
+
+
 def _divergence_vs_independent_f32(rec, pick, sd, sims, seed, base):
     """How often the search outcome of an independently computed f32 predict differs: the oracle
     plays the sampled games with its own float32 YachtNNet (C, the reference's CPU arithmetic,
     MODE_MLP, no replay), and each game is compared move by move with the engine's (action and
-    visit counts).  Returns (fraction of games that diverge, first diverging move per game or -1)."""
+    visit counts).  The same comparison between the oracle and itself with every Linear summed in
+    the reverse order (two valid float32 evaluations) is the rate float32 rounding alone gives.
+    Returns (fraction of games that diverge, first diverging move per game or -1, the f32-vs-f32
+    fraction, its first diverging moves)."""
     orc = O.selfplay(base + pick, seed, sims, 1.5, 15, O.MODE_MLP, net=O.Net(sd, 256, 6), max_moves=48, threads=16)
     assert orc["nerr"] == 0
-    first = np.full(len(pick), -1)
-    for r, e in enumerate(pick):
-        M = min(int(orc["stats"][r, 0]), int(rec["n_moves"][e]))
-        for m in range(M):
-            if rec["info"][e, m, 2] != orc["mv"][r, m, 2] or not np.array_equal(_dense_counts(rec, e, m), orc["counts"][r, m]):
-                first[r] = m
-                break
-    return float((first >= 0).mean()), first
+    rev = O.selfplay(base + pick, seed, sims, 1.5, 15, O.MODE_MLP, net=O.Net(sd, 256, 6, reverse_sums=True),
+                     max_moves=48, threads=16)
+    assert rev["nerr"] == 0
+    n = len(pick)
+    eng_mv = [rec["info"][e, :int(rec["n_moves"][e]), 2] for e in pick]
+    orc_mv = [orc["mv"][r, :int(orc["stats"][r, 0]), 2] for r in range(n)]
+    rev_mv = [rev["mv"][r, :int(rev["stats"][r, 0]), 2] for r in range(n)]
+    first = _first_divergence(eng_mv, lambda r, m: _dense_counts(rec, pick[r], m), orc_mv,
+                              lambda r, m: orc["counts"][r, m], n)
+    first_ff = _first_divergence(rev_mv, lambda r, m: rev["counts"][r, m], orc_mv, lambda r, m: orc["counts"][r, m], n)
+    return float((first >= 0).mean()), first, float((first_ff >= 0).mean()), first_ff
 
 
 def _net_prior_sampled_games_vs_oracle(E, N, n, sims, seed, base, stride, divergence=False):
@@ -164,13 +181,18 @@ def _net_prior_sampled_games_vs_oracle(E, N, n, sims, seed, base, stride, diverg
         assert np.array_equal(rec["final"][e], orc["final"][r])
     assert check_recorded_priors(pi, v, cnt, leaves, sd, every=16) > 10000
     if divergence:
-        frac, first = _divergence_vs_independent_f32(rec, pick, sd, sims, seed, base)
-        d = first[first >= 0]
+        frac, first, frac_ff, first_ff = _divergence_vs_independent_f32(rec, pick, sd, sims, seed, base)
+
+        def summary(f):
+            d = f[f >= 0]
+            return (f"first diverging move: median {np.median(d) if len(d) else -1:.0f}, min "
+                    f"{d.min() if len(d) else -1}, max {d.max() if len(d) else -1}; histogram by 8 moves "
+                    f"{np.bincount(d // 8, minlength=6).tolist() if len(d) else []}")
         print(f"\nindependent f32 predict (oracle MODE_MLP) vs the engine over {len(pick)} games x {sims} sims: "
-              f"{frac:.3f} of the games diverge; first diverging move: median "
-              f"{np.median(d) if len(d) else -1:.0f}, min {d.min() if len(d) else -1}, max {d.max() if len(d) else -1}; "
-              f"histogram by 8 moves {np.bincount(d // 8, minlength=6).tolist() if len(d) else []}")
-        st["divergence"] = (frac, first)
+              f"{frac:.3f} of the games diverge; {summary(first)}")
+        print(f"the same oracle with every Linear summed in reverse order (f32 vs f32): {frac_ff:.3f} of the "
+              f"games diverge; {summary(first_ff)}")
+        st["divergence"] = (frac, first, frac_ff, first_ff)
     eng.close()
     return st
 
