@@ -103,6 +103,20 @@ def test_predict_vs_reference(golden, hidden, nblocks):
     np.testing.assert_allclose(v, g["v"], rtol=0, atol=1e-5)
 
 
+def test_reverse_sum_order_is_another_valid_f32_forward(golden):
+    """oracle.Net(reverse_sums=True) (the f32-vs-f32 divergence baseline of
+    test_gpu_selfplay.py) sums every Linear last to first: its outputs differ from the forward
+    order's in the last bits and hold the same tolerance to the reference."""
+    g = golden("predict_h256_b6.npz")
+    sd = spec.closed_form_weights(256, 6)
+    pi, v = O.Net(sd, 256, 6).predict_states(g["states"])
+    pr, vr = O.Net(sd, 256, 6, reverse_sums=True).predict_states(g["states"])
+    assert (pi != pr).mean() > 0.5
+    np.testing.assert_allclose(pr, g["pi"], rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(vr, g["v"], rtol=0, atol=1e-5)
+    np.testing.assert_allclose(pr, pi, rtol=1e-5, atol=1e-7)
+
+
 def _episode_case(g, i):
     meta = g["meta"][i]
     return dict(seed=int(meta[0]), env=int(meta[1]), sims=int(meta[2]), tt=int(meta[3]), nmoves=int(meta[4]),
