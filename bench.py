@@ -289,7 +289,8 @@ def coach_iter_leg(model, world, games_per_gpu=8192, seed=0, amp=True, warm=True
     steps = 15 * -(-n // 512)
     out = {"config": f"one Coach.learn iteration, main.py args: numEps {args.numEps} ({games_per_gpu}/GPU x {world}), "
                      f"25 sims, maxlenOfQueue 200000, 15 epochs x batch 512 "
-                     f"({'autocast + GradScaler on fp16 MFMA' if amp else 'f32'}), dropout 0.3, arenaCompare 10",
+                     f"({'autocast + GradScaler on fp16 MFMA' if amp else 'f32'}; every rank the whole minibatch), "
+                     f"dropout 0.3, arenaCompare 10",
            "examples_kept": n, "train_steps": steps, "gate_tally_prev_new_draws": list(c.last_pit)}
     out.update({k: round(v, 4) for k, v in c.phase_times.items()})
     out["train_ms_per_step"] = 1000.0 * c.phase_times["train_s"] / max(steps, 1)
@@ -302,8 +303,10 @@ def coach_leg(model, image, n_envs, max_moves, sims, world, train_steps=60, aren
               seed=0):
     """Config 5's Coach iteration after the self-play the timed steps just did (Coach.py:74-139),
     on every rank: the pooled replay buffer from the (all-gathered) record images
-    (yk_examples_from_records), `train_steps` DDP train steps of the reference minibatch (512
-    examples split over the ranks, gradient all-reduce, clip, AdamW; NNetWrapper.train), and
+    (yk_examples_from_records), `train_steps` train steps of the reference minibatch (512
+    examples, clip, AdamW; NNetWrapper.train: every rank the whole minibatch, the default
+    ddp_batch "replicated" - and at N > 1 also timed "split": the minibatch split over the
+    ranks with a gradient all-reduce per step), and
     the gating arena (previous vs new net, MCTS temp 0 each, one dual-tree batch sharded over
     the ranks).  Returns this rank's phase times; rank 0 reports them."""
     import numpy as np
@@ -341,17 +344,32 @@ def coach_leg(model, image, n_envs, max_moves, sims, world, train_steps=60, aren
     torch.cuda.synchronize()
     train_steps = -(-len(timed) // bs)
     t_tr = (time.perf_counter() - t1) / max(train_steps, 1)
+    t_split = None
+    if world > 1:  # the DDP alternative: each rank a 1/N share, one RCCL all-reduce per step
+        spl = NNetWrapper(game, dotdict(args, ddp_batch="split"))
+        spl.nnet.load_state_dict(model.state_dict())
+        spl.train(warm, verbose=False)
+        D.barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        spl.train(timed, verbose=False)
+        torch.cuda.synchronize()
+        t_split = (time.perf_counter() - t1) / max(train_steps, 1)
     D.barrier()
     t2 = time.perf_counter()
     pw, nw, dr = GatingArena(game, prev, new, args).playGames(arena_games, env_base=10**6)
     torch.cuda.synchronize()
     t_ar = time.perf_counter() - t2
     return {"config": f"pooled examples of the timed batch ({n} examples from {world} rank(s)); "
-                      f"{train_steps} train steps of minibatch {bs} split over {world} rank(s) (DDP all-reduce, "
-                      f"clip 5.0, AdamW, dropout {args.dropout}, f32); gating arena {arena_games} games, "
+                      f"{train_steps} train steps of minibatch {bs} (every rank the whole minibatch: "
+                      f"ddp_batch replicated; clip 5.0, AdamW, dropout {args.dropout}, f32); gating arena {arena_games} games, "
                       f"{arena_sims} sims, previous vs new net on dual trees, sharded",
             "examples": n, "examples_ms": 1000.0 * t_ex, "train_ms_per_step": 1000.0 * t_tr,
-            "train_examples_per_s": bs / t_tr, "arena_s": t_ar, "arena_games_per_s": arena_games / t_ar,
+            "train_examples_per_s": bs / t_tr,
+            "train_ms_per_step_split": None if t_split is None else 1000.0 * t_split,
+            "train_split_basis": "ddp_batch split: the minibatch split over the ranks, one gradient all-reduce per "
+                                 "step (N > 1 only)",
+            "arena_s": t_ar, "arena_games_per_s": arena_games / t_ar,
             "arena_tally_prev_new_draws": [pw, nw, dr]}
 
 

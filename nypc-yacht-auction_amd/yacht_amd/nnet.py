@@ -188,10 +188,16 @@ class NNetWrapper:
 
         `examples`: the reference's list of (board, pi, v), an ExampleShard (device replay
         buffer), or a list of either (trainExamplesHistory).  Under torch.distributed every
-        rank holds the same pooled examples and draws the same permutation; each minibatch is
-        split across the ranks, and the all-reduce of the share-weighted gradients gives every
-        rank the whole minibatch's gradient, so all ranks take the single-process step (up to
-        f32 summation order) and their parameters stay identical."""
+        rank holds the same pooled examples and draws the same permutation, and
+        args.ddp_batch picks how the ranks share a minibatch:
+          "replicated" (default): every rank takes the whole minibatch's step itself - no
+            collective, parameters bit-identical to one process training alone.  The step is
+            latency-bound (a 16-row tile per workgroup, 32 of them at batch 512), so
+            a rank's share of a split batch would not run faster, and the split adds an
+            all-reduce per step;
+          "split": the minibatch split across the ranks, the share-weighted gradients
+            all-reduced (DDP): the single-process step up to f32 summation order;
+          "per_rank": every rank its own batch_size rows (a world x batch_size global batch)."""
         from . import dist as D
         from .replay import as_device_examples
         tr = self._trainer()
@@ -199,7 +205,10 @@ class NNetWrapper:
         rank, world = D.rank_world()
         n = states.shape[0]
         bs = self.args.batch_size
-        rows = bs * world if world > 1 and self.args.get("ddp_batch", "split") == "per_rank" else bs
+        mode = self.args.get("ddp_batch", "replicated") if world > 1 else "replicated"
+        if mode not in ("replicated", "split", "per_rank"):
+            raise ValueError(f"ddp_batch must be replicated, split or per_rank, not {mode!r}")
+        rows = bs * world if mode == "per_rank" else bs
         vw = self.args.get("vloss_weight", 1.0)
         g = torch.Generator(device="cuda")
         g.manual_seed(int(self.args.get("seed", 0)) + 1000003 * tr.step_count)
@@ -209,7 +218,7 @@ class NNetWrapper:
             total, count = 0.0, 0
             for i in range(0, n, rows):
                 idx = perm[i:i + rows]
-                if world == 1:
+                if mode == "replicated":
                     tr.step(states, targets, values, idx=idx)
                     b = idx.numel()
                 else:

@@ -152,6 +152,11 @@ def _coach_worker(rank, world, port, ckdir, out):
     coach.nnet.train([shard], verbose=False)
     out[f"p{rank}"] = {k: v.numpy().copy() for k, v in coach.nnet.nnet.state_dict().items()}
     out[f"pit{rank}"] = GatingArena(game, coach.pnet, coach.nnet, args).playGames(args.arenaCompare, env_base=900)
+    # DDP split: the minibatch split over the ranks, gradients all-reduced
+    ws = NNetWrapper(game, dotdict(args, ddp_batch="split"))
+    ws.nnet.load_state_dict(coach.pnet.nnet.state_dict())
+    ws.train([shard], verbose=False)
+    out[f"ps{rank}"] = {k: v.numpy().copy() for k, v in ws.nnet.state_dict().items()}
     # DDP weak scaling: every rank its own batch_size rows (a global minibatch of 2 x batch_size)
     wk = NNetWrapper(game, dotdict(args, ddp_batch="per_rank"))
     wk.nnet.load_state_dict(coach.pnet.nnet.state_dict())
@@ -193,13 +198,18 @@ def test_coach_iteration_two_ranks_sharing_gpu0(Y, tmp_path):
     _, img1 = _selfplay(E, coach.nnet.yk_net(), 3, 4, 21, 503)  # rank 1's own games
     part = R.examples_from_images(img1, 3, 48, 4)
     assert torch.equal(part.targets.cpu(), torch.from_numpy(out["ex0"][1][3 * 48:]))
-    # DDP: both ranks bit-identical; equal to the single-process train up to f32 summation order
+    # replicated (the default): every rank takes the whole minibatch's step - bit-identical to the
+    # single-process train, no collective
     p0, p1 = out["p0"], out["p1"]
     assert all(np.array_equal(p0[k], p1[k]) for k in p0)
     coach.nnet.train([single], verbose=False)
     sp = coach.nnet.nnet.state_dict()
-    a = np.concatenate([p0[k].reshape(-1) for k in p0]).astype(np.float64)
-    b = np.concatenate([sp[k].numpy().reshape(-1) for k in p0]).astype(np.float64)
+    assert all(np.array_equal(p0[k], sp[k].numpy()) for k in p0)
+    # DDP split: both ranks bit-identical; equal to the single-process train up to f32 summation order
+    ps0, ps1 = out["ps0"], out["ps1"]
+    assert all(np.array_equal(ps0[k], ps1[k]) for k in ps0)
+    a = np.concatenate([ps0[k].reshape(-1) for k in ps0]).astype(np.float64)
+    b = np.concatenate([sp[k].numpy().reshape(-1) for k in ps0]).astype(np.float64)
     # AdamW divides by sqrt(v) + eps, so a gradient entry near eps can move its weight by up to
     # 2 lr on a summation-order change; everything else agrees to f32 rounding
     assert np.linalg.norm(a - b) / np.linalg.norm(b) < 1e-4
@@ -215,7 +225,7 @@ def test_coach_iteration_two_ranks_sharing_gpu0(Y, tmp_path):
     b = np.concatenate([wide.nnet.state_dict()[k].numpy().reshape(-1) for k in pr0[0]]).astype(np.float64)
     assert np.linalg.norm(a - b) / np.linalg.norm(b) < 1e-4 and (np.abs(a - b) > 1e-5).mean() < 1e-3
     # the sharded gating arena's tally is the single-GPU arena's on the same two nets: the
-    # ranks' previous net (the initial weights, net0) against their DDP-trained p0
+    # ranks' previous net (the initial weights, net0) against their trained p0
     newnet = NNetWrapper(game, args)
     newnet.nnet.load_state_dict({k: torch.from_numpy(v) for k, v in p0.items()})
     pit = GatingArena(game, net0, newnet, args).playGames(args.arenaCompare, env_base=900)
