@@ -6,7 +6,7 @@
 // arithmetic - the fp16 rounding points included - on hand-written v_mfma_f32_16x16x32_f16
 // kernels instead of library GEMMs (yk_train.hip keeps the f32 rocBLAS step for the f32 mode).
 //
-// A step is ten launches (yk_train_amp.h):
+// A step is nine launches (yk_train_amp.h):
 //   k_amp_fwd      one 512-thread workgroup per 16-row tile: features -> input layer -> the
 //                  residual blocks -> the heads' LayerNorms, every dense layer from a register
 //                  ring of fp16 weight fragments that streams the next layer during the row pass;
@@ -22,12 +22,14 @@
 //                  backward chain (LayerNorm / SiLU / dropout backward, the dX GEMMs) to the input
 //   k_amp_dw       every weight gradient (13 + 2 GEMMs, K = the batch) in one grouped launch
 //   k_amp_vecsum   bias / LayerNorm gradients and the loss sums: fixed-order column sums
-//   k_amp_sq, k_amp_adamw, k_amp_pack  unscale + norm, clip + AdamW (or skip), GradScaler
-//                  update and the fp16 weight copies for the next step
+//   k_amp_sq       unscale + the gradient norm
+//   k_amp_update   clip + AdamW (or skip), GradScaler update and the fp16 weight copies for the
+//                  next step, a 32 x 32 weight tile (or a vector slice) per workgroup
 // Weight fragments use yk_net.h's packing (one plane): for W[N][K], the 1 KB piece (nt, ks) holds
 // W[16 nt + (l & 15)][32 ks + 8 (l >> 4) + j] for lane l, j < 8.  The T layout of an activation
 // matrix X[rows][C] is the same packing of X^T (piece (ct, rs): X[32 rs + 8 (l >> 4) + j][16 ct +
 // (l & 15)]), so dW = dU^T X is an MFMA over 32-row slices with both operands read whole.
+#include <algorithm>
 #include <cmath>
 #include <vector>
 
@@ -1087,35 +1089,6 @@ __device__ __forceinline__ double sq_total(const double* part) {
     __syncthreads();
     return tot;
 }
-// scaler.step: skipped when the gradients are not finite; else unscale, clip_grad_norm_, AdamW
-// (torch's single-tensor update, bias corrections from the step count of the steps taken)
-__global__ void k_amp_adamw(float* __restrict__ P, float* __restrict__ G, float* __restrict__ M, float* __restrict__ V,
-                            long n, const double* __restrict__ part, double* sq_out, const Scaler* sc, float max_norm,
-                            float lr, float wd, float b1, float b2, float eps) {
-    const double total = sq_total(part);
-    if (blockIdx.x == 0 && threadIdx.x == 0) *sq_out = total;
-    if (!isfinite(total)) return;
-    const float inv = 1.0f / sc->scale;
-    const double st = (double)(sc->steps + 1);
-    const float step_size = (float)((double)lr / (1.0 - pow((double)b1, st)));
-    const float bc2_sqrt = (float)sqrt(1.0 - pow((double)b2, st));
-    const float norm = (float)sqrt(total);
-    float coef = max_norm / (norm + 1e-6f);
-    coef = coef > 1.0f ? 1.0f : coef;
-    const float decay = 1.0f - lr * wd;
-    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-        const float gi = (G[i] * inv) * coef;
-        G[i] = gi;
-        float pi = P[i] * decay;
-        const float mi = M[i] + (gi - M[i]) * (1.0f - b1);
-        const float vi = V[i] * b2 + (1.0f - b2) * gi * gi;
-        M[i] = mi;
-        V[i] = vi;
-        const float denom = sqrtf(vi) / bc2_sqrt + eps;
-        pi -= step_size * (mi / denom);
-        P[i] = pi;
-    }
-}
 // fp16 fragments of one weight matrix W[N][K] (f32, row-major): `trans` packs W^T
 struct PackJob {
     const float* W;
@@ -1123,27 +1096,10 @@ struct PackJob {
     int N, K, Np, Kp, trans;  // packed shape Np x Kp (of W or of W^T)
     long first;               // first item (float4) of this job
 };
-// scaler.update (block 0, thread 0; GradScaler('cuda') defaults: growth 2, backoff 0.5) and the
-// fp16 weight copies for the next step
-// blk_job[b]: the job of block b (every job's item count is a multiple of the block size, so a
-// block lies in one job; checked in amp_create)
-__global__ void k_amp_pack(const PackJob* __restrict__ jobs, const uint8_t* __restrict__ blk_job, long total,
-                           Scaler* sc, const double* __restrict__ part, int update) {
-    const double t = (update && blockIdx.x == 0) ? sq_total(part) : 0.0;
-    if (update && blockIdx.x == 0 && threadIdx.x == 0) {
-        if (!isfinite(t)) {
-            sc->scale *= 0.5f;
-            sc->tracker = 0;
-            sc->found_inf = 1;
-        } else {
-            sc->steps += 1;
-            sc->found_inf = 0;
-            if (++sc->tracker == sc->growth_interval) {
-                sc->scale *= 2.0f;
-                sc->tracker = 0;
-            }
-        }
-    }
+// the fp16 weight copies of the parameters (creation, a parameter load); the optimiser step
+// refreshes them itself (k_amp_update).  blk_job[b]: the job of block b (every job's item count
+// is a multiple of the block size, so a block lies in one job; checked in amp_create)
+__global__ void k_amp_pack(const PackJob* __restrict__ jobs, const uint8_t* __restrict__ blk_job, long total) {
     const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= total) return;
     const PackJob jb = jobs[blk_job[blockIdx.x]];
@@ -1166,6 +1122,115 @@ __global__ void k_amp_pack(const PackJob* __restrict__ jobs, const uint8_t* __re
         v[t] = (_Float16)x;
     }
     *reinterpret_cast<half8*>(jb.dst + e) = v;
+}
+
+// scaler.step + scaler.update + the fp16 repack in one launch: a block owns a 32 x 32 tile of one
+// weight matrix - AdamW on its 1024 elements (torch's single-tensor update), then both fp16
+// fragment orientations of the tile from LDS -
+// or a 1024-element slice of the vectors (biases, LayerNorms, v_head.4).  The GradScaler state is
+// double-buffered: every block reads `sc`, block 0 writes the updated state to `sc_next` (the
+// host swaps them), so no block can see a half-updated scale.
+struct UpdJob {
+    float *W, *Gm, *Mm, *Vm;  // the matrix [N][K] in the parameter / gradient / moment buffers (or a vector range)
+    float4 *dstN, *dstT;      // fp16 fragments of W (packed columns KpN) and of W^T (packed columns KpT), or null
+    int N, K, KpN, KpT;
+};
+struct UpdItem {
+    int job, n0, k0;  // a matrix tile's first row / column; a vector slice: n0 = first element, k0 = count
+};
+__device__ __forceinline__ void adamw_elem(float& p, float& g, float& m, float& v, float inv, float coef,
+                                           float decay, float b1, float b2, float eps, float step_size,
+                                           float bc2_sqrt) {  // torch.optim.AdamW's single-tensor step
+    const float gi = (g * inv) * coef;
+    g = gi;
+    float pi = p * decay;
+    const float mi = m + (gi - m) * (1.0f - b1);
+    const float vi = v * b2 + (1.0f - b2) * gi * gi;
+    m = mi;
+    v = vi;
+    const float denom = sqrtf(vi) / bc2_sqrt + eps;
+    pi -= step_size * (mi / denom);
+    p = pi;
+}
+__global__ __launch_bounds__(256) void k_amp_update(const UpdJob* __restrict__ jobs, const UpdItem* __restrict__ items,
+                                                    const double* __restrict__ part, double* sq_out,
+                                                    const Scaler* __restrict__ sc, Scaler* __restrict__ sc_next,
+                                                    float max_norm, float lr, float wd, float b1, float b2, float eps) {
+    __shared__ _Float16 Tl[32][40];
+    const double total = sq_total(part);
+    const Scaler s0 = *sc;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        *sq_out = total;
+        Scaler n = s0;  // GradScaler('cuda').update: growth 2, backoff 0.5
+        if (!isfinite(total)) {
+            n.scale *= 0.5f;
+            n.tracker = 0;
+            n.found_inf = 1;
+        } else {
+            n.steps += 1;
+            n.found_inf = 0;
+            if (++n.tracker == n.growth_interval) {
+                n.scale *= 2.0f;
+                n.tracker = 0;
+            }
+        }
+        *sc_next = n;
+    }
+    if (!isfinite(total)) return;  // step skipped: parameters and their fp16 copies unchanged
+    const float inv = 1.0f / s0.scale;
+    const double st = (double)(s0.steps + 1);
+    const float step_size = (float)((double)lr / (1.0 - pow((double)b1, st)));
+    const float bc2_sqrt = (float)sqrt(1.0 - pow((double)b2, st));
+    const float norm = (float)sqrt(total);
+    float coef = max_norm / (norm + 1e-6f);
+    coef = coef > 1.0f ? 1.0f : coef;
+    const float decay = 1.0f - lr * wd;
+    const UpdItem it = items[blockIdx.x];
+    const UpdJob jb = jobs[it.job];
+    const int t = threadIdx.x;
+    if (!jb.dstN) {  // a vector slice: 4 consecutive elements per thread
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int e = 4 * t + i;
+            if (e < it.k0) {
+                const long o = (long)it.n0 + e;
+                adamw_elem(jb.W[o], jb.Gm[o], jb.Mm[o], jb.Vm[o], inv, coef, decay, b1, b2, eps, step_size, bc2_sqrt);
+            }
+        }
+        return;
+    }
+    const int r = t >> 3, c = (t & 7) * 4;
+    const int n = it.n0 + r;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int k = it.k0 + c + i;
+        float pv = 0.f;
+        if (n < jb.N && k < jb.K) {
+            const long o = (long)n * jb.K + k;
+            float p = jb.W[o], g = jb.Gm[o], m = jb.Mm[o], v = jb.Vm[o];
+            adamw_elem(p, g, m, v, inv, coef, decay, b1, b2, eps, step_size, bc2_sqrt);
+            jb.W[o] = p;
+            jb.Gm[o] = g;
+            jb.Mm[o] = m;
+            jb.Vm[o] = v;
+            pv = p;
+        }
+        Tl[r][c + i] = (_Float16)pv;
+    }
+    __syncthreads();
+    const int f = (t >> 6) & 1, l = t & 63;
+    half8 h;
+    if (t < 128) {  // W: fragment (n0 / 16 + f, k0 / 32), lane l = W[16 nt + (l & 15)][32 ks + 8 (l >> 4) + j]
+        const int rr = 16 * f + (l & 15), kk = 8 * (l >> 4);
+#pragma unroll
+        for (int j = 0; j < 8; j++) h[j] = Tl[rr][kk + j];
+        *reinterpret_cast<half8*>(jb.dstN + ((long)(it.n0 / 16 + f) * (jb.KpN / 32) + it.k0 / 32) * 64 + l) = h;
+    } else if (jb.dstT) {  // W^T: fragment (k0 / 16 + f, n0 / 32), lane l = W[32 ks + 8 (l >> 4) + j][16 nt + (l & 15)]
+        const int kk = 16 * f + (l & 15), rr = 8 * (l >> 4);
+#pragma unroll
+        for (int j = 0; j < 8; j++) h[j] = Tl[rr + j][kk];
+        *reinterpret_cast<half8*>(jb.dstT + ((long)(it.k0 / 16 + f) * (jb.KpT / 32) + it.n0 / 32) * 64 + l) = h;
+    }
 }
 
 }  // namespace
@@ -1191,7 +1256,16 @@ struct AmpTrain {
     int n_pk_jobs = 0;
     long pk_total = 0;
     double* sqpart = nullptr;
-    Scaler* sc = nullptr;
+    Scaler* sc = nullptr;       // the current GradScaler state
+    Scaler* sc_next = nullptr;  // k_amp_update writes the next one here; the host swaps the two
+    UpdJob* upd_jobs = nullptr;
+    UpdItem* upd_items = nullptr;
+    int n_upd_items = 0;
+    const float *upd_M = nullptr, *upd_V = nullptr;  // the moment buffers the jobs were built for
+    const long* off_host = nullptr;                    // (amp_create's offsets, kept for the jobs)
+    std::vector<long> offs;
+    float4 *win_f = nullptr, *w1f = nullptr, *w2f = nullptr, *w1t = nullptr, *w2t = nullptr, *wpif = nullptr,
+           *wpit = nullptr, *wv1f = nullptr, *wv1t = nullptr;
     float* lsum_src_dummy = nullptr;
     float2* lrow = nullptr;
     float* lsum = nullptr;
@@ -1250,6 +1324,8 @@ int amp_create(AmpTrain** out, int H, int NB, int Bmax, float* P, float* G, cons
     AA(wv1t, (size_t)VH * H / 8);
     d.win_f = win_f; d.w1f = w1f; d.w2f = w2f; d.w1t = w1t; d.w2t = w2t;
     d.wpif = wpif; d.wpit = wpit; d.wv1f = wv1f; d.wv1t = wv1t;
+    a->win_f = win_f; a->w1f = w1f; a->w2f = w2f; a->w1t = w1t; a->w2t = w2t;
+    a->wpif = wpif; a->wpit = wpit; a->wv1f = wv1f; a->wv1t = wv1t;
     AA(d.xT, (size_t)4 * RS * 512);
     AA(d.hT, NB * tlH + 1);
     AA(d.r1T, NB * tlH + 1);
@@ -1280,6 +1356,7 @@ int amp_create(AmpTrain** out, int H, int NB, int Bmax, float* P, float* G, cons
     AA(d.colpart, T * d.NVEC * H);
     AA(a->sqpart, (size_t)SQ_BLOCKS);
     AA(a->sc, 1);
+    AA(a->sc_next, 1);
     if (rc != YK_OK) {
         amp_destroy(a);
         return rc;
@@ -1292,6 +1369,7 @@ int amp_create(AmpTrain** out, int H, int NB, int Bmax, float* P, float* G, cons
     d.off = a->off_dev;
     d.sc = a->sc;
     std::vector<long> offv(off, off + ntens);
+    a->offs = offv;
     YK_HIP(hipMemcpy(a->off_dev, offv.data(), sizeof(long) * ntens, hipMemcpyHostToDevice));
     Scaler s0{init_scale > 0.f ? init_scale : 65536.0f, 0, 0, 0, growth_interval > 0 ? growth_interval : 2000};
     YK_HIP(hipMemcpy(a->sc, &s0, sizeof(Scaler), hipMemcpyHostToDevice));
@@ -1398,7 +1476,7 @@ void amp_destroy(AmpTrain* a) {
 
 int amp_pack(AmpTrain* a, hipStream_t s) {
     hipLaunchKernelGGL(k_amp_pack, dim3((unsigned)((a->pk_total + 255) / 256)), dim3(256), 0, s, a->pk_jobs,
-                       a->pk_blk, a->pk_total, a->sc, a->sqpart, 0);
+                       a->pk_blk, a->pk_total);
     YK_LAUNCHED();
     return YK_OK;
 }
@@ -1447,16 +1525,63 @@ int amp_backward(AmpTrain* a, const yk_state_t* states, const int32_t* targets, 
     return YK_OK;
 }
 
+// k_amp_update's work list: a 32 x 32 tile of every packed weight matrix, and 1024-element slices
+// of the parameters no matrix covers
+static int build_update_jobs(AmpTrain* a, long nparams, float* M, float* V) {
+    const int H = a->H, NB = a->NB;
+    const long* off = a->offs.data();
+    const size_t HH = (size_t)H * H;
+    float* P = const_cast<float*>(a->d.P);
+    float* G = a->d.G;
+    std::vector<UpdJob> jobs;
+    std::vector<UpdItem> items;
+    std::vector<std::pair<long, long>> mats;
+    auto mat = [&](long o, int N, int K, float4* dN, int KpN, float4* dT, int KpT) {
+        const int j = (int)jobs.size();
+        jobs.push_back({P + o, G + o, M + o, V + o, dN, dT, N, K, KpN, KpT});
+        for (int n0 = 0; n0 < N; n0 += 32)
+            for (int k0 = 0; k0 < K; k0 += 32) items.push_back({j, n0, k0});
+        mats.push_back({o, o + (long)N * K});
+    };
+    mat(off[T_WIN], H, FEAT, a->win_f, 64, nullptr, 0);
+    for (int b = 0; b < NB; b++) {
+        mat(off[t_blk(b, 0)], H, H, a->w1f + b * HH / 8, H, a->w1t + b * HH / 8, H);
+        mat(off[t_blk(b, 4)], H, H, a->w2f + b * HH / 8, H, a->w2t + b * HH / 8, H);
+    }
+    mat(off[t_head(NB, HP_W)], ASIZE, H, a->wpif, H, a->wpit, LDL);
+    mat(off[t_head(NB, HV_W1)], VH, H, a->wv1f, H, a->wv1t, VH);
+    std::sort(mats.begin(), mats.end());
+    const int jv = (int)jobs.size();
+    jobs.push_back({P, G, M, V, nullptr, nullptr, 0, 0, 0, 0});
+    long pos = 0;
+    mats.push_back({nparams, nparams});
+    for (const auto& m : mats) {
+        for (long e = pos; e < m.first; e += 1024) items.push_back({jv, (int)e, (int)std::min<long>(1024, m.first - e)});
+        pos = std::max(pos, m.second);
+    }
+    if (!a->upd_jobs && (aalloc(a, &a->upd_jobs, jobs.size()) || aalloc(a, &a->upd_items, items.size())))
+        return YK_ERR_NOMEM;
+    YK_HIP(hipMemcpy(a->upd_jobs, jobs.data(), sizeof(UpdJob) * jobs.size(), hipMemcpyHostToDevice));
+    YK_HIP(hipMemcpy(a->upd_items, items.data(), sizeof(UpdItem) * items.size(), hipMemcpyHostToDevice));
+    a->n_upd_items = (int)items.size();
+    a->upd_M = M;
+    a->upd_V = V;
+    return YK_OK;
+}
+
 int amp_apply(AmpTrain* a, long nparams, float* M, float* V, double* sq_out, float max_norm, float lr, float wd,
               float b1, float b2, float eps, hipStream_t s) {
+    if (a->upd_M != M || a->upd_V != V) {  // the update jobs address the trainer's moment buffers
+        const int rc = build_update_jobs(a, nparams, M, V);
+        if (rc != YK_OK) return rc;
+    }
     hipLaunchKernelGGL(k_amp_sq, dim3(SQ_BLOCKS), dim3(256), 0, s, a->d.G, nparams, a->sc, a->sqpart);
     YK_LAUNCHED();
-    hipLaunchKernelGGL(k_amp_adamw, dim3(2048), dim3(256), 0, s, const_cast<float*>(a->d.P), a->d.G, M, V, nparams,
-                       a->sqpart, sq_out, a->sc, max_norm, lr, wd, b1, b2, eps);
+    hipLaunchKernelGGL(k_amp_update, dim3((unsigned)a->n_upd_items), dim3(256), 0, s, a->upd_jobs, a->upd_items,
+                       a->sqpart, sq_out, a->sc, a->sc_next, max_norm, lr, wd, b1, b2, eps);
     YK_LAUNCHED();
-    hipLaunchKernelGGL(k_amp_pack, dim3((unsigned)((a->pk_total + 255) / 256)), dim3(256), 0, s, a->pk_jobs,
-                       a->pk_blk, a->pk_total, a->sc, a->sqpart, 1);
-    YK_LAUNCHED();
+    std::swap(a->sc, a->sc_next);  // the next launches read the updated GradScaler state
+    a->d.sc = a->sc;
     return YK_OK;
 }
 
