@@ -189,9 +189,11 @@ __device__ __forceinline__ void gemm_ring(const _Float16* A, int sa, float4 (&ri
         if (g < KS) {
 #pragma unroll
             for (int t = 0; t < NT; t++) w[t] = cur[((long)(nt0 + t) * KS + g) * 64 + lane];
-        } else if (nxt) {
+        } else {  // the next layer's slices; after the last layer `cur` again (unused): the refills stay
+                  // unconditional, so the wait counters after this loop are exact (no vmcnt(0) drains)
+            const float4* src = nxt ? nxt : cur;
 #pragma unroll
-            for (int t = 0; t < NT; t++) w[t] = nxt[((long)(nt0 + t) * KS + g - KS) * 64 + lane];
+            for (int t = 0; t < NT; t++) w[t] = src[((long)(nt0 + t) * KS + g - KS) * 64 + lane];
         }
         __builtin_amdgcn_sched_barrier(0);
         a = an;
@@ -271,10 +273,13 @@ __global__ __launch_bounds__(TTHR) void k_amp_fwd(AmpDev d, const yk_state_t* __
     __shared__ __attribute__((aligned(16))) float Xs[TR * LD];
     __shared__ __attribute__((aligned(16))) float Ts[TR * LD];
     __shared__ __attribute__((aligned(16))) _Float16 Pa[TR * SA];
-    __shared__ __attribute__((aligned(16))) float VL[3 * H];
+    __shared__ __attribute__((aligned(16))) float VL[(3 * H + TTHR - 1) / TTHR * TTHR];  // (padded: unconditional writes)
     const int tile = blockIdx.x, row0 = tile * TR;
     const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-    const bool gw = wave < NACT;
+    // every wave owns columns when NACT == TW (hidden >= 128): a compile-time true, so no branch
+    // around the weight ring (at a branch join the wait counters merge to the stricter count, and
+    // a vmcnt(0) there would drain the ring's in-flight refills)
+    const bool gw = NACT == TW || wave < NACT;
     const int nt0 = wave * NT, c0 = lane * VPL;
     const bool zero_half = row0 + TR >= B && (tile & 1) == 0;
     const float sc = p > 0.f ? 1.0f / (1.0f - p) : 1.0f;
@@ -367,7 +372,8 @@ __global__ __launch_bounds__(TTHR) void k_amp_fwd(AmpDev d, const yk_state_t* __
 #pragma unroll                               // ring's refills, so the LDS copy never waits behind them)
             for (int k = 0; k < (3 * H + TTHR - 1) / TTHR; k++) {
                 const int i = tid + TTHR * k;
-                if (i < 3 * H) vr[k] = d.P[poff(H, d.NB, t_blk(b, kb + i / H)) + i % H];
+                const int ic = i < 3 * H ? i : 3 * H - 1;  // unconditional: no branch join before the ring
+                vr[k] = d.P[poff(H, d.NB, t_blk(b, kb + ic / H)) + ic % H];
             }
             const float4* cur = (half == 0 ? d.w1f : d.w2f) + b * HH8;
             const float4* nxt = half == 0 ? d.w2f + b * HH8 : (b + 1 < NB ? d.w1f + (b + 1) * HH8 : nullptr);
@@ -376,10 +382,7 @@ __global__ __launch_bounds__(TTHR) void k_amp_fwd(AmpDev d, const yk_state_t* __
                 store_acc<NT>(Ts, LD, nt0, acc);
             }
 #pragma unroll
-            for (int k = 0; k < (3 * H + TTHR - 1) / TTHR; k++) {
-                const int i = tid + TTHR * k;
-                if (i < 3 * H) VL[i] = vr[k];
-            }
+            for (int k = 0; k < (3 * H + TTHR - 1) / TTHR; k++) VL[tid + TTHR * k] = vr[k];
             lds_barrier();
             float* U = (half == 0 ? d.u1 : d.u2) + (long)b * d.Bmax * H;
             const int L = 1 + 2 * b + half;
@@ -652,7 +655,10 @@ __global__ __launch_bounds__(TTHR) void k_amp_headbwd(AmpDev d, const int32_t* _
     const int tile = blockIdx.x, part = blockIdx.y, row0 = tile * TR;
     const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const int ks0 = part * PKS / BQ, ks1 = (part + 1) * PKS / BQ, ns = ks1 - ks0;
-    const bool gw = wave < NACT;
+    // every wave owns columns when NACT == TW (hidden >= 128): a compile-time true, so no branch
+    // around the weight ring (at a branch join the wait counters merge to the stricter count, and
+    // a vmcnt(0) there would drain the ring's in-flight refills)
+    const bool gw = NACT == TW || wave < NACT;
     const int nt0 = wave * NT;
     float4 ring[RD][NT];
     if (gw) {  // the first slices of Wpi^T stream in while the gradient block is built
@@ -775,7 +781,10 @@ __global__ __launch_bounds__(TTHR) void k_amp_bwd(AmpDev d, int B, float p, uint
     __shared__ __attribute__((aligned(16))) float CP[TW * 3 * H];
     const int tile = blockIdx.x, row0 = tile * TR;
     const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-    const bool gw = wave < NACT;
+    // every wave owns columns when NACT == TW (hidden >= 128): a compile-time true, so no branch
+    // around the weight ring (at a branch join the wait counters merge to the stricter count, and
+    // a vmcnt(0) there would drain the ring's in-flight refills)
+    const bool gw = NACT == TW || wave < NACT;
     const int nt0 = wave * NT, c0 = lane * VPL;
     const bool zero_half = row0 + TR >= B && (tile & 1) == 0;
     const float sc = p > 0.f ? 1.0f / (1.0f - p) : 1.0f;
@@ -927,12 +936,15 @@ __global__ __launch_bounds__(TTHR) void k_amp_bwd(AmpDev d, int B, float p, uint
             flush_gbb<H>(d, CP, tile, CV_BLK + 6 * b + (half == 0 ? 0 : 3));
             write_tl(Pa, SA, 0, H, (half == 0 ? d.du1T : d.du2T) + b * TLH, d.RS, 0, tile, zero_half);
             // the next row pass's operands, then dX = fp16(dU16 W16) (W2 of half 1, W1 of half 0)
-            if (half == 1)
-                row_prefetch<H>(R, d, d.u1 + (long)b * d.Bmax * H, 1 + 2 * b, t_blk(b, 2), t_blk(b, 3), row0, B);
-            else if (b > 0)
-                row_prefetch<H>(R, d, d.u2 + (long)(b - 1) * d.Bmax * H, 2 * b, t_blk(b - 1, 6), t_blk(b - 1, 7), row0, B);
-            else
-                row_prefetch<H>(R, d, d.z0, 0, T_GIN, T_BEIN, row0, B);
+            // (one call on selected operands: loads in one code path keep the wait counters exact)
+            {
+                const bool h1 = half == 1, more = b > 0;
+                const float* Up = h1 ? d.u1 + (long)b * d.Bmax * H : more ? d.u2 + (long)(b - 1) * d.Bmax * H : d.z0;
+                const int Lp = h1 ? 1 + 2 * b : more ? 2 * b : 0;
+                const int tg = h1 ? t_blk(b, 2) : more ? t_blk(b - 1, 6) : (int)T_GIN;
+                const int tb = h1 ? t_blk(b, 3) : more ? t_blk(b - 1, 7) : (int)T_BEIN;
+                row_prefetch<H>(R, d, Up, Lp, tg, tb, row0, B);
+            }
             __builtin_amdgcn_sched_barrier(0);
             const float4* cur = (half == 1 ? d.w2t : d.w1t) + b * HH8;
             const float4* nxt = half == 1 ? d.w1t + b * HH8 : (b > 0 ? d.w2t + (b - 1) * HH8 : nullptr);
