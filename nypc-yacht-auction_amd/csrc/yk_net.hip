@@ -567,7 +567,8 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
     __shared__ __attribute__((aligned(16))) float T[TSZ];
     __shared__ __attribute__((aligned(16))) _Float16 P[2 * ROWS * SA];  // the next GEMM's input planes
     __shared__ __attribute__((aligned(16))) float VS[NVS];  // static vectors (yk_net.h VS_*)
-    __shared__ __attribute__((aligned(16))) float VB[NVB];  // this block's b1 g1 be1 b2 g2 be2
+    constexpr int NB4 = NVB / 4, PB = (NB4 + NTHR - 1) / NTHR;
+    __shared__ __attribute__((aligned(16))) float VB[4 * NTHR * PB];  // this block's b1 g1 be1 b2 g2 be2 (padded)
     __shared__ uint32_t VD[ROWS];                            // per row: which logits are stored
     __shared__ float HN[ROWS];                               // per row: |a_pi|^2 (policy-head input)
     __shared__ uint8_t TL[PI_TILES];                         // policy tiles a valid-only pass computes
@@ -598,7 +599,10 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
         if (!amask) return;
     }
     const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-    const bool gw = wave < NACT;  // owns columns of the H-wide layers
+    // owns columns of the H-wide layers: every wave when NACT == WAVES (hidden >= 128), as a
+    // compile-time true - a branch around the weight ring would make the wait counters merge at its
+    // join, and the resulting vmcnt(0) drains the ring's in-flight refills of the next layer
+    const bool gw = NACT == WAVES || wave < NACT;
     const int nt0 = wave * NT;
     const int c0 = lane * VPL;
     TSTAMP(0);
@@ -750,15 +754,14 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
     for (int b = 0; b < net.NB; b++) {
         const long wo = (long)b * H * H;
         const float* after = net.w1 + wo + (long)H * H;  // the stream after fc2: the next block's fc1
-        constexpr int NB4 = NVB / 4, PB = (NB4 + NTHR - 1) / NTHR;
         float4 vb[PB];
 #pragma unroll
         for (int k = 0; k < PB; k++) vb[k] = reinterpret_cast<const float4*>(net.vblk + (long)b * NVB)[min(tid + NTHR * k, NB4 - 1)];
         if (gw) mma_ring<PL, H, NT, RW>(P, SA, ring, acc, net.w1 + wo, net.w2 + wo, nt0);
         if (b == 2) TSTAMP(16);
 #pragma unroll
-        for (int k = 0; k < PB; k++)  // the previous block's readers passed a barrier
-            if (tid + NTHR * k < NB4) reinterpret_cast<float4*>(VB)[tid + NTHR * k] = vb[k];
+        for (int k = 0; k < PB; k++)  // the previous block's readers passed a barrier; unconditional
+            reinterpret_cast<float4*>(VB)[tid + NTHR * k] = vb[k];  // (no branch join after the ring)
         if (gw) store_acc<NT>(T, LD, nt0, acc, nullptr);
         lds_barrier();  // T complete; every wave is done reading x's planes
         if (b == 2) TSTAMP(17);
