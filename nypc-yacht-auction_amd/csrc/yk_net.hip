@@ -566,7 +566,8 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
     __shared__ __attribute__((aligned(16))) float X[ROWS * LD];
     __shared__ __attribute__((aligned(16))) float T[TSZ];
     __shared__ __attribute__((aligned(16))) _Float16 P[2 * ROWS * SA];  // the next GEMM's input planes
-    __shared__ __attribute__((aligned(16))) float VS[NVS];  // static vectors (yk_net.h VS_*)
+    constexpr int NV4 = NVS / 4, PER = (NV4 + NTHR - 1) / NTHR;
+    __shared__ __attribute__((aligned(16))) float VS[4 * NTHR * PER];  // static vectors (yk_net.h VS_*; padded)
     constexpr int NB4 = NVB / 4, PB = (NB4 + NTHR - 1) / NTHR;
     __shared__ __attribute__((aligned(16))) float VB[4 * NTHR * PB];  // this block's b1 g1 be1 b2 g2 be2 (padded)
     __shared__ uint32_t VD[ROWS];                            // per row: which logits are stored
@@ -611,13 +612,12 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
     // wait behind the weight stream: vmcnt retires in order), then each wave's two state rows by
     // scalar loads (wave-uniform addresses: SMEM, lgkmcnt), then the weight stream - the input
     // layer and the trunk ring's first RW slices of fc1 - and only then the features
-    constexpr int NV4 = NVS / 4, PER = (NV4 + NTHR - 1) / NTHR;
     float4 vsv[PER];
 #pragma unroll
     for (int k = 0; k < PER; k++) vsv[k] = reinterpret_cast<const float4*>(net.vstat)[min(tid + NTHR * k, NV4 - 1)];
 #pragma unroll
     for (int k = 0; k < PER; k++)
-        if (tid + NTHR * k < NV4) reinterpret_cast<float4*>(VS)[tid + NTHR * k] = vsv[k];
+        reinterpret_cast<float4*>(VS)[tid + NTHR * k] = vsv[k];  // unconditional: the PER loads are waited for once
     constexpr int FPT = ROWS * 64 / NTHR;  // feature rows per wave (row = wave + WAVES k)
     static_assert(FPT * WAVES == ROWS, "one feature row per wave and k");
     YkS fs[FPT];
@@ -632,21 +632,33 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
             for (int q = 0; q < 8; q++) fs[k].w[q] = p[q];
         }
     }
+    // explicit features (predict on given rows) are loaded here, ahead of the weight stream: a
+    // vector load issued after it would retire behind it (vmcnt is in order)
+    float xv[FPT];
+#pragma unroll
+    for (int k = 0; k < FPT; k++) {
+        const int row = row0 + wave + WAVES * k;
+        xv[k] = 0.f;
+        if (xin && row < n && lane < FEAT) xv[k] = xin[(long)(rows ? rows[row] : row) * FEAT + lane];
+    }
     W2 w0[2][NT];
     W2 ring[RW][NT];
-    const float* w_first = net.w1;
+    const float* w_first = net.NB > 0 ? net.w1 : net.w_in;  // (a valid address either way: see below)
     if (gw) {
 #pragma unroll
         for (int ks = 0; ks < 2; ks++)
 #pragma unroll
             for (int t = 0; t < NT; t++) w0[ks][t] = ld_w2<PL>(net.w_in, 2, nt0 + t, ks, lane);
     }
-    if (gw && net.NB > 0) {
+    __builtin_amdgcn_sched_barrier(0);  // the input layer's slices ahead of the ring's (in-order vmcnt)
+    if (gw) {  // unconditional (no NB > 0 branch): a join here would make every later wait count the
+               // ring as absent and over-wait (the slices are unused when NB = 0)
 #pragma unroll
         for (int ks = 0; ks < RW; ks++)
 #pragma unroll
             for (int t = 0; t < NT; t++) ring[ks][t] = ld_w2<PL>(w_first, KS, nt0 + t, ks, lane);
     }
+    __builtin_amdgcn_sched_barrier(0);  // the first layer streams in under the featurize / input phase
     // featurize (state_to_vec, NNet.py:65-86) straight into the input layer's planes, K = 64
     uint32_t vdk[FPT];
 #pragma unroll
@@ -654,7 +666,7 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
         const int rr = wave + WAVES * k, f = lane;
         const int row = row0 + rr;
         float val = 0.f;
-        if (row < n && f < FEAT) val = xin ? xin[(long)(rows ? rows[row] : row) * FEAT + f] : feature(fs[k], f);
+        if (row < n && f < FEAT) val = xin ? xv[k] : feature(fs[k], f);
         const float one[1] = {val};
         put_planes<PL, 1>(P, SA, rr, f, one);
         const uint32_t vdr = row >= n || !((amask >> rr) & 1u) ? LM_NONE

@@ -522,17 +522,20 @@ __global__ __launch_bounds__(TTHR) void k_amp_head(AmpDev d, int B) {
         m[j] = -INFINITY;
         s[j] = 0.f;
     }
-    auto load = [&](float4(&w)[KS], int n) {
+    // a tile's bias is loaded with its weight slices (ahead of them: the in-order wait counter
+    // would otherwise make the bias wait drain the next tile's slices in flight)
+    auto load = [&](float4(&w)[KS], float& bias, int n) {
+        bias = bpi[min(16 * n + (lane & 15), ASIZE - 1)];
 #pragma unroll
         for (int ks = 0; ks < KS; ks++) w[ks] = d.wpif[((long)n * KS + ks) * 64 + lane];
     };
-    auto do_tile = [&](const float4(&w)[KS], int n) {
+    auto do_tile = [&](const float4(&w)[KS], float bias_raw, int n) {
         floatx4 acc = zero4();
 #pragma unroll
         for (int ks = 0; ks < KS; ks++) acc = mfma(*reinterpret_cast<const float4*>(ap + 32 * ks), w[ks], acc);
         const int col = 16 * n + (lane & 15);
         if (col < ASIZE) {
-            const float bias = r16(bpi[col]);
+            const float bias = r16(bias_raw);
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 const int row = row0 + 4 * q + j;
@@ -548,15 +551,16 @@ __global__ __launch_bounds__(TTHR) void k_amp_head(AmpDev d, int B) {
         }
     };
     float4 wa[KS], wb[KS];  // two tiles' slices: the wave's next tile streams in under this one
+    float ba = 0.f, bb = 0.f;
     int nt = t0 + wave;
-    if (nt < t1) load(wa, nt);
+    if (nt < t1) load(wa, ba, nt);
     for (; nt < t1; nt += 2 * TW) {
         const int n2 = nt + TW;
-        if (n2 < t1) load(wb, n2);
-        do_tile(wa, nt);
+        if (n2 < t1) load(wb, bb, n2);
+        do_tile(wa, ba, nt);
         if (n2 >= t1) break;
-        if (n2 + TW < t1) load(wa, n2 + TW);
-        do_tile(wb, n2);
+        if (n2 + TW < t1) load(wa, ba, n2 + TW);
+        do_tile(wb, bb, n2);
     }
 #pragma unroll
     for (int j = 0; j < 4; j++)
