@@ -664,28 +664,40 @@ __global__ __launch_bounds__(TTHR) void k_amp_headbwd(AmpDev d, const int32_t* _
     // a vmcnt(0) there would drain the ring's in-flight refills)
     const bool gw = NACT == TW || wave < NACT;
     const int nt0 = wave * NT;
-    float4 ring[RD][NT];
-    if (gw) {  // the first slices of Wpi^T stream in while the gradient block is built
-#pragma unroll
-        for (int s = 0; s < RD; s++)
-#pragma unroll
-            for (int t = 0; t < NT; t++)
-                ring[s][t] = s < ns ? d.wpit[((long)(nt0 + t) * PKS + ks0 + s) * 64 + lane] : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
     if (tid < TR) {
         const int row = row0 + tid;
         LSE[tid] = row < B ? d.lse[row] : 0.f;
         TG[tid] = row < B ? tgt_all[idx ? idx[row] : row] : -1;
     }
+    // this part's logits first (every thread's, unconditionally, clamped), then the first slices
+    // of Wpi^T: the gradient block then waits for the logits only (vmcnt retires in order)
+    const int W = ns * 32;
+    constexpr int LPT = (TR * SPMAX * 32 + TTHR - 1) / TTHR;  // logits per thread
+    float lg[LPT];
+#pragma unroll
+    for (int k = 0; k < LPT; k++) {
+        const int i = tid + TTHR * k, r = min(i / W, TR - 1), c = i - (i / W) * W;
+        const int row = min(row0 + r, B - 1), a = min(32 * ks0 + c, ASIZE - 1);
+        lg[k] = d.logits[(long)row * LDL + a];
+    }
+    float4 ring[RD][NT];
+    if (gw) {  // the first slices of Wpi^T stream in while the gradient block is built
+#pragma unroll
+        for (int s = 0; s < RD; s++)
+#pragma unroll
+            for (int t = 0; t < NT; t++) ring[s][t] = d.wpit[((long)(nt0 + t) * PKS + min(ks0 + s, PKS - 1)) * 64 + lane];
+    }
     __syncthreads();
     const float S = d.sc->scale, invB = 1.0f / (float)B;
-    const int W = ns * 32;
-    for (int i = tid; i < TR * W; i += TTHR) {
-        const int r = i / W, c = i - r * W, a = 32 * ks0 + c, row = row0 + r;
-        float g = 0.f;
-        if (row < B && a < ASIZE)
-            g = r16(S * (expf(d.logits[(long)row * LDL + a] - LSE[r]) - (a == TG[r] ? 1.0f : 0.0f)) * invB);
-        DL[r * SD + c] = (_Float16)g;
+#pragma unroll
+    for (int k = 0; k < LPT; k++) {
+        const int i = tid + TTHR * k;
+        if (i < TR * W) {
+            const int r = i / W, c = i - r * W, a = 32 * ks0 + c, row = row0 + r;
+            float g = 0.f;
+            if (row < B && a < ASIZE) g = r16(S * (expf(lg[k] - LSE[r]) - (a == TG[r] ? 1.0f : 0.0f)) * invB);
+            DL[r * SD + c] = (_Float16)g;
+        }
     }
     lds_barrier();
     write_tl(DL, SD, 0, W, d.dlT, d.RS, 2 * ks0, tile, row0 + TR >= B && (tile & 1) == 0);
@@ -704,15 +716,17 @@ __global__ __launch_bounds__(TTHR) void k_amp_headbwd(AmpDev d, const int32_t* _
 #pragma unroll
         for (int j = 0; j < RD; j++) {  // static ring slots
             const int k = k0 + j;
-            if (k < ns) {
-                const float4 a = *reinterpret_cast<const float4*>(ap + 32 * k);
+            const float4 a = *reinterpret_cast<const float4*>(ap + 32 * min(k, SPMAX - 1));
+            const bool on = k < ns;  // (a select, not a branch: the refills below stay unconditional)
 #pragma unroll
-                for (int t = 0; t < NT; t++) acc[t] = mfma(a, ring[j][t], acc[t]);
-                if (k + RD < ns) {
-#pragma unroll
-                    for (int t = 0; t < NT; t++) ring[j][t] = d.wpit[((long)(nt0 + t) * PKS + ks0 + k + RD) * 64 + lane];
-                }
+            for (int t = 0; t < NT; t++) {
+                const floatx4 r = mfma(a, ring[j][t], acc[t]);
+                acc[t] = on ? r : acc[t];
             }
+#pragma unroll
+            for (int t = 0; t < NT; t++)  // clamped; unused past the part's slices
+                ring[j][t] = d.wpit[((long)(nt0 + t) * PKS + min(ks0 + k + RD, PKS - 1)) * 64 + lane];
+            __builtin_amdgcn_sched_barrier(0);
         }
     }
     const int r = lane & 15, q = lane >> 4;
