@@ -1231,21 +1231,43 @@ __global__ __launch_bounds__(256) void k_amp_update(const UpdJob* __restrict__ j
     }
     const int r = t >> 3, c = (t & 7) * 4;
     const int n = it.n0 + r;
+    const long o4 = (long)n * jb.K + it.k0 + c;
+    const bool vec = (jb.K & 3) == 0 && n < jb.N && it.k0 + c + 3 < jb.K &&
+                     ((reinterpret_cast<uintptr_t>(jb.W) | reinterpret_cast<uintptr_t>(jb.Gm) |
+                       reinterpret_cast<uintptr_t>(jb.Mm) | reinterpret_cast<uintptr_t>(jb.Vm)) & 15) == 0;
+    if (vec) {  // 16-byte aligned rows: four elements per load
+        const long o = o4;
+        float4 p = *reinterpret_cast<const float4*>(jb.W + o), g = *reinterpret_cast<const float4*>(jb.Gm + o);
+        float4 m = *reinterpret_cast<const float4*>(jb.Mm + o), v = *reinterpret_cast<const float4*>(jb.Vm + o);
+        adamw_elem(p.x, g.x, m.x, v.x, inv, coef, decay, b1, b2, eps, step_size, bc2_sqrt);
+        adamw_elem(p.y, g.y, m.y, v.y, inv, coef, decay, b1, b2, eps, step_size, bc2_sqrt);
+        adamw_elem(p.z, g.z, m.z, v.z, inv, coef, decay, b1, b2, eps, step_size, bc2_sqrt);
+        adamw_elem(p.w, g.w, m.w, v.w, inv, coef, decay, b1, b2, eps, step_size, bc2_sqrt);
+        *reinterpret_cast<float4*>(jb.W + o) = p;
+        *reinterpret_cast<float4*>(jb.Gm + o) = g;
+        *reinterpret_cast<float4*>(jb.Mm + o) = m;
+        *reinterpret_cast<float4*>(jb.Vm + o) = v;
+        Tl[r][c] = (_Float16)p.x;
+        Tl[r][c + 1] = (_Float16)p.y;
+        Tl[r][c + 2] = (_Float16)p.z;
+        Tl[r][c + 3] = (_Float16)p.w;
+    } else {
 #pragma unroll
-    for (int i = 0; i < 4; i++) {
-        const int k = it.k0 + c + i;
-        float pv = 0.f;
-        if (n < jb.N && k < jb.K) {
-            const long o = (long)n * jb.K + k;
-            float p = jb.W[o], g = jb.Gm[o], m = jb.Mm[o], v = jb.Vm[o];
-            adamw_elem(p, g, m, v, inv, coef, decay, b1, b2, eps, step_size, bc2_sqrt);
-            jb.W[o] = p;
-            jb.Gm[o] = g;
-            jb.Mm[o] = m;
-            jb.Vm[o] = v;
-            pv = p;
+        for (int i = 0; i < 4; i++) {
+            const int k = it.k0 + c + i;
+            float pv = 0.f;
+            if (n < jb.N && k < jb.K) {
+                const long o = (long)n * jb.K + k;
+                float p = jb.W[o], g = jb.Gm[o], m = jb.Mm[o], v = jb.Vm[o];
+                adamw_elem(p, g, m, v, inv, coef, decay, b1, b2, eps, step_size, bc2_sqrt);
+                jb.W[o] = p;
+                jb.Gm[o] = g;
+                jb.Mm[o] = m;
+                jb.Vm[o] = v;
+                pv = p;
+            }
+            Tl[r][c + i] = (_Float16)pv;
         }
-        Tl[r][c + i] = (_Float16)pv;
     }
     __syncthreads();
     const int f = (t >> 6) & 1, l = t & 63;
