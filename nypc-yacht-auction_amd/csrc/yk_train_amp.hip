@@ -296,8 +296,14 @@ __global__ __launch_bounds__(TTHR) void k_amp_fwd(AmpDev d, const yk_state_t* __
 #pragma unroll
             for (int t = 0; t < NT; t++) w0[s][t] = d.win_f[((long)(nt0 + t) * 2 + s) * 64 + lane];
     }
+    // the heads' LayerNorm affines, needed after the trunk: loaded now, ahead of the weight stream
+    float hg[4][VPL];
+#pragma unroll
+    for (int v = 0; v < 4; v++)
+#pragma unroll
+        for (int i = 0; i < VPL; i++) hg[v][i] = d.P[poff(H, d.NB, t_head(NB, v == 0 ? HP_G : v == 1 ? HP_B : v == 2 ? HV_G : HV_B)) + c0 + i];
     float4 ring[RW][NT];
-    if (gw && NB > 0) ring_fill<KS, NT, RW>(ring, d.w1f, nt0);
+    if (gw) ring_fill<KS, NT, RW>(ring, NB > 0 ? d.w1f : d.wpif, nt0);  // (whatever NB is: no branch join)
 #pragma unroll
     for (int k = 0; k < 2; k++) {  // state_to_vec (NNet.py:65-86), K padded to 64
         const int r = wave + TW * k, row = row0 + r;
@@ -434,10 +440,6 @@ __global__ __launch_bounds__(TTHR) void k_amp_fwd(AmpDev d, const yk_state_t* __
     // the heads' LayerNorms (one set of statistics, two affine maps) -> SiLU: a_pi, a_v (f32),
     // cast to fp16 for pi_head.2 / v_head.2  YachtNNet.py:40-52
     _Float16* Pv = reinterpret_cast<_Float16*>(Ts);
-    const float* gp = d.P + poff(H, d.NB, t_head(NB, HP_G));
-    const float* bp = d.P + poff(H, d.NB, t_head(NB, HP_B));
-    const float* gv = d.P + poff(H, d.NB, t_head(NB, HV_G));
-    const float* bv = d.P + poff(H, d.NB, t_head(NB, HV_B));
     lds_barrier();  // every wave is done reading Ts
 #pragma unroll
     for (int rr = 0; rr < TRPW; rr++) {
@@ -456,8 +458,8 @@ __global__ __launch_bounds__(TTHR) void k_amp_fwd(AmpDev d, const yk_state_t* __
             for (int i = 0; i < VPL; i++) {
                 d.hF[(long)row * H + c0 + i] = x[i];
                 const float xh = (x[i] - mu) * rs;
-                Pa[r * SA + c0 + i] = (_Float16)silu(xh * gp[c0 + i] + bp[c0 + i]);
-                Pv[r * SA + c0 + i] = (_Float16)silu(xh * gv[c0 + i] + bv[c0 + i]);
+                Pa[r * SA + c0 + i] = (_Float16)silu(xh * hg[0][i] + hg[1][i]);
+                Pv[r * SA + c0 + i] = (_Float16)silu(xh * hg[2][i] + hg[3][i]);
             }
         } else {
 #pragma unroll
@@ -820,11 +822,10 @@ __global__ __launch_bounds__(TTHR) void k_amp_bwd(AmpDev d, int B, float p, uint
 #pragma unroll
             for (int t = 0; t < NT; t++) wv[s][t] = d.wv1t[((long)(nt0 + t) * 4 + s) * 64 + lane];
     }
-    for (int i = tid; i < TR * VH / 8; i += TTHR) {
+    for (int i = tid; i < TR * VH / 8; i += TTHR) {  // (clamped loads, zeroed by a select: no branch)
         const int r = i / (VH / 8), c8 = i % (VH / 8), row = row0 + r;
-        const float4 v = row < B ? reinterpret_cast<const float4*>(d.dz1_rm + (long)row * VH)[c8]
-                                 : make_float4(0.f, 0.f, 0.f, 0.f);
-        *reinterpret_cast<float4*>(Pa + r * SV + 8 * c8) = v;
+        const float4 v = reinterpret_cast<const float4*>(d.dz1_rm + (long)min(row, B - 1) * VH)[c8];
+        *reinterpret_cast<float4*>(Pa + r * SV + 8 * c8) = row < B ? v : make_float4(0.f, 0.f, 0.f, 0.f);
     }
     lds_barrier();
     floatx4 acc[NT];
@@ -865,12 +866,13 @@ __global__ __launch_bounds__(TTHR) void k_amp_bwd(AmpDev d, int B, float p, uint
         gv[i] = d.P[poff(H, NB, t_head(NB, HV_G)) + c0 + i];
         bv[i] = d.P[poff(H, NB, t_head(NB, HV_B)) + c0 + i];
     }
-    RowPre<VPL> R;
-    if (NB > 0) row_prefetch<H>(R, d, d.u2 + (long)(NB - 1) * d.Bmax * H, 2 * NB, t_blk(NB - 1, 6), t_blk(NB - 1, 7), row0, B);
-    else row_prefetch<H>(R, d, d.z0, 0, T_GIN, T_BEIN, row0, B);
+    RowPre<VPL> R;  // (one call on selected operands, and the ring filled whatever NB is - from a large
+                    // enough matrix when NB = 0 - so no branch joins before the heads pass's waits)
+    row_prefetch<H>(R, d, NB > 0 ? d.u2 + (long)(NB - 1) * d.Bmax * H : d.z0, NB > 0 ? 2 * NB : 0,
+                    NB > 0 ? t_blk(NB - 1, 6) : (int)T_GIN, NB > 0 ? t_blk(NB - 1, 7) : (int)T_BEIN, row0, B);
     __builtin_amdgcn_sched_barrier(0);
     float4 ring[RW][NT];
-    if (gw && NB > 0) ring_fill<KS, NT, RW>(ring, d.w2t + (NB - 1) * HH8, nt0);
+    if (gw) ring_fill<KS, NT, RW>(ring, NB > 0 ? d.w2t + (NB - 1) * HH8 : d.wpit, nt0);
     lds_barrier();
     // heads backward (YachtNNet.py:40-52): dT = dA SiLU'(T) for both heads (f32), one LayerNorm
     // backward over the shared statistics -> dh
