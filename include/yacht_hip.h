@@ -313,6 +313,12 @@ int yk_trainer_step(yk_trainer_t* t, const yk_state_t* states, const int32_t* ta
                     const int32_t* batch_idx, int batch, void* stream);
 /* HOST out[3]: sum over the last batch of cross-entropy, of squared value error; grad sq-norm */
 int yk_trainer_losses(yk_trainer_t* t, double* out);
+/* a reporting epoch's "Avg Loss" (NNet.py:150-160) without a host round trip per minibatch:
+ * begin zeroes a device accumulator; every later yk_trainer_backward adds its batch's
+ * ce/b + vloss_weight*se/b to it (one 1-thread launch on that stream) until end, which
+ * synchronises and writes HOST out[2] = (sum of those batch losses, batches) */
+int yk_trainer_epoch_loss_begin(yk_trainer_t* t, double vloss_weight);
+int yk_trainer_epoch_loss_end(yk_trainer_t* t, double* out);
 /* copy parameters (which 0), gradients (1), exp_avg (2), exp_avg_sq (3) to / from HOST arrays in
  * state_dict order (NULL entries skipped); set: step >= 0 also sets the optimiser step count */
 int yk_trainer_get(yk_trainer_t* t, int which, float* const* out);

@@ -480,6 +480,9 @@ struct yk_trainer {
     double* sqpart = nullptr;  // k_sqnorm partials
     float2* lrow = nullptr;    // per-row (ce, squared value error) of the last batch
     float* lsum = nullptr;     // their column sums (k_colsums)
+    double* eloss = nullptr;   // report epoch: [0] sum of per-batch mean losses, [1] batches (k_epoch_loss)
+    bool eloss_on = false;
+    double eloss_vw = 1.0;
     double host_loss[3] = {0, 0, 0};
     int64_t row_base = 0;        // global row of the next backward's first example (dropout)
     yk::AmpTrain* amp = nullptr;  // mixed-precision mode (yk_train_amp.hip)
@@ -668,6 +671,7 @@ int yk_trainer_create(yk_trainer_t** out, int H, int NB, const float* const* par
     TA(t->sqpart, SQ_BLOCKS);
     TA(t->lrow, Bm);
     TA(t->lsum, 2);
+    TA(t->eloss, 2);
     // the column-sum jobs: (row buffer, gradient tensor, width)
     std::vector<ColJob> jobs;
     if (rc == YK_OK) {
@@ -752,11 +756,8 @@ int yk_trainer_buffers(yk_trainer_t* t, float** params, float** grads, int64_t* 
     return YK_OK;
 }
 
-int yk_trainer_backward(yk_trainer_t* t, const yk_state_t* states, const int32_t* targets, const float* values,
-                        const int32_t* batch_idx, int batch, void* stream) {
-    if (!t || !states || !targets || !values) return YK_ERR_ARG;
-    if (batch <= 0 || batch > t->Bmax) return YK_ERR_ARG;
-    hipStream_t s = as_stream(stream);
+static int backward_impl(yk_trainer_t* t, const yk_state_t* states, const int32_t* targets, const float* values,
+                         const int32_t* batch_idx, int batch, hipStream_t s) {
     if (t->amp)
         return yk::amp_backward(t->amp, states, targets, values, batch_idx, batch, t->cfg.dropout, t->cfg.seed, t->step,
                                 t->row_base, t->cfg.vloss_weight, t->lrow, t->lsum, s);
@@ -768,6 +769,44 @@ int yk_trainer_backward(yk_trainer_t* t, const yk_state_t* states, const int32_t
         case 512: return step_impl<8>(t, states, targets, values, batch_idx, batch, s);
     }
     return YK_ERR_ARG;
+}
+
+// one report epoch's running loss, kept on the device so a reporting epoch takes no host
+// round trip per minibatch: += ce/b + vw*se/b, in the order NNet.py:150-152's float sum takes
+__global__ void k_epoch_loss(const float* lsum, double* eloss, double b, double vw) {
+    if (threadIdx.x == 0) {
+        eloss[0] += (double)lsum[0] / b + vw * (double)lsum[1] / b;
+        eloss[1] += 1.0;
+    }
+}
+
+int yk_trainer_backward(yk_trainer_t* t, const yk_state_t* states, const int32_t* targets, const float* values,
+                        const int32_t* batch_idx, int batch, void* stream) {
+    if (!t || !states || !targets || !values) return YK_ERR_ARG;
+    if (batch <= 0 || batch > t->Bmax) return YK_ERR_ARG;
+    hipStream_t s = as_stream(stream);
+    int rc = backward_impl(t, states, targets, values, batch_idx, batch, s);
+    if (rc == YK_OK && t->eloss_on) {
+        hipLaunchKernelGGL(k_epoch_loss, dim3(1), dim3(64), 0, s, t->lsum, t->eloss, (double)batch, t->eloss_vw);
+        YK_LAUNCHED();
+    }
+    return rc;
+}
+
+int yk_trainer_epoch_loss_begin(yk_trainer_t* t, double vloss_weight) {
+    if (!t) return YK_ERR_ARG;
+    YK_HIP(hipMemset(t->eloss, 0, sizeof(double) * 2));
+    t->eloss_on = true;
+    t->eloss_vw = vloss_weight;
+    return YK_OK;
+}
+
+int yk_trainer_epoch_loss_end(yk_trainer_t* t, double* out) {
+    if (!t || !out) return YK_ERR_ARG;
+    t->eloss_on = false;
+    YK_HIP(hipDeviceSynchronize());
+    YK_HIP(hipMemcpy(out, t->eloss, sizeof(double) * 2, hipMemcpyDeviceToHost));
+    return YK_OK;
 }
 
 int yk_trainer_apply(yk_trainer_t* t, void* stream) {

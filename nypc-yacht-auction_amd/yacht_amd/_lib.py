@@ -75,6 +75,8 @@ SIGNATURES = {
     "yk_trainer_apply": [P, P],
     "yk_trainer_step": [P, P, P, P, P, I, P],
     "yk_trainer_losses": [P, P],
+    "yk_trainer_epoch_loss_begin": [P, C.c_double],
+    "yk_trainer_epoch_loss_end": [P, P],
     "yk_trainer_get": [P, I, P],
     "yk_trainer_set": [P, I, P, C.c_int64],
     "yk_trainer_step_count": [P],

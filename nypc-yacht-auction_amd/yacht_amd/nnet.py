@@ -215,7 +215,8 @@ class NNetWrapper:
         for epoch in range(self.args.epochs):
             perm = torch.randperm(n, generator=g, device="cuda").to(torch.int32)
             report = verbose and (epoch % 5 == 0 or epoch == self.args.epochs - 1)
-            total, count = 0.0, 0
+            if report:
+                tr.epoch_loss_begin(vw)  # summed on the device, read once after the epoch
             for i in range(0, n, rows):
                 idx = perm[i:i + rows]
                 if mode == "replicated":
@@ -232,12 +233,10 @@ class NNetWrapper:
                         tr.grads().zero_()
                     D.allreduce_grads(tr, weight=b / idx.numel())
                     tr.apply()
-                if report and b:
-                    ce, se, _ = tr.losses()
-                    total += ce / b + vw * se / b
-                    count += 1
-            if report and rank == 0:
-                print(f"Epoch {epoch + 1}/{self.args.epochs}, Avg Loss: {total / max(count, 1):.4f}")
+            if report:
+                total, count = tr.epoch_loss_end()
+                if rank == 0:
+                    print(f"Epoch {epoch + 1}/{self.args.epochs}, Avg Loss: {total / max(count, 1):.4f}")
         with torch.no_grad():
             self.nnet.load_state_dict(tr.state_dict())  # the torch copy feeds checkpoints and predict
         self._yk = None

@@ -88,6 +88,16 @@ class Trainer:
         call("yk_trainer_losses", self.handle, out.ctypes.data)
         return out
 
+    def epoch_loss_begin(self, vloss_weight: float):
+        """Start a device-side running sum of every later backward's ce/b + vw*se/b."""
+        call("yk_trainer_epoch_loss_begin", self.handle, float(vloss_weight))
+
+    def epoch_loss_end(self):
+        """(sum of the batch losses since epoch_loss_begin, number of batches); synchronises."""
+        out = np.zeros(2, dtype=np.float64)
+        call("yk_trainer_epoch_loss_end", self.handle, out.ctypes.data)
+        return float(out[0]), int(out[1])
+
     @property
     def step_count(self) -> int:
         """Optimiser steps taken (amp: skipped steps are not counted, as torch's AdamW state)."""

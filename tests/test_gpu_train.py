@@ -96,6 +96,8 @@ def test_three_steps_vs_torch_fp32(T, golden):
     X = K.featurize(S)
     tg = torch.tensor(rng.randint(0, 3226, 3 * B), dtype=torch.int32, device="cuda")
     vv = torch.tensor(rng.rand(3 * B) * 2 - 1, dtype=torch.float32, device="cuda")
+    tr.epoch_loss_begin(1.5)
+    total = 0.0
     for k in range(3):
         sl = slice(k * B, (k + 1) * B)
         idx = torch.arange(k * B, (k + 1) * B, dtype=torch.int32, device="cuda")
@@ -103,6 +105,9 @@ def test_three_steps_vs_torch_fp32(T, golden):
         lp, lv = _torch_step_reference(model, opt, X[sl], tg[sl], vv[sl])
         ce, se, _ = tr.losses()
         assert abs(ce / B - lp) <= 1e-5 * abs(lp) + 1e-6 and abs(se / B - lv) <= 1e-5 * abs(lv) + 1e-6
+        total += ce / B + 1.5 * se / B
+    # the device-side report-epoch sum (NNetWrapper.train's "Avg Loss") is the host sum, bit for bit
+    assert tr.epoch_loss_end() == (total, 3)
     # gradients and moments: per-tensor relative error (f32 reductions in another order through
     # 13 layers); parameters: the update p - p0 agrees to 0.1 % in norm, and at most 1e-4 of the
     # weights are off by more than 0.5 % of one AdamW step (1e-5): Adam normalises each element,
