@@ -18,6 +18,7 @@ YachtNNet (kaiming-uniform per YachtNNet._init, seed 0, hidden 256, 6 blocks).
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import os
 import sys
@@ -492,7 +493,8 @@ def main():
         img = last_gather[0] if world > 1 else eng.pack_records(stream=stream)
         coach = coach_leg(model, img, args.envs, 64, args.sims, world, seed=args.seed)
         del img
-        coach["iteration"] = coach_iter_leg(model, world, games_per_gpu=args.coach_games, seed=args.seed)
+        with contextlib.redirect_stdout(sys.stderr):  # Coach.learn's progress lines: stdout is the JSON line
+            coach["iteration"] = coach_iter_leg(model, world, games_per_gpu=args.coach_games, seed=args.seed)
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()
