@@ -55,8 +55,13 @@ struct NodeRec {          // 96 bytes
 struct Edge {             // 16 bytes
     double Q;
     uint32_t N;
-    uint32_t tag;
+    uint32_t tag;         // [0:2) python value kind of Q; [2:32) child node id + 1 when the edge's
+                          // transition draws no dice (0: not known) - a revisit then skips the
+                          // step, the canonical form and the index probe (section 6)
 };
+__device__ __forceinline__ uint32_t edge_kind(uint32_t tag) { return tag & 3u; }
+constexpr uint32_t PATH_DET = 0x80000000u;  // path entry low word: node id | PATH_DET when the
+                                            // level's transition consumed no random draw
 
 struct EngDev {
     int E, NCAP, HCAP, ECAP, M, VCAP;
@@ -100,6 +105,7 @@ struct EngDev {
     uint8_t* leaf_flag;
     uint64_t* path;        // [E][MAXD]: (p_off + j) << 32 | node id
     uint8_t* path_len;
+    uint32_t* end_node;    // [E] id + 1 of the node the descent stopped at (no valid action), else 0
     double* res_v;
     uint32_t* res_t;
     const float* logits;   // [E][PI_LD]
@@ -455,7 +461,9 @@ __global__ __launch_bounds__(256) void k_move_begin(EngDev d, int move, int exte
             const uint32_t before = __popcll(bal & ((1ull << lane) - 1));
             uint16_t nsl = 0;
             if (vis) {
-                edst[ne + before] = esrc[sl - 1];
+                Edge x = esrc[sl - 1];
+                x.tag = edge_kind(x.tag);  // node ids change: the cached child is dropped
+                edst[ne + before] = x;
                 nsl = (uint16_t)(ne + before + 1);
             }
             ne += (uint32_t)__popcll(bal);
@@ -509,6 +517,7 @@ __device__ __forceinline__ void select_game(const EngDev& d, int e, int lane, co
         if (lane == 0) {
             d.leaf_flag[e] = 0;
             d.path_len[e] = 0;
+            d.end_node[e] = 0;
         }
         return;
     }
@@ -524,10 +533,17 @@ __device__ __forceinline__ void select_game(const EngDev& d, int e, int lane, co
     int depth = 0;
     uint64_t scanned = 0;
     int leaf = 0;
+    int known = -1;        // the node this level's state is, when the edge taken to it cached it
+    uint32_t end_id = 0;   // id + 1 of a node the descent stops at
     PyV res{0.0, T_INT};
     SEL_T0(t_all);
     while (true) {
         SEL_T0(t_lv);
+        if (known >= 0) {  // the cached child: its key is the state step + canonical would give
+            const uint64_t* kp = nodes[known].key;
+#pragma unroll
+            for (int i = 0; i < 8; i++) s.w[i] = kp[i];
+        }
         const double es = game_ended(s, 1);  // Es (MCTS.py:78-82)
         if (es != 0.0) {
             res = PyV{-es, T_F64};
@@ -542,8 +558,8 @@ __device__ __forceinline__ void select_game(const EngDev& d, int e, int lane, co
             rc1 = d.root_c[2 * t + 1];
         }
         const bool cached = rc0.x != 0;
-        const uint64_t hsh = cached ? 0ull : index_hash(s);
-        const int nid = cached ? (int)rc0.x - 1 : lookup(d, g, t, s, hsh);
+        const uint64_t hsh = (cached || known >= 0) ? 0ull : index_hash(s);
+        const int nid = cached ? (int)rc0.x - 1 : known >= 0 ? known : lookup(d, g, t, s, hsh);
         SEL_ACC(0, t_lv);
         if (nid < 0) {  // leaf: predict (MCTS.py:84-115)
             leaf = 1;
@@ -563,6 +579,7 @@ __device__ __forceinline__ void select_game(const EngDev& d, int e, int lane, co
         }
         if (V == 0) {  // no valid action: MCTS.py:141-147 returns 0 (python int)
             res = PyV{0.0, T_INT};
+            end_id = (uint32_t)nid + 1;
             break;
         }
         // UCB argmax, MCTS.py:117-135: float32 arithmetic, strict '>' => lowest action wins
@@ -577,6 +594,7 @@ __device__ __forceinline__ void select_game(const EngDev& d, int e, int lane, co
         const uint16_t* S = Sbase + p_off;
         float best = -INFINITY;
         int bj = 0x7FFFFFFF;
+        uint32_t btag = 0;  // the edge tag of the lane's best entry (0: unvisited)
         // software-pipelined scan: iteration it+1's P / slot loads fly while iteration it's
         // visited-edge gathers resolve
         float4 p4 = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -610,6 +628,7 @@ __device__ __forceinline__ void select_game(const EngDev& d, int e, int lane, co
                     if (u > best) {
                         best = u;
                         bj = j;
+                        btag = sv[t] ? ev[t].tag : 0u;
                     }
                 }
             }
@@ -627,18 +646,37 @@ __device__ __forceinline__ void select_game(const EngDev& d, int e, int lane, co
         SEL_ACC(1, t_sc);
         SEL_T0(t_st);
         int j = bj;
+        // the winner's lane holds its tag: its own best is the wave's (lowest j among equals)
+        const uint32_t wtag = __builtin_amdgcn_readlane(btag, __builtin_amdgcn_readfirstlane((j & 255) >> 2));
         if (j == 0x7FFFFFFF) j = 0;  // MCTS.py:138-143: first valid action
         if (depth >= MAXD) {
             if (lane == 0) atomicOr(d.err, ERR_DEPTH);
             res = PyV{0.0, T_INT};
             break;
         }
-        if (lane == 0) path[depth] = ((uint64_t)(p_off + (uint32_t)j) << 32) | (uint32_t)nid;
-        depth++;
+#ifdef YK_SEL_TIMING
+        if (lane == 0) {
+            g_sel[(long)e * 16 + 4] += 1;
+            g_sel[(long)e * 16 + 5] += (unsigned long long)V;
+        }
+#endif
+        const uint32_t child = bj == 0x7FFFFFFF ? 0u : (wtag >> 2);  // id + 1, 0: not cached
+        if (child) {  // a deterministic transition taken before: the child node is known
+            if (lane == 0) path[depth] = ((uint64_t)(p_off + (uint32_t)j) << 32) | (uint32_t)nid | PATH_DET;
+            depth++;
+            known = (int)child - 1;
+            SEL_ACC(2, t_st);
+            continue;
+        }
+        known = -1;
         const VInfo vi = unpack_vinfo(vinfo, (uint32_t)V);
         const int a = compact_to_action(vi, j);
         int np = 1;
+        const uint64_t ctr0 = rs.ctr;
         const int st = step_state<true>(s, 1, a, rs, np);  // MCTS.py:149 (all lanes: wave-parallel dice)
+        const uint32_t det = rs.ctr == ctr0 ? PATH_DET : 0u;  // no dice drawn: the child is a function of (s, a)
+        if (lane == 0) path[depth] = ((uint64_t)(p_off + (uint32_t)j) << 32) | (uint32_t)nid | det;
+        depth++;
         if (st != YK_ST_OK) {
             if (lane == 0) atomicOr(d.err, ERR_STEP);
             res = PyV{0.0, T_INT};
@@ -646,17 +684,12 @@ __device__ __forceinline__ void select_game(const EngDev& d, int e, int lane, co
         }
         s = canonical(s, np);  // MCTS.py:150
         SEL_ACC(2, t_st);
-        if (lane == 0) {
-#ifdef YK_SEL_TIMING
-            g_sel[(long)e * 16 + 4] += 1;
-            g_sel[(long)e * 16 + 5] += (unsigned long long)V;
-#endif
-        }
     }
     SEL_ACC(3, t_all);
     if (lane == 0) {
         d.leaf_flag[e] = (uint8_t)(leaf ? (t < d.E ? 1 : 2) : 0);  // which net predicts it (dual trees)
         d.path_len[e] = (uint8_t)depth;
+        d.end_node[e] = end_id;
         d.res_v[e] = res.v;
         d.res_t[e] = res.t;
         ctr_arr[e] = rs.ctr;
@@ -724,6 +757,7 @@ __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int l
     const int t = tree_of(d, e);
     const int g = d.gen[t];
     PyV res{d.res_v[e], d.res_t[e]};
+    uint32_t end_id = 0;  // id + 1 of the node the path's last edge leads to, if any
     if (d.leaf_flag[e]) {
         SEL_T0(t_x0);
         const YkS s = ld_state(d.leaf_state + e);
@@ -921,6 +955,9 @@ __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int l
                 r.pad = 0;
                 d.nodes[g][(long)t * d.NCAP + nid] = r;
                 if (!insert_index(d, g, t, ihsh, nid)) atomicOr(d.err, ERR_HASH);
+            }
+            end_id = nid + 1;
+            if (lane == 0) {
                 d.node_count[g * d.T + t] = nid + 1;
                 d.arena_top[t] = off + (uint32_t)VP;
                 uint64_t* gs = d.gstats + (long)e * 8;
@@ -931,6 +968,8 @@ __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int l
             }
         }
         res = PyV{-(double)v, T_F32};  // return -v  (MCTS.py:115)
+    } else {
+        end_id = d.end_node[e];
     }
     // ---- backup (MCTS.py:154-164): the path's nodes are distinct, so every level updates in
     // parallel; level k receives v * (-1)^(depth-1-k) ("return -v" per level).
@@ -948,6 +987,12 @@ __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int l
             pe = path[lane];
             sl = Sb[pe >> 32];
         }
+        // the child each level's edge leads to: the next level's node, or for the last edge the
+        // node the descent ended at (the new leaf, or a node without valid actions); cached in
+        // the edge's tag when that transition drew no dice
+        const uint32_t pnext = __shfl((uint32_t)pe, (lane + 1) & 63, 64);
+        const uint32_t cnode = lane + 1 < depth ? (pnext & ~PATH_DET) + 1 : end_id;
+        const uint32_t cbits = ((uint32_t)pe & PATH_DET) ? cnode << 2 : 0u;
         const bool is_new = lane < depth && sl == 0;
         const uint64_t bal = __ballot(is_new);
         const uint32_t eid = ne0 + (uint32_t)__popcll(bal & ((1ull << lane) - 1));
@@ -957,17 +1002,17 @@ __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int l
             if ((depth - 1 - lane) & 1) v.v = -v.v;
             if (sl) {
                 Edge& ed = edges[sl - 1];
-                const PyV q = pv_update(PyV{ed.Q, ed.tag}, ed.N, v);
+                const PyV q = pv_update(PyV{ed.Q, edge_kind(ed.tag)}, ed.N, v);
                 ed.Q = q.v;
-                ed.tag = q.t;
+                ed.tag = q.t | cbits;
                 ed.N += 1;
             } else if (eid < (uint32_t)d.ECAP && eid < 65535u) {
-                edges[eid] = Edge{v.v, 1u, v.t};
+                edges[eid] = Edge{v.v, 1u, v.t | cbits};
                 Sb[pe >> 32] = (uint16_t)(eid + 1);
             } else {
                 atomicOr(d.err, ERR_EDGES);
             }
-            nodes[(uint32_t)pe].Ns += 1;
+            nodes[(uint32_t)pe & ~PATH_DET].Ns += 1;
         }
         if (lane == 0) {
             d.edge_count[g * d.T + t] = ne1;
@@ -1481,6 +1526,7 @@ int yk_engine_create(yk_engine_t** out, const yk_engine_config_t* cfg, yk_net_t*
     A(d.leaf_flag, E);
     A(d.path, E * MAXD);
     A(d.path_len, E);
+    A(d.end_node, E);
     A(d.res_v, E);
     A(d.res_t, E);
     A(eng->vpred, E);

@@ -53,6 +53,9 @@ __device__ unsigned long long g_tstamp[4096 * 32];
 // [0] workgroups, [1] sum of needed tiles, [2] rows, [3] bid-only workgroups, [4] sum over launches
 // of the launch's max, [5] this launch's max, [6] launches, [8 + k] histogram of tiles / 32
 __device__ unsigned long long g_tiles[16];
+// every YK_VD_EVERY-th valid-only launch: each row's logit descriptor (tools/diag_sort.py)
+constexpr int VD_SAMPLES = 64, VD_ROWS = 8192, YK_VD_EVERY = 75;
+__device__ uint32_t g_vdump[VD_SAMPLES][VD_ROWS];
 __global__ void k_tilestat_flush() {
     g_tiles[4] += g_tiles[5];
     g_tiles[5] = 0;
@@ -912,6 +915,11 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
     lds_barrier();
     TSTAMP(9);
 #ifdef YK_TILESTAT
+    if (valid_only && tid < ROWS) {
+        const unsigned long long li = g_tiles[6];
+        if (li % YK_VD_EVERY == 0 && li / YK_VD_EVERY < VD_SAMPLES && row0 + tid < VD_ROWS && part == 0)
+            g_vdump[li / YK_VD_EVERY][row0 + tid] = VD[tid];
+    }
     if (tid == 0 && valid_only) {
         uint32_t m[7] = {0, 0, 0, 0, 0, 0, 0};  // 204 tile bits
         auto set = [&](int c0, int c1) {       // columns c0 .. c1 inclusive
@@ -1282,6 +1290,11 @@ int yk_diag_tiles(uint64_t* out) {  // HOST out[16]; resets the counters
     YK_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tiles), sizeof(uint64_t) * 16));
     const uint64_t z[16] = {};
     YK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_tiles), z, sizeof(z)));
+    return YK_OK;
+}
+int yk_diag_vdump(uint32_t* out) {  // HOST out[VD_SAMPLES * VD_ROWS]
+    YK_HIP(hipDeviceSynchronize());
+    YK_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_vdump), sizeof(uint32_t) * VD_SAMPLES * VD_ROWS));
     return YK_OK;
 }
 #endif
