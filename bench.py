@@ -35,6 +35,7 @@ SPLIT_PRODUCTS = 3             # k_forward: each f32 product = 3 fp16 MFMA produ
 SPLIT_PEAK_TFLOPS = F16_MFMA_PEAK_TFLOPS / SPLIT_PRODUCTS
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E spec peak
 H, NB, A = 256, 6, 3226
+GAME_MOVES = 48  # every Yacht Auction game has exactly 48 real moves: the record image's size
 # algorithmic FLOPs per expansion (one predicted row), YachtNNet.py:24-70 at hidden 256, 6 blocks
 PREDICT_FLOP = 2 * (59 * H + 2 * NB * H * H + H * 128 + 128 + H * A)  # = 3,320,576
 
@@ -363,8 +364,10 @@ def coach_leg(model, image, n_envs, max_moves, sims, world, train_steps=60, aren
     t_ar = time.perf_counter() - t2
     return {"config": f"pooled examples of the timed batch ({n} examples from {world} rank(s)); "
                       f"{train_steps} train steps of minibatch {bs} (every rank the whole minibatch: "
-                      f"ddp_batch replicated; clip 5.0, AdamW, dropout {args.dropout}, f32); gating arena {arena_games} games, "
+                      f"ddp_batch replicated; clip 5.0, AdamW, dropout {args.dropout}); gating arena {arena_games} games, "
                       f"{arena_sims} sims, previous vs new net on dual trees, sharded",
+            "train_mode": "amp (autocast + GradScaler on fp16 MFMA, NNet.py:113-116: args.cuda)" if new.uses_amp()
+                          else "f32",
             "examples": n, "examples_ms": 1000.0 * t_ex, "train_ms_per_step": 1000.0 * t_tr,
             "train_examples_per_s": bs / t_tr,
             "train_ms_per_step_split": None if t_split is None else 1000.0 * t_split,
@@ -416,11 +419,12 @@ def main():
     model = YachtNNet(hidden=H, nblocks=NB)  # random init of the reference architecture
     sd = model.state_dict()
     net = YkNet(sd, H, NB)
-    eng = SelfPlayEngine(args.envs, args.sims, 1.5, 15, net=net, max_moves=64, arena_entries=args.arena_entries,
+    eng = SelfPlayEngine(args.envs, args.sims, 1.5, 15, net=net, max_moves=GAME_MOVES, arena_entries=args.arena_entries,
                          groups=args.groups)
     stream = torch.cuda.current_stream()
     env_base = D.env_base(rank, args.envs)
     gathered_bytes = 0
+    image_bytes = 0
 
     last_gather = [None]
 
@@ -435,6 +439,7 @@ def main():
 
     for i in range(args.warmup):
         step(i)
+    image_bytes = int(eng.pack_records(stream=stream).numel())
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -491,7 +496,7 @@ def main():
     coach = None
     if not args.no_coach:
         img = last_gather[0] if world > 1 else eng.pack_records(stream=stream)
-        coach = coach_leg(model, img, args.envs, 64, args.sims, world, seed=args.seed)
+        coach = coach_leg(model, img, args.envs, GAME_MOVES, args.sims, world, seed=args.seed)
         del img
         with contextlib.redirect_stdout(sys.stderr):  # Coach.learn's progress lines: stdout is the JSON line
             coach["iteration"] = coach_iter_leg(model, world, games_per_gpu=args.coach_games, seed=args.seed)
@@ -528,15 +533,21 @@ def main():
         # the pooled replay buffer holds every rank's complete games (48 moves each), and
         # the ranks played different games (global env ids)
         from yacht_amd.engine import unpack_record_image
-        imgs = [unpack_record_image(last_gather[0][r].cpu().numpy(), args.envs, 64, args.sims) for r in range(world)]
+        imgs = [unpack_record_image(last_gather[0][r].cpu().numpy(), args.envs, GAME_MOVES, args.sims)
+                for r in range(world)]
         ok = all(bool((im["n_moves"] == 48).all()) for im in imgs)
         ok = ok and len({im["final"].tobytes() for im in imgs}) == world
         out["allgather_check"] = "ok" if ok and gather_ok else "FAILED"
         out["allgather_check_basis"] = ("every rank's slot of the pooled buffer equals that rank's own packed image "
                                         "byte for byte, the per-slot checksums agree on all ranks, every game has "
                                         "48 moves and the ranks' final boards differ")
-        out["allgather_bytes"] = gathered_bytes
         out["dist_backend"] = dist.get_backend()
+    # the trajectory all-gather's payload: one fixed-size record image per rank (48 moves), gathered
+    # into every rank's buffer (at N = 1 there is no collective; the figure is the image it would send)
+    out["record_image_bytes_per_rank"] = image_bytes
+    out["allgather_bytes"] = gathered_bytes if world > 1 else image_bytes
+    out["allgather_bytes_basis"] = ("bytes of the pooled buffer every rank receives per episode batch (N x the "
+                                    "per-rank image); N = 1: the one image, no collective runs")
     if kt:
         # dominant kernel and its roofline (algorithmic work per launch / average launch time)
         per = {k: (ms / n if n else 0.0, n, ms) for k, (ms, n) in kt.items()}

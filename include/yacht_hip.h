@@ -135,8 +135,10 @@ int yk_net_destroy(yk_net_t* net);
 /* Precision of every forward of this net (predict, leaf prior, the engine's expansions):
  * YK_PREDICT_F32 (default) - f32-equivalent products (fp16 hi/lo planes, three MFMAs each; within
  * 1e-5 of the reference's float32 CPU path); YK_PREDICT_F16 - fp16 weights and GEMM inputs with
- * f32 accumulation, one MFMA per product, as the reference's own GPU predict runs under
- * autocast('cuda') (yacht/NNet.py:186-189).  LayerNorm, SiLU, softmax and tanh stay f32. */
+ * f32 accumulation, one MFMA per product: the operand precision of the reference's own GPU
+ * predict under autocast('cuda') (yacht/NNet.py:186-189), but with f32 outputs - the Linear
+ * outputs and bias adds stay f32 where autocast rounds them to fp16, so it is closer to float32
+ * than autocast is and not bit-equal to it.  LayerNorm, SiLU, softmax and tanh stay f32. */
 #define YK_PREDICT_F32 0
 #define YK_PREDICT_F16 1
 int yk_net_set_precision(yk_net_t* net, int mode);
@@ -279,8 +281,8 @@ int yk_mcts_reset(yk_engine_t* eng);
  * semantics (init_scale, x2 after growth_interval finite steps, x0.5 and the step skipped on an
  * inf / nan gradient), unscale before the clip.  Dropout masks come from the Philox stream
  * (seed, layer, step, row, column), not torch's generator; rows are numbered from the offset set
- * by yk_trainer_set_row_offset (0 by default), so ranks splitting one minibatch draw the masks of
- * the whole minibatch.  Parameters, gradients and Adam moments are flat device buffers in
+ * by yk_trainer_set_row_offset (0 by default; it applies to the next backward only and resets to 0
+ * after it), so ranks splitting one minibatch draw the masks of the whole minibatch.  Parameters, gradients and Adam moments are flat device buffers in
  * state_dict order. */
 typedef struct {
     int max_batch;          /* batch_size (rows per step, upper bound) */

@@ -133,19 +133,24 @@ __device__ __host__ inline uint64_t philox_draw(uint64_t seed, uint32_t env, uin
 // Dropout keep masks of the trainers (yk_train.hip, yk_train_amp.hip): element e (= global row x H
 // + column) of layer `layer` at optimiser step `step` is kept iff its 16-bit uniform - bits
 // 16 (e % 4) .. of the Philox draw of its group of four - is >= p (one draw per 4 elements).
+// The cache is keyed by (layer, group): one cache may serve every layer of a kernel, and a row
+// whose last group of layer l is its first of layer l + 1 (a wave holding a single row at H <= 256)
+// must not reuse layer l's mask.
 struct KeepCache {
     long g = -1;
+    int layer = -1;
     uint32_t m = 0;
 };
 __device__ inline bool dropout_keep(KeepCache& kc, uint64_t seed, int layer, uint64_t step, long e, float p) {
     if (p <= 0.0f) return true;
     const long g = e >> 2;
-    if (g != kc.g) {
+    if (g != kc.g || layer != kc.layer) {
         const uint64_t d = philox_draw(seed, 0x44524F50u + (uint32_t)layer, (step << 32) ^ (uint64_t)g);
         uint32_t m = 0;
 #pragma unroll
         for (int k = 0; k < 4; k++) m |= ((float)((d >> (16 * k)) & 0xFFFFu) * (1.0f / 65536.0f) >= p ? 1u : 0u) << k;
         kc.g = g;
+        kc.layer = layer;
         kc.m = m;
     }
     return (kc.m >> (e & 3)) & 1u;

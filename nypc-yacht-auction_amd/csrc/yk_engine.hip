@@ -36,9 +36,7 @@ constexpr int MAXD = 64;          // max search depth (path entries)
 constexpr int LUT_N = 1 << 16;    // f32(sqrt(Ns)), f32(sqrt(Ns + 1e-8)) table size
 constexpr int GAMES_PER_BLOCK = 4;
 constexpr int GROUP_ALIGN = 16;   // group boundaries on forward row tiles
-#ifndef YK_EXPAND_WPE
-#define YK_EXPAND_WPE 4  // waves per SIMD the expand kernel is register-budgeted for
-#endif
+constexpr int YK_EXPAND_WPE = 4;  // waves per SIMD the expand kernel is register-budgeted for
 
 // python value kinds on the search path (MCTS.py:82, 115, 147)
 enum : uint32_t { T_INT = 0, T_F64 = 1, T_F32 = 2 };
@@ -490,25 +488,8 @@ __global__ __launch_bounds__(256) void k_move_begin(EngDev d, int move, int exte
     }
 }
 
-// Diagnostic builds only (-DYK_SEL_TIMING, tools/diag_select.py): per-game s_memtime
-// accumulators of the descent's phases.
-#ifdef YK_SEL_TIMING
-__device__ unsigned long long g_sel[16384 * 16];
-#define SEL_T0(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
-#define SEL_ACC(k, t0) \
-    if (lane == 0) g_sel[(long)e * 16 + (k)] += __builtin_amdgcn_s_memtime() - (t0)
-#else
 #define SEL_T0(v)
 #define SEL_ACC(k, t0)
-#endif
-// Diagnostic builds only (-DYK_XSPAN, tools/diag_xspan.py): for 16 sampled k_expand_backup launches,
-// per game: start, end of expand + backup, end, the expanded node's valid count, descent levels, and
-// the wave's hardware ids - how a launch's time relates to its games' own times.
-#ifdef YK_XSPAN
-constexpr int XS_SAMPLES = 16, XS_GAMES = 4096;
-__device__ unsigned long long g_xs[XS_SAMPLES][XS_GAMES][8];
-__device__ int g_xs_slot = -1;
-#endif
 
 // One simulation's descent (MCTS.search, MCTS.py:56-152 up to the recursion).
 // All 64 lanes of the game's wave call it together.
@@ -536,9 +517,7 @@ __device__ __forceinline__ void select_game(const EngDev& d, int e, int lane, co
     int known = -1;        // the node this level's state is, when the edge taken to it cached it
     uint32_t end_id = 0;   // id + 1 of a node the descent stops at
     PyV res{0.0, T_INT};
-    SEL_T0(t_all);
     while (true) {
-        SEL_T0(t_lv);
         if (known >= 0) {  // the cached child: its key is the state step + canonical would give
             const uint64_t* kp = nodes[known].key;
 #pragma unroll
@@ -560,7 +539,6 @@ __device__ __forceinline__ void select_game(const EngDev& d, int e, int lane, co
         const bool cached = rc0.x != 0;
         const uint64_t hsh = (cached || known >= 0) ? 0ull : index_hash(s);
         const int nid = cached ? (int)rc0.x - 1 : known >= 0 ? known : lookup(d, g, t, s, hsh);
-        SEL_ACC(0, t_lv);
         if (nid < 0) {  // leaf: predict (MCTS.py:84-115)
             leaf = 1;
             if (lane == 0) {
@@ -589,7 +567,6 @@ __device__ __forceinline__ void select_game(const EngDev& d, int e, int lane, co
         // which saves a dependent load per level (expand 53.35 -> 53.02 us, profiles/r03_expand_ab.log)
         const float sq = (float)sqrt((double)Ns);
         const float sqe = (float)sqrt((double)Ns + 1e-8);
-        SEL_T0(t_sc);
         const float* P = Pbase + p_off;
         const uint16_t* S = Sbase + p_off;
         float best = -INFINITY;
@@ -643,8 +620,6 @@ __device__ __forceinline__ void select_game(const EngDev& d, int e, int lane, co
             }
         }
         scanned += (uint64_t)V;
-        SEL_ACC(1, t_sc);
-        SEL_T0(t_st);
         int j = bj;
         // the winner's lane holds its tag: its own best is the wave's (lowest j among equals)
         const uint32_t wtag = __builtin_amdgcn_readlane(btag, __builtin_amdgcn_readfirstlane((j & 255) >> 2));
@@ -654,18 +629,11 @@ __device__ __forceinline__ void select_game(const EngDev& d, int e, int lane, co
             res = PyV{0.0, T_INT};
             break;
         }
-#ifdef YK_SEL_TIMING
-        if (lane == 0) {
-            g_sel[(long)e * 16 + 4] += 1;
-            g_sel[(long)e * 16 + 5] += (unsigned long long)V;
-        }
-#endif
         const uint32_t child = bj == 0x7FFFFFFF ? 0u : (wtag >> 2);  // id + 1, 0: not cached
         if (child) {  // a deterministic transition taken before: the child node is known
             if (lane == 0) path[depth] = ((uint64_t)(p_off + (uint32_t)j) << 32) | (uint32_t)nid | PATH_DET;
             depth++;
             known = (int)child - 1;
-            SEL_ACC(2, t_st);
             continue;
         }
         known = -1;
@@ -683,9 +651,7 @@ __device__ __forceinline__ void select_game(const EngDev& d, int e, int lane, co
             break;
         }
         s = canonical(s, np);  // MCTS.py:150
-        SEL_ACC(2, t_st);
     }
-    SEL_ACC(3, t_all);
     if (lane == 0) {
         d.leaf_flag[e] = (uint8_t)(leaf ? (t < d.E ? 1 : 2) : 0);  // which net predicts it (dual trees)
         d.path_len[e] = (uint8_t)depth;
@@ -716,41 +682,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(YK_EXPAND_W
     const int e = d.e_lo + blockIdx.x * GAMES_PER_BLOCK + (threadIdx.x >> 6);
     if (e >= d.e_hi) return;
     if (d.done[e]) return;
-#ifdef YK_SEL_TIMING
-    const unsigned long long t_ex = __builtin_amdgcn_s_memtime();
-#endif
-#ifdef YK_XSPAN
-    const int xs = g_xs_slot;
-    const unsigned long long xs0 = __builtin_amdgcn_s_memtime(), xr0 = __builtin_amdgcn_s_memrealtime();
-    const uint32_t xs_v = d.leaf_flag[e] ? (uint32_t)valid_info(ld_state(d.leaf_state + e), 1).V : 0xFFFFFFFFu;
-#endif
     expand_backup_game(d, e, lane);
-#ifdef YK_XSPAN
-    const unsigned long long xs1 = __builtin_amdgcn_s_memtime();
-#endif
-#ifdef YK_SEL_TIMING
-    if (lane == 0) g_sel[(long)e * 16 + 6] += __builtin_amdgcn_s_memtime() - t_ex;
-#endif
     if (do_select) {
         wave_sync();  // this wave's backup writes (edges, slots, Ns) precede its descent's reads
         select_game(d, e, lane, env_ids, ctr_arr);
     }
-#ifdef YK_XSPAN
-    if (xs >= 0 && xs < XS_SAMPLES && e < XS_GAMES && lane == 0) {
-        const unsigned long long xs2 = __builtin_amdgcn_s_memtime(), xr2 = __builtin_amdgcn_s_memrealtime();
-        const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID
-        const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
-        unsigned long long* o = g_xs[xs][e];
-        o[0] = xs0;
-        o[1] = xs1;
-        o[2] = xs2;
-        o[3] = xs_v;
-        o[4] = d.path_len[e];
-        o[5] = ((unsigned long long)xcc << 32) | hw;
-        o[6] = xr0;  // s_memrealtime (100 MHz, one clock for the device): the launch's span
-        o[7] = xr2;
-    }
-#endif
 }
 
 __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int lane) {
@@ -759,7 +695,6 @@ __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int l
     PyV res{d.res_v[e], d.res_t[e]};
     uint32_t end_id = 0;  // id + 1 of the node the path's last edge leads to, if any
     if (d.leaf_flag[e]) {
-        SEL_T0(t_x0);
         const YkS s = ld_state(d.leaf_state + e);
         const uint64_t ihsh = d.leaf_hash[e];                  // the index's hash
         const uint64_t hsh = d.prior == 1 ? key_hash(s) : 0ull;  // the hash prior's (spec) hash
@@ -830,7 +765,6 @@ __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int l
                 qt[r] = (h == 0 && r < R && valid(st + 8 * G + r)) ? softmax_p(x[8 * G + r], mx, lse) : 0.f;
             v = d.vpred[e];
             masked = true;
-            SEL_ACC(8, t_x0);
         } else {
 #pragma unroll
             for (int j = 0; j < PW_GMAX; j++) {
@@ -843,7 +777,6 @@ __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int l
             for (int r = 0; r < PW_TMAX; r++) qt[r] = (h == 0 && r < R) ? hash_prior_pi(hsh, st + 8 * G + r) : 0.f;
             v = hash_prior_v(hsh);
         }
-        SEL_T0(t_x1);
         // mask with the valid moves
 #pragma unroll
         for (int j = 0; j < PW_GMAX; j++) {
@@ -896,8 +829,6 @@ __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int l
             lsum = (lane & o) ? y + lsum : lsum + y;
         }
         const float sum = lsum;
-        SEL_ACC(9, t_x1);
-        SEL_T0(t_x2);
         // ---- allocate + write P over the compact valid set, zero edge slots
         const int VP = pad4(V);
         const uint32_t off = d.arena_top[t];
@@ -942,7 +873,6 @@ __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int l
                     }
                 }
             }
-            SEL_ACC(10, t_x2);
             if (lane == 0) {
                 NodeRec r;
 #pragma unroll
@@ -973,7 +903,6 @@ __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int l
     }
     // ---- backup (MCTS.py:154-164): the path's nodes are distinct, so every level updates in
     // parallel; level k receives v * (-1)^(depth-1-k) ("return -v" per level).
-    SEL_T0(t_bk);
     const int depth = d.path_len[e];
     if (depth > 0) {
         NodeRec* nodes = d.nodes[g] + (long)t * d.NCAP;
@@ -1020,7 +949,6 @@ __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int l
             if (ne1 > gs[5]) gs[5] = ne1;
         }
     }
-    SEL_ACC(12, t_bk);
 }
 
 // getActionProb tail (MCTS.py:40-54) + Coach sampling/step (Coach.py:59-72).  One wave per game.
@@ -1342,7 +1270,7 @@ int check_errors(yk_engine* eng, hipStream_t s) {
 }
 // `sims` simulations for every game of groups 0 .. G-1, group g on stream st[g].  Within a group
 // (and a game) the simulations are sequential; the groups' streams run free, so a forward runs
-// beside the other groups' expand.  (YK_STAGGER, diagnostic: group g's forward k waits for group
+// beside the other groups' expand.  (Staggering them - group g's forward k waiting for group
 // g-1's forward k through an event; at 8192 games x 2 groups that costs 1.2 %,
 // profiles/r02h_stagger_ab.log.)
 int run_sims(yk_engine* eng, int G, const hipStream_t* st, int sims, const uint32_t* env_ids, uint64_t* ctr) {
@@ -1360,9 +1288,6 @@ int run_sims(yk_engine* eng, int G, const hipStream_t* st, int sims, const uint3
         for (int g = 0; g < G; g++) {
             const EngDev& d = dg[g];
             if (d.prior == 0) {
-#ifdef YK_STAGGER
-                if (g > 0) YK_HIP(hipStreamWaitEvent(st[g], eng->ev_fwd[g - 1], 0));
-#endif
                 if (timed) prof_mark(eng, g, KC_FORWARD, st[g]);
                 // predict row = game: no compaction; workgroups without a leaf exit at once
                 // (dual trees: the agent's leaves on its net, then the opponent's on its own)
@@ -1385,20 +1310,8 @@ int run_sims(yk_engine* eng, int G, const hipStream_t* st, int sims, const uint3
                     YK_HIP(hipEventRecord(eng->ev_d1, eng->dstream));
                     YK_HIP(hipStreamWaitEvent(st[g], eng->ev_d1, 0));
                 }
-#ifdef YK_STAGGER
-                if (G > 1) YK_HIP(hipEventRecord(eng->ev_fwd[g], st[g]));
-#endif
             }
             if (timed) prof_mark(eng, g, KC_EXPAND, st[g]);
-#ifdef YK_XSPAN
-            {
-                static long xs_launch = 0;
-                const long q = xs_launch++;
-                const int slot = (q % 300 == 150 && q / 300 < XS_SAMPLES) ? (int)(q / 300) : -1;
-                YK_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_xs_slot), &slot, sizeof(int), 0, hipMemcpyHostToDevice, st[g]));
-                YK_HIP(hipStreamSynchronize(st[g]));  // the host value must outlive the copy
-            }
-#endif
             hipLaunchKernelGGL(k_expand_backup, game_grid(d), bb, 0, st[g], d, k + 1 < sims ? 1 : 0, env_ids, ctr);
             YK_LAUNCHED();
             if (timed && eng->prof_stride > 1) prof_mark(eng, g, -1, st[g]);  // untimed sims follow
@@ -1411,22 +1324,6 @@ int run_sims(yk_engine* eng, int G, const hipStream_t* st, int sims, const uint3
 
 extern "C" {
 
-#ifdef YK_XSPAN
-int yk_diag_xspan(uint64_t* out) {  // HOST out[16][4096][8]
-    YK_HIP(hipDeviceSynchronize());
-    YK_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_xs), sizeof(uint64_t) * XS_SAMPLES * XS_GAMES * 8));
-    return YK_OK;
-}
-#endif
-#ifdef YK_SEL_TIMING
-int yk_diag_select(uint64_t* out, int n) {  // HOST out[n][16]; resets the accumulators
-    YK_HIP(hipDeviceSynchronize());
-    YK_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sel), sizeof(uint64_t) * 16 * (size_t)n));
-    std::vector<uint64_t> z((size_t)16 * n, 0);
-    YK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_sel), z.data(), sizeof(uint64_t) * z.size()));
-    return YK_OK;
-}
-#endif
 
 int yk_engine_create(yk_engine_t** out, const yk_engine_config_t* cfg, yk_net_t* net) {
     if (!out || !cfg) return YK_ERR_ARG;
@@ -1479,9 +1376,7 @@ int yk_engine_create(yk_engine_t** out, const yk_engine_config_t* cfg, yk_net_t*
     eng->ngroups = G;
     // forward head split: when a group's row tiles do not fill the CUs, 2 or 4
     // workgroups per tile each take a slice of the policy head (the trunk runs in each)
-#ifndef YK_FPARTS_MAX
-#define YK_FPARTS_MAX 4
-#endif
+constexpr int YK_FPARTS_MAX = 4;
     {
         int cus = 256, dev = 0;
         if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);

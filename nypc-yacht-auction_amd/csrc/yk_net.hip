@@ -36,41 +36,15 @@ typedef _Float16 half4 __attribute__((ext_vector_type(4)));
 
 namespace {
 
-// Diagnostic builds only: per-phase s_memtime stamps of wave 0 (tools/trunk_ablate.cpp).
-#ifdef YK_TIMING
-__device__ unsigned long long g_tstamp[4096 * 32];
-#define TSTAMP(i) \
-    if (threadIdx.x == 0) g_tstamp[blockIdx.x * 32 + (i)] = __builtin_amdgcn_s_memtime()
-#define WSTAMP(i) /* per wave: slots i + wave */ \
-    if ((threadIdx.x & 63) == 0) g_tstamp[blockIdx.x * 32 + (i) + (threadIdx.x >> 6)] = __builtin_amdgcn_s_memtime()
-#else
 #define TSTAMP(i)
 #define WSTAMP(i)
-#endif
-// Diagnostic builds only (-DYK_TILESTAT, tools/diag_tiles.py): policy-head tiles a workgroup
-// would need if it computed only the union of its rows' valid columns.
-#ifdef YK_TILESTAT
-// [0] workgroups, [1] sum of needed tiles, [2] rows, [3] bid-only workgroups, [4] sum over launches
-// of the launch's max, [5] this launch's max, [6] launches, [8 + k] histogram of tiles / 32
-__device__ unsigned long long g_tiles[16];
-// every YK_VD_EVERY-th valid-only launch: each row's logit descriptor (tools/diag_sort.py)
-constexpr int VD_SAMPLES = 64, VD_ROWS = 8192, YK_VD_EVERY = 75;
-__device__ uint32_t g_vdump[VD_SAMPLES][VD_ROWS];
-__global__ void k_tilestat_flush() {
-    g_tiles[4] += g_tiles[5];
-    g_tiles[5] = 0;
-    g_tiles[6] += 1;
-}
-#endif
 
 constexpr int ROWS = 16;     // rows per workgroup (the MFMA M)
 constexpr int WAVES = 8;     // waves per workgroup
 constexpr int NTHR = 64 * WAVES;
 constexpr int RPW = ROWS / WAVES;  // rows per wave in the row passes
 constexpr int PCH = 4;       // policy-head tiles per chunk
-#ifndef YK_PW
-#define YK_PW 2
-#endif
+constexpr int YK_PW = 2;    // policy-head ring depth, two fp16 planes
 // policy-head ring depth (32-deep slices): a single fp16 plane (PL = 1, the fp16 predict mode)
 // takes half the registers per slice, so its ring is twice as deep
 constexpr int pw_of(int PL) { return PL == 1 ? 2 * YK_PW : YK_PW; }
@@ -108,11 +82,7 @@ struct W2 {
 // PL = 1 (fp16 predict mode) loads the hi plane only: half the weight bytes of the stream
 template <int PL>
 __device__ __forceinline__ W2 ld_w2(const float* __restrict__ P, int KS, int nt, int ks, int lane) {
-#ifdef YK_ABL_W  // diagnostic: every slice from the first 2 KB (no weight stream; results invalid)
-    const float* p = P + ((long)(ks & 1) * 2 * 64 + lane) * 4;
-#else
     const float* p = P + ((long)(nt * KS + ks) * 2 * 64 + lane) * 4;
-#endif
     if constexpr (PL == 1) return W2{*reinterpret_cast<const float4*>(p), make_float4(0.f, 0.f, 0.f, 0.f)};
     return W2{*reinterpret_cast<const float4*>(p), *reinterpret_cast<const float4*>(p + 256)};
 }
@@ -345,9 +315,6 @@ __device__ __forceinline__ void ln_apply2(f2v (&x)[R][NP], const float (&mean)[R
 }
 template <int NP, int R>
 __device__ __forceinline__ void layernorm2(f2v (&x)[R][NP], const float* g, const float* b, int c0, int H) {
-#ifdef YK_ABL_LN  // diagnostic: the trunk's LayerNorms skipped (results invalid)
-    return;
-#endif
     float mean[R], rstd[R];
     ln_stats2<NP, R>(x, mean, rstd, H);
     ln_apply2<NP, R>(x, mean, rstd, g, b, c0);
@@ -509,23 +476,10 @@ __device__ __forceinline__ void pi_chunk(const _Float16* A, int sa, W2 (&ring)[R
             const int row = row0 + 4 * q + j;
             const bool mine = col < ASIZE && (allc[j] || ((rows >> j) & 1u));
             pa[t][j] += b;
-#if defined(YK_STORE_NOBR)  // diagnostic: every lane stores, the rows' unkept columns into row padding
-            {
-                const bool st = row < n && mine;
-                const long o = st ? (long)row * PI_LD + col : (long)(row < n ? row : row0) * PI_LD + 16 * REAL_TILES + rr;
-                logits[o] = pa[t][j];
-            }
-#elif defined(YK_NT_STORE)  // diagnostic: non-temporal logits stores
-            if (row < n && mine) __builtin_nontemporal_store(pa[t][j], logits + (long)row * PI_LD + col);
-#elif !defined(YK_NO_STORE)  // diagnostic: the policy head without its logits stores
             if (row < n && mine) logits[(long)row * PI_LD + col] = pa[t][j];
-#endif
             if (!mine) pa[t][j] = -INFINITY;  // outside the row's softmax
         }
     }
-#ifdef YK_NO_STATS  // diagnostic: the policy head without its softmax statistics
-    if (lane < 0)
-#endif
 #pragma unroll
     for (int j = 0; j < 4; j++) {
         float mn = sm[j];
@@ -558,9 +512,7 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
     constexpr int NACT = H / (16 * NT);              // waves owning columns of the H-wide layers
     constexpr int VPL = H / 64;                      // values per lane in row passes
     constexpr int KS = H / 32;                       // 32-deep slices of an H-deep layer
-#ifndef YK_RCAP
-#define YK_RCAP 16
-#endif
+    constexpr int YK_RCAP = 16;
     constexpr int RCAP = H >= 512 ? 8 : YK_RCAP;      // ring slices x tiles held per wave (VGPR budget)
     constexpr int RW = KS * NT <= RCAP ? KS : RCAP / NT;  // trunk ring depth (slices)
     constexpr int NVS = vstat_size(H), NVB = 6 * H;
@@ -609,7 +561,6 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
     const bool gw = NACT == WAVES || wave < NACT;
     const int nt0 = wave * NT;
     const int c0 = lane * VPL;
-    TSTAMP(0);
 
     // loads in the order they are needed: the static vectors first (their LDS writes must not
     // wait behind the weight stream: vmcnt retires in order), then each wave's two state rows by
@@ -689,7 +640,6 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
         }
         if (w) atomicOr(&UM[lane], w);
     }
-    TSTAMP(1);
 
     floatx4 acc[NT];
     // inp: Linear -> LayerNorm -> SiLU (-> Dropout, identity in eval)  YachtNNet.py:30-35
@@ -763,7 +713,6 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
         }
     }
     lds_barrier();
-    TSTAMP(2);
 
     // ResidualBlock x NB: h = LN1(SiLU(fc1 x)); h = LN2(SiLU(fc2 h)); x + h  YachtNNet.py:17-21
     for (int b = 0; b < net.NB; b++) {
@@ -773,13 +722,11 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
 #pragma unroll
         for (int k = 0; k < PB; k++) vb[k] = reinterpret_cast<const float4*>(net.vblk + (long)b * NVB)[min(tid + NTHR * k, NB4 - 1)];
         if (gw) mma_ring<PL, H, NT, RW>(P, SA, ring, acc, net.w1 + wo, net.w2 + wo, nt0);
-        if (b == 2) TSTAMP(16);
 #pragma unroll
         for (int k = 0; k < PB; k++)  // the previous block's readers passed a barrier; unconditional
             reinterpret_cast<float4*>(VB)[tid + NTHR * k] = vb[k];  // (no branch join after the ring)
         if (gw) store_acc<NT>(T, LD, nt0, acc, nullptr);
         lds_barrier();  // T complete; every wave is done reading x's planes
-        if (b == 2) TSTAMP(17);
         if constexpr (VPL % 2 == 0) {
             f2v x[RPW][VPL / 2];
 #pragma unroll
@@ -802,15 +749,12 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
             }
         }
         lds_barrier();
-        if (b == 2) TSTAMP(18);
         if (gw) {
             if (b + 1 < net.NB) mma_ring<PL, H, NT, RW>(P, SA, ring, acc, net.w2 + wo, after, nt0);
             else mma_ring<PL, H, NT, RW, false>(P, SA, ring, acc, net.w2 + wo, nullptr, nt0);
         }
-        if (b == 2) TSTAMP(19);
         if (gw) store_acc<NT>(T, LD, nt0, acc, nullptr);
         lds_barrier();  // T complete; every wave is done reading h's planes
-        if (b == 2) TSTAMP(21);
         if constexpr (VPL % 2 == 0) {
             f2v x[RPW][VPL / 2];
 #pragma unroll
@@ -846,7 +790,6 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
             }
         }
         lds_barrier();
-        if (b < 6) TSTAMP(3 + b);
     }
 
     // heads: pi_head = LN -> SiLU -> Linear; v_head = LN -> SiLU -> Linear -> SiLU -> Linear -> tanh.
@@ -913,44 +856,6 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
         }
     }
     lds_barrier();
-    TSTAMP(9);
-#ifdef YK_TILESTAT
-    if (valid_only && tid < ROWS) {
-        const unsigned long long li = g_tiles[6];
-        if (li % YK_VD_EVERY == 0 && li / YK_VD_EVERY < VD_SAMPLES && row0 + tid < VD_ROWS && part == 0)
-            g_vdump[li / YK_VD_EVERY][row0 + tid] = VD[tid];
-    }
-    if (tid == 0 && valid_only) {
-        uint32_t m[7] = {0, 0, 0, 0, 0, 0, 0};  // 204 tile bits
-        auto set = [&](int c0, int c1) {       // columns c0 .. c1 inclusive
-            for (int t = c0 / 16; t <= c1 / 16; t++) m[t >> 5] |= 1u << (t & 31);
-        };
-        int rows_on = 0;
-        bool bid_only = true;
-        for (int r = 0; r < ROWS; r++) {
-            const uint32_t v = VD[r], md = v & 0xF;
-            if (md == LM_NONE) continue;
-            rows_on++;
-            if (md != LM_BID) bid_only = false;
-            if (md == LM_BID) set(0, NBID - 1);
-            else if (md == LM_ALL) set(0, ASIZE - 1);
-            else
-                for (int c = 0; c < NCAT; c++)
-                    if (!((v >> (4 + c)) & 1u)) {
-                        const int a0 = NBID + NCOMB * c;
-                        set(a0, md == LM_SCORE10 ? a0 + NCOMB - 1 : a0);
-                    }
-        }
-        int cnt = 0;
-        for (int i = 0; i < 7; i++) cnt += __popc(m[i]);
-        atomicAdd(&g_tiles[0], 1ull);
-        atomicMax(&g_tiles[5], (unsigned long long)cnt);
-        atomicAdd(&g_tiles[8 + cnt / 32], 1ull);
-        atomicAdd(&g_tiles[1], (unsigned long long)cnt);
-        atomicAdd(&g_tiles[2], (unsigned long long)rows_on);
-        if (bid_only) atomicAdd(&g_tiles[3], 1ull);
-    }
-#endif
     // The policy head over all real tiles (full) or over the union of the rows' valid columns.
     // A row's softmax runs over every action (`allc`: the reference's exp(log_softmax), NNet.py:193)
     // or - engine rows - over the tiles holding its valid actions: pi_a / sum_valid(pi) (MCTS.py:88-91)
@@ -1031,12 +936,8 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
         }
 #pragma unroll
         for (int t = 0; t < PCH; t++) tcur[t] = tnxt[t];
-        if (c == 1 || c == 3) TSTAMP(10 + (c >> 1));  // stamps 10, 11 after chunk pairs
-        if (c == 5) TSTAMP(12);
     }
 #undef YK_PI_CHUNK
-    TSTAMP(14);
-    WSTAMP(24);
     store_acc<1>(X, LD, wave, av, VS + VS_BV1 * H);  // X (the trunk output) was read by the head LNs only
     // softmax statistics of the policy logits per row: over the 16 column lanes, then the waves
     float2* SS = reinterpret_cast<float2*>(T);  // T (a_v's planes) is no longer read
@@ -1052,7 +953,6 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
 #pragma unroll
         for (int j = 0; j < 4; j++) SS[wave * ROWS + 4 * (lane >> 4) + j] = make_float2(sm[j], ss[j]);
     }
-    TSTAMP(23);
 #pragma unroll
     for (int rr = 0; rr < RPW; rr++) {  // SiLU -> Linear(128, 1) -> tanh  YachtNNet.py:49-52,69
         const int r = wave * RPW + rr;
@@ -1071,7 +971,6 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
             mlse[(long)part * mstride + row0 + tid] = make_float2(m, parts > 1 ? sm : __logf(sm));
         }
     }
-    TSTAMP(15);
 }
 
 // exp(log_softmax(x)) over the first 3226 columns from the forward's per-row (max, log sum
@@ -1161,9 +1060,6 @@ int launch_forward(const NetDev& net, const yk_state_t* states, const float* x, 
         default: return YK_ERR_ARG;
     }
 #undef YK_FWD
-#ifdef YK_TILESTAT
-    if (valid_only) hipLaunchKernelGGL(k_tilestat_flush, dim3(1), dim3(1), 0, stream);
-#endif
     YK_LAUNCHED();
     return YK_OK;
 }
@@ -1284,20 +1180,6 @@ int yk_net_create(yk_net_t** out, int H, int NB, const float* const* p, int npar
     return YK_OK;
 }
 
-#ifdef YK_TILESTAT
-int yk_diag_tiles(uint64_t* out) {  // HOST out[16]; resets the counters
-    YK_HIP(hipDeviceSynchronize());
-    YK_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tiles), sizeof(uint64_t) * 16));
-    const uint64_t z[16] = {};
-    YK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_tiles), z, sizeof(z)));
-    return YK_OK;
-}
-int yk_diag_vdump(uint32_t* out) {  // HOST out[VD_SAMPLES * VD_ROWS]
-    YK_HIP(hipDeviceSynchronize());
-    YK_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_vdump), sizeof(uint32_t) * VD_SAMPLES * VD_ROWS));
-    return YK_OK;
-}
-#endif
 
 int yk_net_set_precision(yk_net_t* net, int mode) {
     if (!net || (mode != YK_PREDICT_F32 && mode != YK_PREDICT_F16)) return YK_ERR_ARG;

@@ -786,6 +786,7 @@ int yk_trainer_backward(yk_trainer_t* t, const yk_state_t* states, const int32_t
     if (batch <= 0 || batch > t->Bmax) return YK_ERR_ARG;
     hipStream_t s = as_stream(stream);
     int rc = backward_impl(t, states, targets, values, batch_idx, batch, s);
+    t->row_base = 0;  // the offset applies to the one backward it was set for (yk_trainer_set_row_offset)
     if (rc == YK_OK && t->eloss_on) {
         hipLaunchKernelGGL(k_epoch_loss, dim3(1), dim3(64), 0, s, t->lsum, t->eloss, (double)batch, t->eloss_vw);
         YK_LAUNCHED();

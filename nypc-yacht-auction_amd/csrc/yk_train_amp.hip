@@ -1208,8 +1208,24 @@ __global__ __launch_bounds__(256) void k_amp_update(const UpdJob* __restrict__ j
         }
         *sc_next = n;
     }
-    if (!isfinite(total)) return;  // step skipped: parameters and their fp16 copies unchanged
     const float inv = 1.0f / s0.scale;
+    if (!isfinite(total)) {  // step skipped: parameters and their fp16 copies unchanged; the gradient
+        // buffer is left unscaled as torch's unscale_ leaves p.grad (not clipped: its coefficient is nan)
+        const UpdItem it = items[blockIdx.x];
+        const UpdJob jb = jobs[it.job];
+        const int t = threadIdx.x;
+        if (!jb.dstN) {
+            for (int i = 0; i < 4; i++)
+                if (4 * t + i < it.k0) jb.Gm[(long)it.n0 + 4 * t + i] *= inv;
+        } else {
+            const int n = it.n0 + (t >> 3);
+            for (int i = 0; i < 4; i++) {
+                const int k = it.k0 + (t & 7) * 4 + i;
+                if (n < jb.N && k < jb.K) jb.Gm[(long)n * jb.K + k] *= inv;
+            }
+        }
+        return;
+    }
     const double st = (double)(s0.steps + 1);
     const float step_size = (float)((double)lr / (1.0 - pow((double)b1, st)));
     const float bc2_sqrt = (float)sqrt(1.0 - pow((double)b2, st));

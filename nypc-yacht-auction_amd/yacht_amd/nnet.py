@@ -75,8 +75,9 @@ class YkNet:
     """Owns a device copy of the weights in the kernels' layout (yk_net_create).
 
     precision "f32" (default): f32-equivalent products, within 1e-5 of the reference's float32
-    predict.  "f16": fp16 weights / GEMM inputs with f32 accumulation - the arithmetic of the
-    reference's own GPU predict under autocast('cuda') (NNet.py:186-189), an opt-in perf mode."""
+    predict.  "f16": fp16 weights / GEMM inputs with f32 accumulation and f32 Linear outputs - the
+    operand precision of the reference's own GPU predict under autocast('cuda') (NNet.py:186-189;
+    autocast also rounds the outputs to fp16, this mode does not), an opt-in perf mode."""
 
     def __init__(self, state_dict, hidden: int, nblocks: int, precision: str = "f32"):
         arrs = [np.ascontiguousarray(t.detach().to("cpu", torch.float32).numpy() if torch.is_tensor(t)
@@ -169,20 +170,28 @@ class NNetWrapper:
         return self.yk_net().predict_states(states)
 
     # ---- training (NNet.py:118-174) on the native trainer (yacht_amd/train.py)
+    def uses_amp(self) -> bool:
+        """The reference trains under autocast('cuda') + GradScaler whenever args.cuda
+        (NNet.py:113-116, 141-155) and in float32 otherwise (:157-165): args.amp, when given,
+        overrides that (amp=False: the float32 step on the GPU)."""
+        a = self.args
+        return bool(a.get("amp", a.get("cuda", True)))
+
     def _trainer(self):
         from .train import Trainer
         if getattr(self, "_tr", None) is None:
             a = self.args
             self._tr = Trainer(self.nnet.state_dict(), a.hidden, a.nblocks, lr=a.lr, weight_decay=a.weight_decay,
                                max_batch=a.batch_size, vloss_weight=a.get("vloss_weight", 1.0),
-                               dropout=a.dropout, seed=a.get("seed", 0), amp=bool(a.get("amp", False)))
+                               dropout=a.dropout, seed=a.get("seed", 0), amp=self.uses_amp())
         return self._tr
 
     def train(self, examples, verbose=True):
         """The reference loop: `epochs` passes over shuffled minibatches of `batch_size`
         (drop_last False), one CE(argmax pi) + vloss_weight * MSE step each, clip 5.0, AdamW -
-        in float32 (the reference's CPU path), or with args.amp the reference's GPU path
-        (autocast('cuda') + GradScaler, NNet.py:113-116, 141-155) on fp16 MFMA kernels.
+        as the reference's GPU path when args.cuda (autocast('cuda') + GradScaler,
+        NNet.py:113-116, 141-155) on fp16 MFMA kernels, or in float32 (the reference's CPU path)
+        with args.cuda False or args.amp False (uses_amp).
         Shuffles come from a torch generator seeded per call (the reference uses the global
         torch RNG); dropout masks from the trainer's Philox stream.
 

@@ -23,7 +23,8 @@ torch = pytest.importorskip("torch")
 
 ARGS = dict(numIters=1, numEps=6, tempThreshold=15, updateThreshold=0.55, maxlenOfQueue=200000, numMCTSSims=4,
             arenaCompare=6, cpuct=1.5, numItersForTrainExamplesHistory=5, lr=2e-3, weight_decay=1e-4, epochs=2,
-            batch_size=40, vloss_weight=1.5, cuda=True, hidden=64, nblocks=1, dropout=0.0, seed=3)
+            batch_size=40, vloss_weight=1.5, cuda=True, hidden=64, nblocks=1, dropout=0.0, seed=3,
+            amp=False)  # the float32 step: the DDP-split comparison below is held to f32 summation order
 
 
 @pytest.fixture(scope="module")

@@ -154,7 +154,13 @@ def test_nnetwrapper_train_and_checkpoint(T, tmp_path):
     examples = [ex for ep in coach.executeEpisodes(4) for ex in ep]
     args = dotdict(lr=2e-3, weight_decay=1e-4, epochs=2, batch_size=64, vloss_weight=1.5, cuda=True, hidden=64,
                    nblocks=1, dropout=0.3)
+    # args.cuda selects the reference's GPU arithmetic (autocast + GradScaler, NNet.py:113-116),
+    # args.amp False the float32 step; this test counts optimiser steps, which a GradScaler skip
+    # would not, so it runs the float32 mode
+    assert NNetWrapper(game, args).uses_amp() and not NNetWrapper(game, dotdict(args, cuda=False)).uses_amp()
+    args = dotdict(args, amp=False)
     w = NNetWrapper(game, args)
+    assert not w._trainer().amp
     pi0, _ = w.predict(examples[0][0])
     w.train(examples, verbose=False)
     pi1, v1 = w.predict(examples[0][0])
@@ -248,11 +254,14 @@ def test_coach_learn_iteration_and_resume(T, tmp_path):
 
 
 @pytest.mark.parametrize("amp", [False, True])
-def test_dropout_rows_split_over_calls_equal_the_whole_batch(T, golden, amp):
-    """Two backwards of half a minibatch each (row offsets 0 and B/2, gradients averaged) take the
-    whole minibatch's dropout masks: the gradient equals one backward over all B rows."""
+@pytest.mark.parametrize("B", [64, 63])
+def test_dropout_rows_split_over_calls_equal_the_whole_batch(T, golden, amp, B):
+    """Two backwards of part of a minibatch each (row offsets 0 and B//2, gradients weighted by
+    their shares) take the whole minibatch's dropout masks: the gradient equals one backward over
+    all B rows.  An odd B leaves a row alone in its wave in one call but not in the other, which is
+    where a mask cache shared across layers would hand a row the previous layer's mask."""
     K, N, TR = T
-    H, NB, B = 64, 2, 64
+    H, NB = 64, 2
     W = golden("states.npz")["states"][:B]
     rng = np.random.RandomState(2)
     S = K.states_to_device(W)
@@ -265,10 +274,11 @@ def test_dropout_rows_split_over_calls_equal_the_whole_batch(T, golden, amp):
     g_whole = whole.grads().cpu().numpy().copy()
     half = TR.Trainer(_sd(H, NB), H, NB, **kw)
     acc = 0
+    cuts = (0, B // 2, B)
     for k in range(2):
-        idx = torch.arange(k * B // 2, (k + 1) * B // 2, dtype=torch.int32, device="cuda")
-        half.backward(S, tg, vv, idx=idx, row0=k * B // 2)
-        acc = acc + 0.5 * half.grads().cpu().numpy().astype(np.float64)
+        idx = torch.arange(cuts[k], cuts[k + 1], dtype=torch.int32, device="cuda")
+        half.backward(S, tg, vv, idx=idx, row0=cuts[k])
+        acc = acc + (cuts[k + 1] - cuts[k]) / B * half.grads().cpu().numpy().astype(np.float64)
     # f32 (or fp16-rounded, amp) sums in another grouping
     assert _relnorm(acc, g_whole) < (2e-3 if amp else 1e-4)  # wrong masks would be O(1) off
     other = TR.Trainer(_sd(H, NB), H, NB, **kw)
@@ -375,3 +385,26 @@ def test_amp_steps_vs_torch_autocast_gradscaler(T, golden, H, NB, B):
         assert d_ours <= 1.5 * d_f32 + 2e-2, ("update", name, d_ours, d_f32)
     st = tr.amp_state()
     assert st["scale"] == scale_amp and tr.step_count == st["steps"]
+
+
+def test_amp_skipped_step_leaves_unscaled_gradients(T, golden):
+    """A step GradScaler skips (the scaled fp16 gradients overflow) leaves the parameters alone and
+    the gradient buffer unscaled, as torch's unscale_ leaves p.grad."""
+    K, N, TR = T
+    H, NB, B = 64, 1, 32
+    W = golden("states.npz")["states"][:B]
+    rng = np.random.RandomState(6)
+    S = K.states_to_device(W)
+    tg = torch.tensor(rng.randint(0, 3226, B), dtype=torch.int32, device="cuda")
+    vv = torch.tensor(rng.rand(B) * 2 - 1, dtype=torch.float32, device="cuda")
+    tr = TR.Trainer(_sd(H, NB), H, NB, max_batch=B, dropout=0.0, amp=True, init_scale=2.0 ** 40)
+    p0 = tr.params().cpu().numpy().copy()
+    tr.backward(S, tg, vv)
+    g_scaled = tr.grads().cpu().numpy().copy()
+    assert not np.isfinite(g_scaled).all()
+    tr.apply()
+    st = tr.amp_state()
+    assert st["found_inf"] and st["steps"] == 0 and st["scale"] == 2.0 ** 39
+    assert np.array_equal(tr.params().cpu().numpy(), p0)
+    want = g_scaled * np.float32(2.0 ** -40)
+    np.testing.assert_array_equal(tr.grads().cpu().numpy(), want)

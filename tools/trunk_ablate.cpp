@@ -4,7 +4,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
-#include "../nypc-yacht-auction_amd/csrc/yk_net.hip"
+#include "yk_net.hip"  // tools/stage_hooks.sh: the sources with tools/diag_hooks.patch applied
 
 int main(int argc, char** argv) {
     const int H = 256, NB = 6, n = argc > 1 ? atoi(argv[1]) : 3480, iters = 200;

@@ -4,10 +4,11 @@
 # YK_ABL_LN (the trunk's LayerNorms skipped), both.  GPU box.
 cd "$(dirname "$0")/.." || exit 2
 set -e
+bash tools/stage_hooks.sh
 i=0
 for v in "" "-DYK_ABL_W" "-DYK_ABL_LN" "-DYK_ABL_W -DYK_ABL_LN"; do
   /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -std=c++17 -ffp-contract=off -DYK_TIMING $v -Iinclude \
-     -Inypc-yacht-auction_amd/csrc tools/trunk_ablate.cpp nypc-yacht-auction_amd/csrc/yk_env.hip -o /tmp/tabl_$i -w &
+     -I/tmp/yk_hooks/csrc tools/trunk_ablate.cpp /tmp/yk_hooks/csrc/yk_env.hip -o /tmp/tabl_$i -w &
   i=$((i+1))
 done
 wait
