@@ -30,7 +30,7 @@ sys.path.insert(0, REPO)
 
 METRIC = "MCTS node-expansions/sec/GPU @4096 envs x100 sims; episodes/sec 1-8 GPU"
 F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense f16 matrix peak (~2.5 PF)
-SPLIT_PRODUCTS = 3             # k_forward: each f32 product = 3 fp16 MFMA products (hi.hi, hi.lo, lo.hi)
+SPLIT_PRODUCTS = 4             # k_forward: each f32 product = 4 fp16 MFMA products (hi.hi, hi.lo, lo.hi, lo.lo)
 # the f32-equivalent peak of that arithmetic: what the forward's algorithmic FLOPs are priced against
 SPLIT_PEAK_TFLOPS = F16_MFMA_PEAK_TFLOPS / SPLIT_PRODUCTS
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E spec peak
@@ -570,8 +570,8 @@ def main():
                    "traffic": tr[0] if tr else None,
                    "traffic_source": tr[1] if tr else None,
                    "work_per_launch": f"{exp_per_launch:.0f} expansions x {PREDICT_FLOP} FLOP (f32)",
-                   "peak_basis": "f16 dense MFMA peak / 3: every f32 product runs as hi*hi + hi*lo + "
-                                 "lo*hi on fp16 planes with f32 accumulation",
+                   "peak_basis": "f16 dense MFMA peak / 4: every f32 product runs as hi*hi + hi*lo + lo*hi + "
+                                 "(lo 2^-11)*lo on fp16 planes with f32 accumulation",
                    "limiter": "per-CU weight stream: each 16-row tile streams all 6.7 MB of weight "
                               "planes through its CU, and one CU streams a weight set shared by all CUs "
                               "at 110-123 GB/s at any CU count; the fp16 MFMAs overlap the stream "

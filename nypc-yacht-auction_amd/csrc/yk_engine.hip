@@ -37,6 +37,12 @@ constexpr int LUT_N = 1 << 16;    // f32(sqrt(Ns)), f32(sqrt(Ns + 1e-8)) table s
 constexpr int GAMES_PER_BLOCK = 4;
 constexpr int GROUP_ALIGN = 16;   // group boundaries on forward row tiles
 constexpr int YK_EXPAND_WPE = 4;  // waves per SIMD the expand kernel is register-budgeted for
+// The root's incremental UCB scan: per tree, the root's compact set sorted by P
+// (descending, ascending index on ties) and the list of its visited edges, valid for one move
+constexpr int RO_CAP = 3072;      // >= the largest compact valid set (3024)
+constexpr int RV_CAP = 1024;      // visited root edges kept; more -> the move falls back to full scans
+constexpr uint32_t RV_OFF = 0xFFFFFFFFu;
+constexpr int RS_N = 4096;        // k_root_sort's bitonic width (pow2 >= RO_CAP)
 
 // python value kinds on the search path (MCTS.py:82, 115, 147)
 enum : uint32_t { T_INT = 0, T_F64 = 1, T_F32 = 2 };
@@ -87,6 +93,10 @@ struct EngDev {
     uint8_t* cur_round;    // [T]
     uint4* root_c;         // [T][2] the move's root once a descent found it: {id + 1 (0: not yet), p_off,
                            //        nvalid, -}, {vinfo lo, hi, -, -}
+    uint32_t* rv_n;        // [T] visited root edges listed in rv (RV_OFF: no sorted root this move)
+    uint32_t* rv;          // [T][RV_CAP] j | slot << 12 of each visited root edge
+    uint16_t* ro_j;        // [T][RO_CAP] the root's compact indices by descending P (ascending j on ties)
+    float* ro_p;           // [T][RO_CAP] their P
     // game state
     yk_state_t* board;
     int32_t* cur;
@@ -373,6 +383,7 @@ __global__ void k_reset(EngDev d, int start_games, uint32_t env_base) {
         d.arena_top[t] = 0;
         d.gen[t] = 0;
         d.cur_round[t] = 0;
+        d.rv_n[t] = RV_OFF;
     }
 #pragma unroll
     for (int k = 0; k < 8; k++) d.gstats[(long)e * 8 + k] = 0;
@@ -399,7 +410,10 @@ __global__ __launch_bounds__(256) void k_move_begin(EngDev d, int move, int exte
     const int e = d.e_lo + blockIdx.x * GAMES_PER_BLOCK + (threadIdx.x >> 6);
     if (e >= d.e_hi) return;
     const int t = tree_of(d, e);
-    if (lane == 0) d.root_c[2 * t] = make_uint4(0, 0, 0, 0);  // ids move at a compaction: look the root up afresh
+    if (lane == 0) {
+        d.root_c[2 * t] = make_uint4(0, 0, 0, 0);  // ids move at a compaction: look the root up afresh
+        d.rv_n[t] = RV_OFF;                         // the sorted root is rebuilt after this move's first expansion
+    }
     if (!external_root) {
         if (d.done[e]) return;
         const YkS b = ld_state(d.board + e);
@@ -491,6 +505,92 @@ __global__ __launch_bounds__(256) void k_move_begin(EngDev d, int move, int exte
 #define SEL_T0(v)
 #define SEL_ACC(k, t0)
 
+// The root's UCB argmax (MCTS.py:117-135) without scanning its whole compact set: the root is the
+// same node for all of a move's simulations, and between two of them only one of its edges changes.
+// An unvisited edge's u = (c P) sqrt(Ns + 1e-8) is monotone in P, so the best unvisited edge is the
+// first unvisited entry of the root's P order (k_root_sort), and entries of equal u - the band that
+// follows it in that order - go to the lowest index (strict '>' in ascending action order).  The
+// visited edges (the list the backups append to) are scanned as before.  Same f32 operations as the
+// full scan, so the same winner, bit for bit.  Returns the winner's compact index (0x7FFFFFFF: none)
+// and its edge tag (0: unvisited); `scanned` counts the entries read.
+__device__ __forceinline__ int root_scan(const EngDev& d, int t, int lane, uint32_t nv, const float* P,
+                                         const uint16_t* S, const Edge* edges, int V, float sq, float sqe,
+                                         uint32_t& wtag, uint64_t& scanned) {
+    const uint16_t* oj = d.ro_j + (long)t * RO_CAP;
+    const float* op = d.ro_p + (long)t * RO_CAP;
+    const uint32_t* rv = d.rv + (long)t * RV_CAP;
+    // the order's first piece is loaded beside the visited list: both only need the tree
+    int jj = lane < V ? (int)oj[lane] : 0;
+    float pp = lane < V ? op[lane] : 0.f;
+    float best = -INFINITY;
+    int bj = 0x7FFFFFFF;
+    uint32_t btag = 0;
+    for (uint32_t i = (uint32_t)lane; i < nv; i += 64) {
+        const uint32_t w = rv[i];
+        const int j = (int)(w & 0xFFFu);
+        const float p = P[j];
+        const Edge ev = edges[(w >> 12) - 1];
+        const float u = (float)ev.Q + ((d.c32 * p) * sq) / (float)(ev.N + 1);
+        if (u > best || (u == best && j < bj)) {
+            best = u;
+            bj = j;
+            btag = ev.tag;
+        }
+    }
+    float ub = -INFINITY;
+    int uj = 0x7FFFFFFF;
+    bool found = false;
+    int walked = 0;
+    for (int k0 = 0; k0 < V; k0 += 64) {
+        const int k = k0 + lane;
+        if (k0) {
+            jj = k < V ? (int)oj[k] : 0;
+            pp = k < V ? op[k] : 0.f;
+        }
+        walked = min(k0 + 64, V);
+        const bool in = k < V;
+        const bool unv = in && S[jj] == 0;
+        const float u = (d.c32 * pp) * sqe;
+        bool cand;
+        if (!found) {
+            const uint64_t bal = __ballot(unv);
+            if (!bal) continue;  // every entry of this piece is visited
+            const int f = __builtin_ctzll(bal);
+            ub = __shfl(u, f, 64);
+            found = true;
+            cand = unv && lane >= f && u == ub;
+        } else {
+            cand = unv && u == ub;
+        }
+        int cj = cand ? jj : 0x7FFFFFFF;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) cj = min(cj, __shfl_xor(cj, o, 64));
+        uj = min(uj, cj);
+        // u is non-increasing along the order: the band goes on into the next piece only if the
+        // piece's last entry still has u == ub
+        if (!(k0 + 64 < V && __shfl(u, 63, 64) == ub)) break;
+    }
+    if (lane == 0 && found && (ub > best || (ub == best && uj < bj))) {
+        best = ub;
+        bj = uj;
+        btag = 0;
+    }
+    const int mine = bj;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const float ob = __shfl_xor(best, o, 64);
+        const int oj2 = __shfl_xor(bj, o, 64);
+        if (ob > best || (ob == best && oj2 < bj)) {
+            best = ob;
+            bj = oj2;
+        }
+    }
+    const uint64_t own = __ballot(mine == bj);  // the lane whose own candidate won holds its tag
+    wtag = own ? __builtin_amdgcn_readlane(btag, (int)__builtin_ctzll(own)) : 0u;
+    scanned += (uint64_t)nv + (uint64_t)walked;
+    return bj;
+}
+
 // One simulation's descent (MCTS.search, MCTS.py:56-152 up to the recursion).
 // All 64 lanes of the game's wave call it together.
 __device__ __forceinline__ void select_game(const EngDev& d, int e, int lane, const uint32_t* env_ids, uint64_t* ctr_arr) {
@@ -517,6 +617,23 @@ __device__ __forceinline__ void select_game(const EngDev& d, int e, int lane, co
     int known = -1;        // the node this level's state is, when the edge taken to it cached it
     uint32_t end_id = 0;   // id + 1 of a node the descent stops at
     PyV res{0.0, T_INT};
+    // the root's pick from its P order and visited list (root_scan), made before the walk, where
+    // little else is live (inside the loop the second scan path would spill)
+    bool pre = false;
+    int pre_bj = 0x7FFFFFFF;
+    uint32_t pre_tag = 0;
+    {
+        const uint32_t rvn = d.rv_n[t];
+        if (rvn != RV_OFF) {  // k_root_sort ran this move: root_c holds the root
+            const uint4 rc = d.root_c[2 * t];
+            const uint32_t Ns = nodes[rc.x - 1].Ns;
+            const float sq = (float)sqrt((double)Ns), sqe = (float)sqrt((double)Ns + 1e-8);
+            pre_bj = __builtin_amdgcn_readfirstlane(
+                root_scan(d, t, lane, rvn, Pbase + rc.y, Sbase + rc.y, edges, (int)rc.z, sq, sqe, pre_tag, scanned));
+            pre_tag = __builtin_amdgcn_readfirstlane(pre_tag);
+            pre = true;
+        }
+    }
     while (true) {
         if (known >= 0) {  // the cached child: its key is the state step + canonical would give
             const uint64_t* kp = nodes[known].key;
@@ -569,60 +686,69 @@ __device__ __forceinline__ void select_game(const EngDev& d, int e, int lane, co
         const float sqe = (float)sqrt((double)Ns + 1e-8);
         const float* P = Pbase + p_off;
         const uint16_t* S = Sbase + p_off;
-        float best = -INFINITY;
-        int bj = 0x7FFFFFFF;
-        uint32_t btag = 0;  // the edge tag of the lane's best entry (0: unvisited)
-        // software-pipelined scan: iteration it+1's P / slot loads fly while iteration it's
-        // visited-edge gathers resolve
-        float4 p4 = make_float4(0.f, 0.f, 0.f, 0.f);
-        ushort4 s4 = make_ushort4(0, 0, 0, 0);
-        if (lane * 4 < V) {
-            p4 = *reinterpret_cast<const float4*>(P + lane * 4);
-            s4 = *reinterpret_cast<const ushort4*>(S + lane * 4);
-        }
-        for (int j0 = lane * 4; j0 < V; j0 += 256) {
-            const float pv[4] = {p4.x, p4.y, p4.z, p4.w};
-            const uint16_t sv[4] = {s4.x, s4.y, s4.z, s4.w};
-            Edge ev[4];
-#pragma unroll
-            for (int t = 0; t < 4; t++)
-                if (j0 + t < V && sv[t]) ev[t] = edges[sv[t] - 1];
-            if (j0 + 256 < V) {
-                p4 = *reinterpret_cast<const float4*>(P + j0 + 256);
-                s4 = *reinterpret_cast<const ushort4*>(S + j0 + 256);
+        int bj_out;
+        uint32_t wtag;
+        if (depth == 0 && pre) {  // the root: picked above from its P order and visited list
+            bj_out = pre_bj;
+            wtag = pre_tag;
+        } else {
+            float best = -INFINITY;
+            int bj = 0x7FFFFFFF;
+            uint32_t btag = 0;  // the edge tag of the lane's best entry (0: unvisited)
+            // software-pipelined scan: iteration it+1's P / slot loads fly while iteration it's
+            // visited-edge gathers resolve
+            float4 p4 = make_float4(0.f, 0.f, 0.f, 0.f);
+            ushort4 s4 = make_ushort4(0, 0, 0, 0);
+            if (lane * 4 < V) {
+                p4 = *reinterpret_cast<const float4*>(P + lane * 4);
+                s4 = *reinterpret_cast<const ushort4*>(S + lane * 4);
             }
+            for (int j0 = lane * 4; j0 < V; j0 += 256) {
+                const float pv[4] = {p4.x, p4.y, p4.z, p4.w};
+                const uint16_t sv[4] = {s4.x, s4.y, s4.z, s4.w};
+                Edge ev[4];
 #pragma unroll
-            for (int t = 0; t < 4; t++) {
-                const int j = j0 + t;
-                if (j < V) {
-                    float u;
-                    const float cp = d.c32 * pv[t];
-                    if (sv[t]) {
-                        u = (float)ev[t].Q + (cp * sq) / (float)(ev[t].N + 1);
-                    } else {
-                        u = cp * sqe;
-                    }
-                    if (u > best) {
-                        best = u;
-                        bj = j;
-                        btag = sv[t] ? ev[t].tag : 0u;
+                for (int t = 0; t < 4; t++)
+                    if (j0 + t < V && sv[t]) ev[t] = edges[sv[t] - 1];
+                if (j0 + 256 < V) {
+                    p4 = *reinterpret_cast<const float4*>(P + j0 + 256);
+                    s4 = *reinterpret_cast<const ushort4*>(S + j0 + 256);
+                }
+#pragma unroll
+                for (int t = 0; t < 4; t++) {
+                    const int j = j0 + t;
+                    if (j < V) {
+                        float u;
+                        const float cp = d.c32 * pv[t];
+                        if (sv[t]) {
+                            u = (float)ev[t].Q + (cp * sq) / (float)(ev[t].N + 1);
+                        } else {
+                            u = cp * sqe;
+                        }
+                        if (u > best) {
+                            best = u;
+                            bj = j;
+                            btag = sv[t] ? ev[t].tag : 0u;
+                        }
                     }
                 }
             }
-        }
 #pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) {
-            const float ob = __shfl_xor(best, o, 64);
-            const int oj = __shfl_xor(bj, o, 64);
-            if (ob > best || (ob == best && oj < bj)) {
-                best = ob;
-                bj = oj;
+            for (int o = 32; o >= 1; o >>= 1) {
+                const float ob = __shfl_xor(best, o, 64);
+                const int oj = __shfl_xor(bj, o, 64);
+                if (ob > best || (ob == best && oj < bj)) {
+                    best = ob;
+                    bj = oj;
+                }
             }
+            scanned += (uint64_t)V;
+            bj_out = bj;
+            // the winner's lane holds its tag: its own best is the wave's (lowest j among equals)
+            wtag = __builtin_amdgcn_readlane(btag, __builtin_amdgcn_readfirstlane((bj & 255) >> 2));
         }
-        scanned += (uint64_t)V;
+        const int bj = bj_out;
         int j = bj;
-        // the winner's lane holds its tag: its own best is the wave's (lowest j among equals)
-        const uint32_t wtag = __builtin_amdgcn_readlane(btag, __builtin_amdgcn_readfirstlane((j & 255) >> 2));
         if (j == 0x7FFFFFFF) j = 0;  // MCTS.py:138-143: first valid action
         if (depth >= MAXD) {
             if (lane == 0) atomicOr(d.err, ERR_DEPTH);
@@ -947,7 +1073,102 @@ __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int l
             d.edge_count[g * d.T + t] = ne1;
             uint64_t* gs = d.gstats + (long)e * 8;
             if (ne1 > gs[5]) gs[5] = ne1;
+            // a new edge at level 0 (the move's root): into the root's visited list (root_scan)
+            if (is_new && eid < (uint32_t)d.ECAP && eid < 65535u) {
+                const uint32_t n = d.rv_n[t];
+                if (n != RV_OFF) {
+                    const uint32_t j = (uint32_t)(pe >> 32) - d.root_c[2 * t].y;
+                    if (n < (uint32_t)RV_CAP) {
+                        d.rv[(long)t * RV_CAP + n] = j | ((eid + 1) << 12);
+                        d.rv_n[t] = n + 1;
+                    } else {
+                        d.rv_n[t] = RV_OFF;  // too many: full scans for the rest of the move
+                    }
+                }
+            }
         }
+    }
+}
+
+// The root's P order for root_scan, once per move after its first expansion (the root is expanded
+// by then, by this move's first simulation or an earlier search): the compact set sorted by P
+// descending, ascending index on ties (a bitonic sort of 64-bit keys P bits << 32 | 0xFFFF - j in
+// LDS; P >= 0, so its bits order as unsigned), and the list of the edges already visited.  One
+// workgroup per game.  Leaves the root in full-scan mode when c <= 0 (the order is then not the
+// UCB order), when the root has no valid action, or when its visited list would overflow.
+__global__ __launch_bounds__(256) void k_root_sort(EngDev d) {
+    __shared__ uint64_t key[RS_N];
+    __shared__ int s_nid;
+    __shared__ uint32_t s_nv;
+    const int e = d.e_lo + (int)blockIdx.x;
+    if (e >= d.e_hi || d.done[e] || d.idle[e] || !(d.c32 > 0.f)) return;
+    const int tid = threadIdx.x;
+    const int t = tree_of(d, e);
+    const int g = d.gen[t];
+    const uint4 rc0 = d.root_c[2 * t];
+    if (tid < 64) {
+        int nid = rc0.x ? (int)rc0.x - 1 : -1;
+        if (nid < 0) {
+            const YkS r = ld_state(d.root + e);
+            nid = lookup(d, g, t, r, index_hash(r));
+        }
+        if (tid == 0) {
+            s_nid = nid;
+            s_nv = 0;
+        }
+    }
+    __syncthreads();
+    const int nid = s_nid;
+    if (nid < 0) return;
+    const NodeRec& nd = d.nodes[g][(long)t * d.NCAP + nid];
+    const int V = (int)nd.nvalid;
+    const uint32_t p_off = nd.p_off;
+    if (V == 0 || V > RO_CAP) return;
+    int n2 = 64;
+    while (n2 < V) n2 <<= 1;
+    const float* P = d.arenaP + (long)t * d.AE + p_off;
+    const uint16_t* S = d.arenaS + (long)t * d.AE + p_off;
+    uint32_t* rv = d.rv + (long)t * RV_CAP;
+    for (int i = tid; i < n2; i += 256) {
+        uint64_t k = 0;  // padding sorts last (a real key's low half is >= 0xFFFF - 3071)
+        if (i < V) {
+            k = ((uint64_t)__float_as_uint(P[i]) << 32) | (uint32_t)(0xFFFFu - (uint32_t)i);
+            const uint16_t sl = S[i];
+            if (sl) {
+                const uint32_t pos = atomicAdd(&s_nv, 1u);
+                if (pos < (uint32_t)RV_CAP) rv[pos] = (uint32_t)i | ((uint32_t)sl << 12);
+            }
+        }
+        key[i] = k;
+    }
+    __syncthreads();
+    for (int size = 2; size <= n2; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int i = tid; i < n2 / 2; i += 256) {
+                const int lo = 2 * i - (i & (stride - 1)), hi = lo + stride;
+                const bool desc = (lo & size) == 0;
+                const uint64_t a = key[lo], b = key[hi];
+                if ((a < b) == desc) {
+                    key[lo] = b;
+                    key[hi] = a;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    uint16_t* oj = d.ro_j + (long)t * RO_CAP;
+    float* op = d.ro_p + (long)t * RO_CAP;
+    for (int i = tid; i < V; i += 256) {
+        const uint64_t k = key[i];
+        oj[i] = (uint16_t)(0xFFFFu - (uint32_t)(k & 0xFFFFu));
+        op[i] = __uint_as_float((uint32_t)(k >> 32));
+    }
+    if (tid == 0) {
+        if (rc0.x == 0) {  // the next descent need not look the root up
+            d.root_c[2 * t] = make_uint4((uint32_t)nid + 1, p_off, (uint32_t)V, 0);
+            d.root_c[2 * t + 1] = make_uint4((uint32_t)nd.vinfo, (uint32_t)(nd.vinfo >> 32), 0, 0);
+        }
+        d.rv_n[t] = s_nv <= (uint32_t)RV_CAP ? s_nv : RV_OFF;
     }
 }
 
@@ -1202,7 +1423,7 @@ struct yk_engine {
 
 namespace {
 // kernel classes for yk_engine_kernel_times
-enum { KC_SELECT = 0, KC_FORWARD = 1, KC_SCAN = 2, KC_EXPAND = 3, KC_MOVE_BEGIN = 4, KC_MOVE_END = 5, KC_N = 8 };
+enum { KC_SELECT = 0, KC_FORWARD = 1, KC_SCAN = 2 /* k_root_sort + the second descent */, KC_EXPAND = 3, KC_MOVE_BEGIN = 4, KC_MOVE_END = 5, KC_N = 8 };
 
 void prof_mark(yk_engine* eng, int g, int cls, hipStream_t s) {  // records an event pair boundary
     if (!eng->prof) return;
@@ -1312,8 +1533,19 @@ int run_sims(yk_engine* eng, int G, const hipStream_t* st, int sims, const uint3
                 }
             }
             if (timed) prof_mark(eng, g, KC_EXPAND, st[g]);
-            hipLaunchKernelGGL(k_expand_backup, game_grid(d), bb, 0, st[g], d, k + 1 < sims ? 1 : 0, env_ids, ctr);
+            // the move's first expansion ends without the next descent: the root's P order is built
+            // in between (k_root_sort; root_scan uses it for the move's remaining simulations)
+            const bool sort_root = k == 0 && sims > 1;
+            hipLaunchKernelGGL(k_expand_backup, game_grid(d), bb, 0, st[g], d, k + 1 < sims && !sort_root ? 1 : 0,
+                               env_ids, ctr);
             YK_LAUNCHED();
+            if (sort_root) {
+                if (timed) prof_mark(eng, g, KC_SCAN, st[g]);
+                hipLaunchKernelGGL(k_root_sort, dim3((unsigned)(d.e_hi - d.e_lo)), bb, 0, st[g], d);
+                YK_LAUNCHED();
+                hipLaunchKernelGGL(k_select, game_grid(d), bb, 0, st[g], d, env_ids, ctr);
+                YK_LAUNCHED();
+            }
             if (timed && eng->prof_stride > 1) prof_mark(eng, g, -1, st[g]);  // untimed sims follow
         }
     }
@@ -1409,6 +1641,10 @@ constexpr int YK_FPARTS_MAX = 4;
     A(d.gen, T);
     A(d.cur_round, T);
     A(d.root_c, 2 * T);
+    A(d.rv_n, T);
+    A(d.rv, T * RV_CAP);
+    A(d.ro_j, T * RO_CAP);
+    A(d.ro_p, T * RO_CAP);
     A(d.board, E);
     A(d.cur, E);
     A(d.ctr, E);

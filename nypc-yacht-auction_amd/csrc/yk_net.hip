@@ -6,10 +6,12 @@
 // their activations in LDS through featurize -> Linear/LN/SiLU -> 6 x ResidualBlock -> head
 // LayerNorms -> value head and policy logits (204 x 16 columns).  Every dense product is
 // f32-equivalent: weights and GEMM inputs are held as fp16 planes hi = fp16(x) and
-// lo = fp16((x - hi) 2^11), and a 16x16x32 tile is hi*hi + 2^-11 (hi*lo + lo*hi) - three
-// v_mfma_f32_16x16x32_f16 with exact products and f32 accumulation (the dropped lo*lo term
-// is 2^-22 relative).  Results track torch's float32 path within the north star's 1e-5
-// (tests/test_gpu_net.py) at 1/5 of the MFMA cycles of v_mfma_f32_16x16x4_f32.
+// lo = fp16((x - hi) 2^11), and a 16x16x32 tile is hi*hi + 2^-11 (hi*lo + lo*hi + (lo 2^-11)*lo) -
+// four v_mfma_f32_16x16x32_f16 with exact products and f32 accumulation (the lo*lo term, 2^-22
+// relative, enters the cross-term accumulator through an fp16 operand lo * 2^-11; dropping it
+// doubled the prior's error against float64, tools/prior_error_emulation.py).  Results track
+// torch's float32 path within the north star's 1e-5 (tests/test_gpu_net.py) at 1/4 of the MFMA
+// cycles of v_mfma_f32_16x16x4_f32.
 //
 // The kernel is latency-bound per workgroup (one per CU), and on this chip a CU does not
 // overlap MFMA execution with its vector-memory stream (tools/stream_bench.hip), so the weight
@@ -91,9 +93,12 @@ __device__ __forceinline__ floatx4 mfma16(float4 a, float4 b, floatx4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, a), __builtin_bit_cast(half8, b), c, 0, 0, 0);
 }
 
-// f32-equivalent product of one A slice (hi, lo planes) and one weight slice: three fp16 MFMAs
-// (exact products, f32 accumulation): hi x hi into m, hi x lo and lo x hi into c, which carries
-// the 2^11 scale of the lo planes until combine().
+// f32-equivalent product of one A slice (hi, lo planes) and one weight slice: four fp16 MFMAs
+// (exact products, f32 accumulation): hi x hi into m; hi x lo, lo x hi and (lo 2^-11) x lo into
+// c, which carries the 2^11 scale of the lo planes until combine().  lo 2^-11 is an exact power-of-
+// two scaling in fp16 (v_pk_mul_f16) down to the fp16 subnormals (kept: denorm mode 16/64 = 3),
+// whose 2^-25 absolute rounding is 2^-36 |w| of a product - below an f32 rounding of any product
+// the lo*lo term matters to.
 struct Acc3 {
     floatx4 m, c;
 };
@@ -103,13 +108,17 @@ __device__ __forceinline__ floatx4 combine(const Acc3& a) {
     if constexpr (PL == 1) return a.m;
     return a.m + a.c * UNSPLIT;
 }
-// one 16x16x32 product into the accumulators: hi*hi (+ the two cross terms when PL = 2)
+__device__ __forceinline__ float4 lo_scaled(float4 al) {  // the lo plane x 2^-11, fp16
+    return __builtin_bit_cast(float4, __builtin_bit_cast(half8, al) * (_Float16)(1.0f / 2048.0f));
+}
+// one 16x16x32 product into the accumulators: hi*hi (+ the three lo terms when PL = 2)
 template <int PL>
 __device__ __forceinline__ void mma3(Acc3& c, float4 ah, float4 al, const W2& w) {
     c.m = mfma16(ah, w.h, c.m);
     if constexpr (PL == 2) {
         c.c = mfma16(ah, w.l, c.c);
         c.c = mfma16(al, w.h, c.c);
+        c.c = mfma16(lo_scaled(al), w.l, c.c);
     }
 }
 
@@ -175,6 +184,9 @@ __device__ __forceinline__ void mma_ring(const _Float16* A, int sa, W2 (&ring)[R
             for (int t = 0; t < NT; t++) c[t].c = mfma16(ah, w[t].l, c[t].c);
 #pragma unroll
             for (int t = 0; t < NT; t++) c[t].c = mfma16(al, w[t].h, c[t].c);
+            const float4 als = lo_scaled(al);
+#pragma unroll
+            for (int t = 0; t < NT; t++) c[t].c = mfma16(als, w[t].l, c[t].c);
         }
         const int g = ks + RW;
         if (g < KS || NEXT) {
@@ -360,6 +372,9 @@ __device__ __forceinline__ void ring_chunk(const _Float16* A, int sa, W2 (&ring)
             for (int t = 0; t < NTL; t++) c[t].c = mfma16(ah, w[t].l, c[t].c);
 #pragma unroll
             for (int t = 0; t < NTL; t++) c[t].c = mfma16(al, w[t].h, c[t].c);
+            const float4 als = lo_scaled(al);
+#pragma unroll
+            for (int t = 0; t < NTL; t++) c[t].c = mfma16(als, w[t].l, c[t].c);
         }
         const int g = ks + RD;
         if (g < KS) {

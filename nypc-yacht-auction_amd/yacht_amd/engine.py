@@ -86,7 +86,7 @@ class SelfPlayEngine:
         return dict(result=result, totals=totals, n_moves=nm, actions=actions, final=final, ctr=ctr)
 
     # class 0: the first descent of each move; class 3: expand + backup + the next descent
-    KERNEL_CLASSES = ("select", "forward", "unused", "expand_backup_select", "move_begin", "move_end")
+    KERNEL_CLASSES = ("select", "forward", "root_sort_select", "expand_backup_select", "move_begin", "move_end")
 
     def profile(self, enable: bool = True, stride: int = 1):
         """Per-kernel HIP event timing; the forward / expand pair of every `stride`-th simulation."""
