@@ -252,14 +252,18 @@ def f16_leg(sd, envs=4096, sims=100, seed=0):
     return out
 
 
-def coach_iter_leg(model, world, games_per_gpu=8192, seed=0, amp=True, warm=True):
+def coach_iter_leg(model, world, games_per_gpu=8192, seed=0, amp=True, warm=True, history=1):
     """Config 5 at its per-GPU shape: ONE whole Coach.learn iteration (Coach.py:74-139) with
     main.py's args (main.py:17-43: 25 sims, tempThreshold 15, maxlenOfQueue 200,000, 15 epochs of
     batch 512, dropout 0.3, arenaCompare 10, updateThreshold 0.55) over numEps = games_per_gpu x
     N games sharded over the N ranks (65,536 on 8 GPUs = config 5), the reference's GPU train
     path (autocast + GradScaler: the amp trainer) unless amp=False.  Per-phase wall times of a
     steady-state iteration: warm=True first runs a 512-game iteration untimed (the first torch.save
-    / zipfile / allocator use of the process cost about 1.5 s once, profiles/r03c_coach_profile.log)."""
+    / zipfile / allocator use of the process cost about 1.5 s once, profiles/r03c_coach_profile.log).
+    history > 1: the steady state of Coach.learn (numItersForTrainExamplesHistory 5, main.py:30):
+    the replay history already holds history - 1 earlier iterations' worth of examples (copies of
+    one untimed self-play iteration's 200,000-example shard), so the timed iteration trains on
+    history x 200,000 examples as every iteration after the fourth does (Coach.py:99-111)."""
     if warm:
         coach_iter_leg(model, world, games_per_gpu=min(512, games_per_gpu), seed=seed + 1, amp=amp, warm=False)
     import shutil
@@ -286,14 +290,18 @@ def coach_iter_leg(model, world, games_per_gpu=8192, seed=0, amp=True, warm=True
     nn = NNetWrapper(game, args)
     nn.nnet.load_state_dict(model.state_dict())
     c = Coach(game, nn, args)
+    if history > 1:
+        earlier = c.selfPlayExamples(args.numEps, maxlen=args.maxlenOfQueue)  # untimed
+        c.trainExamplesHistory = [earlier] * (history - 1)
     c.learn()
-    n = len(c.trainExamplesHistory[0])
+    n = sum(len(x) for x in c.trainExamplesHistory)
     steps = 15 * -(-n // 512)
     out = {"config": f"one Coach.learn iteration, main.py args: numEps {args.numEps} ({games_per_gpu}/GPU x {world}), "
                      f"25 sims, maxlenOfQueue 200000, 15 epochs x batch 512 "
                      f"({'autocast + GradScaler on fp16 MFMA' if amp else 'f32'}; every rank the whole minibatch), "
                      f"dropout 0.3, arenaCompare 10",
-           "examples_kept": n, "train_steps": steps, "gate_tally_prev_new_draws": list(c.last_pit)}
+           "history_iterations": len(c.trainExamplesHistory), "examples_trained": n, "train_steps": steps,
+           "gate_tally_prev_new_draws": list(c.last_pit)}
     out.update({k: round(v, 4) for k, v in c.phase_times.items()})
     out["train_ms_per_step"] = 1000.0 * c.phase_times["train_s"] / max(steps, 1)
     if rank == 0:
@@ -395,6 +403,8 @@ def main():
     ap.add_argument("--no-coach", action="store_true", help="skip the config-5 Coach-iteration legs")
     ap.add_argument("--no-shape", action="store_true", help="skip the config-3 shape leg (2048 x 200)")
     ap.add_argument("--no-f16", action="store_true", help="skip the fp16 predict-mode leg")
+    ap.add_argument("--no-steady", action="store_true",
+                    help="skip the steady-state Coach iteration (a 5-iteration replay history)")
     ap.add_argument("--coach-games", type=int, default=8192,
                     help="games per GPU of the whole-iteration config-5 leg (config 5: 65,536 / 8 = 8192)")
     ap.add_argument("--dist-backend", default=None, help="nccl (RCCL, default on GPUs) or gloo (rehearsal)")
@@ -500,6 +510,9 @@ def main():
         del img
         with contextlib.redirect_stdout(sys.stderr):  # Coach.learn's progress lines: stdout is the JSON line
             coach["iteration"] = coach_iter_leg(model, world, games_per_gpu=args.coach_games, seed=args.seed)
+            if not args.no_steady:
+                coach["iteration_steady"] = coach_iter_leg(model, world, games_per_gpu=args.coach_games,
+                                                           seed=args.seed + 3, warm=False, history=5)
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()

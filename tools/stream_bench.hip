@@ -337,6 +337,48 @@ __global__ __launch_bounds__(NTHR) void k_f16_ring(const float4* __restrict__ w,
     if (acc0[0] + acc1[1] == 12345.f) out[blockIdx.x] = 1.f;
     CLK_END
 }
+// k_f16_ring at 3 or 4 products per slice, with the workgroups of an XCD (blockIdx % 8) starting
+// their walk through the weight set at DIV different offsets (DIV = 1: lock-step, every CU of the
+// XCD reading the same lines together; DIV = 32: each CU of the XCD at its own place) - what a
+// schedule without a global barrier does to the shared-read rate
+template <int R, int NP, int DIV>
+__global__ __launch_bounds__(NTHR) void k_f16_ring_rot(const float4* __restrict__ w, long n4, float* out) {
+    CLK_BEGIN
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const long per = n4 / 64 / 8 / 2;  // 2-KB slices per wave
+    const long off = (long)((blockIdx.x >> 3) % DIV) * (per / DIV);
+    const float4* src = w + (long)wave * per * 128 + lane;
+    float4 ring[R][2];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const long g = (off + r) % per;
+        ring[r][0] = src[g * 128];
+        ring[r][1] = src[g * 128 + 64];
+    }
+    floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+    half8 ah, al;
+    for (int i = 0; i < 8; i++) {
+        ah[i] = (_Float16)(lane * 0.01f + i);
+        al[i] = (_Float16)(lane * 0.001f);
+    }
+    for (long f0 = 0; f0 < per; f0 += R) {
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            const half8 wh = __builtin_bit_cast(half8, ring[r][0]);
+            const half8 wl = __builtin_bit_cast(half8, ring[r][1]);
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, wh, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, wl, acc1, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, wh, acc1, 0, 0, 0);
+            if constexpr (NP == 4) acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, wl, acc1, 0, 0, 0);
+            const long g = (off + f0 + r + R) % per;
+            ring[r][0] = src[g * 128];
+            ring[r][1] = src[g * 128 + 64];
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    if (acc0[0] + acc1[1] == 12345.f) out[blockIdx.x] = 1.f;
+    CLK_END
+}
 // the same MFMAs, no stream
 __global__ __launch_bounds__(NTHR) void k_f16_only(const float4* __restrict__ w, long n4, float* out) {
     CLK_BEGIN
@@ -384,6 +426,17 @@ int main(int argc, char** argv) {
         printf("G=%3d %-28s %8.2f us per launch  %6.1f GB/s per CU  %6.2f TB/s from L2  clock %.2f GHz\n", G, name, us,
                n4 * 16 / (us * 1e3), n4 * 16.0 * G / (us * 1e6), clk[1] ? 0.1 * clk[0] / clk[1] : 0.0);
     };
+    if (argc > 2 && argv[2][0] == 'r') {  // desynchronised workgroups (schedule without a global barrier)
+        for (int g : {256, 128}) {
+            G = g;
+            run("f16x3 ring R=8 lock-step", k_f16_ring_rot<8, 3, 1>);
+            run("f16x3 ring R=8 4 offsets", k_f16_ring_rot<8, 3, 4>);
+            run("f16x3 ring R=8 32 offsets", k_f16_ring_rot<8, 3, 32>);
+            run("f16x4 ring R=8 lock-step", k_f16_ring_rot<8, 4, 1>);
+            run("f16x4 ring R=8 32 offsets", k_f16_ring_rot<8, 4, 32>);
+        }
+        return 0;
+    }
     if (argc > 2 && argv[2][0] == 'v') {  // vector-ALU waves beside a register-load stream
         run("split2: valu alone", k_split2<2>);
         run("split2: vgpr stream alone", k_split2<4>);
