@@ -502,8 +502,6 @@ __global__ __launch_bounds__(256) void k_move_begin(EngDev d, int move, int exte
     }
 }
 
-#define SEL_T0(v)
-#define SEL_ACC(k, t0)
 
 // The root's UCB argmax (MCTS.py:117-135) without scanning its whole compact set: the root is the
 // same node for all of a move's simulations, and between two of them only one of its edges changes.

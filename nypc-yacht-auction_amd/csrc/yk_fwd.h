@@ -14,8 +14,6 @@ namespace ykf {
 using namespace yk;
 namespace {
 
-#define TSTAMP(i)
-#define WSTAMP(i)
 
 constexpr int ROWS = 16;     // rows per workgroup (the MFMA M)
 constexpr int WAVES = 8;     // waves per workgroup

@@ -56,6 +56,33 @@ int main(int argc, char** argv) {
             double a = 0; for (int b = 0; b < nb; b++) a += (double)(t[b * 32 + det[k][1]] - t[b * 32 + det[k][0]]);
             printf("  %-9s %9.0f\n", dn[k], a / nb);
         }
+        // block 2, per wave (tools/diag_sources.py LSTAMP): fc1 GEMM, accumulator store, first barrier,
+        // row pass, second barrier, fc2 GEMM; and the spread of the waves' GEMM ends (skew)
+        std::vector<unsigned long long> ws((size_t)nb * 16 * 8);
+        hipMemcpyFromSymbol(ws.data(), HIP_SYMBOL(g_wstamp), sizeof(unsigned long long) * ws.size());
+        const char* pn[6] = {"fc1 GEMM", "acc store", "barrier 1", "row pass", "barrier 2", "fc2 GEMM"};
+        printf("block 2 per wave (mean over workgroups, ticks):\n  wave ");
+        for (int k = 0; k < 6; k++) printf(" %10s", pn[k]);
+        printf("\n");
+        for (int w = 0; w < 8; w++) {
+            printf("  %4d ", w);
+            for (int k = 0; k < 6; k++) {
+                double a = 0;
+                for (int b = 0; b < nb; b++) a += (double)(ws[(b * 16 + w) * 8 + k + 1] - ws[(b * 16 + w) * 8 + k]);
+                printf(" %10.0f", a / nb);
+            }
+            printf("\n");
+        }
+        double sk = 0, sk5 = 0;
+        for (int b = 0; b < nb; b++) {
+            unsigned long long lo = ~0ull, hi = 0, lo5 = ~0ull, hi5 = 0;
+            for (int w = 0; w < 8; w++) {
+                lo = std::min(lo, ws[(b * 16 + w) * 8 + 1]); hi = std::max(hi, ws[(b * 16 + w) * 8 + 1]);
+                lo5 = std::min(lo5, ws[(b * 16 + w) * 8 + 6]); hi5 = std::max(hi5, ws[(b * 16 + w) * 8 + 6]);
+            }
+            sk += (double)(hi - lo); sk5 += (double)(hi5 - lo5);
+        }
+        printf("  spread of the waves' fc1 GEMM ends %.0f, fc2 GEMM ends %.0f ticks\n", sk / nb, sk5 / nb);
     }
 #endif
     return 0;

@@ -10,11 +10,14 @@ src=nypc-yacht-auction_amd/csrc
 case $name in base*) src=ab_base/csrc ;; esac
 out=/tmp/yk_$name
 mkdir -p $out
-# the diagnostic hooks (stamps, ablation switches, yk_diag_* readers) live in tools/diag_hooks.patch,
-# not in the production sources: stage a copy with the hooks applied (a no-op without their defines)
-rm -rf $out/stage && mkdir -p $out/stage && cp -r $src $out/stage/csrc
-patch -s -d $out/stage -p2 < tools/diag_hooks.patch
-src=$out/stage/csrc
+# the diagnostic hooks (stamps, yk_diag_* readers) are not in the production sources: with a
+# -DYK_* switch, build from a copy with them inserted (tools/diag_sources.py)
+case " $* " in
+  *" -DYK_"*)
+    [ "$src" = nypc-yacht-auction_amd/csrc ] || { echo "hooks need the in-tree sources" >&2; exit 2; }
+    python3 tools/diag_sources.py $out/stage > /dev/null
+    src=$out/stage/csrc ;;
+esac
 for f in yk_env yk_net yk_engine yk_train yk_train_amp yk_replay; do
   [ -f $src/$f.hip ] || continue
   /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -fPIC -std=c++17 -ffp-contract=off -w "$@" \
