@@ -1417,6 +1417,7 @@ struct yk_engine {
     } pg[YK_MAX_GROUPS];
     double kms[8] = {0};
     int64_t klaunch[8] = {0};
+    bool root_scan = true;  // the incremental root scan (k_root_sort + root_scan); YK_ROOT_SCAN=0: full scans
 };
 
 namespace {
@@ -1533,7 +1534,7 @@ int run_sims(yk_engine* eng, int G, const hipStream_t* st, int sims, const uint3
             if (timed) prof_mark(eng, g, KC_EXPAND, st[g]);
             // the move's first expansion ends without the next descent: the root's P order is built
             // in between (k_root_sort; root_scan uses it for the move's remaining simulations)
-            const bool sort_root = k == 0 && sims > 1;
+            const bool sort_root = k == 0 && sims > 1 && eng->root_scan;
             hipLaunchKernelGGL(k_expand_backup, game_grid(d), bb, 0, st[g], d, k + 1 < sims && !sort_root ? 1 : 0,
                                env_ids, ctr);
             YK_LAUNCHED();
@@ -1687,6 +1688,11 @@ constexpr int YK_FPARTS_MAX = 4;
     }
 #undef A
     if (rc == YK_OK && hipHostMalloc((void**)&eng->host_done, sizeof(int32_t)) != hipSuccess) rc = YK_ERR_NOMEM;
+    {  // YK_ROOT_SCAN=0: every descent scans the root's whole compact set (A/B, and the test that both
+       // give the same trees)
+        const char* ev = getenv("YK_ROOT_SCAN");
+        eng->root_scan = !(ev && ev[0] == '0');
+    }
     if (rc == YK_OK && G > 1) {
         if (hipEventCreateWithFlags(&eng->ev_fork, hipEventDisableTiming) != hipSuccess) rc = YK_ERR_HIP;
         for (int g = 0; g < G && rc == YK_OK; g++)

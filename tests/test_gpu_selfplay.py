@@ -348,3 +348,27 @@ def test_sampled_kernel_timing_counts_and_results(Y):
         assert x == out[0][1]
         for k in ("states", "info", "ctr", "values", "final", "n_moves", "visits_off", "visits"):
             assert np.array_equal(rec[k], out[0][0][k]), k
+
+
+@pytest.mark.parametrize("prior,sims", [("hash", 40), ("net", 25), ("hash", 200)])
+def test_incremental_root_scan_equals_full_scan(Y, prior, sims, monkeypatch):
+    """The root's UCB argmax from its P order and visited list (k_root_sort + root_scan, MCTS.py:117-135)
+    picks exactly what scanning the whole compact set picks: identical trees, records and stream
+    counters with YK_ROOT_SCAN=0 (every descent a full scan) and the default."""
+    _, E, N = Y
+    n, seed, base = 192, 707, 900
+    net = N.YkNet(spec.closed_form_weights(256, 6), 256, 6) if prior == "net" else None
+    out = []
+    for mode in ("0", "1"):
+        monkeypatch.setenv("YK_ROOT_SCAN", mode)
+        eng = E.SelfPlayEngine(n, sims, 1.5, 15, net=net, prior=prior, max_moves=48)
+        eng.run(seed, base)
+        st = eng.stats()
+        assert st["errors"] == 0
+        out.append((eng.records(), st))
+        eng.close()
+    (r0, s0), (r1, s1) = out
+    assert s1["expansions"] == s0["expansions"] and s1["path_edges"] == s0["path_edges"]
+    assert s1["scanned"] < s0["scanned"]  # the root's entries are no longer all read every simulation
+    for k in ("states", "info", "ctr", "values", "final", "n_moves", "visits_off", "visits"):
+        assert np.array_equal(r1[k], r0[k]), k
