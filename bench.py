@@ -410,9 +410,13 @@ def main():
     ap.add_argument("--dist-backend", default=None, help="nccl (RCCL, default on GPUs) or gloo (rehearsal)")
     ap.add_argument("--groups", type=int, default=0,
                     help="game groups on their own streams (0: the engine's auto choice)")
+    ap.add_argument("--root-scan", type=int, default=1,
+                    help="0: every descent scans the root's whole compact set (YK_ROOT_SCAN=0; A/B only)")
     ap.add_argument("--arena-entries", type=int, default=0,
                     help="P-arena entries per game (0: the engine's overflow-free default)")
     args = ap.parse_args()
+    if not args.root_scan:
+        os.environ["YK_ROOT_SCAN"] = "0"
 
     import torch
     import torch.distributed as dist

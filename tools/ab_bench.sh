@@ -10,16 +10,19 @@ mkdir -p gpurun_out
 R=${1:-2}; shift
 names=(head); declare -A LIB ARGS
 LIB[head]=""; ARGS[head]=""
-if [ -d ab_base/csrc ]; then
-  bash tools/variant_lib.sh base > /dev/null || exit 3
-  names+=(base); LIB[base]=/tmp/yk_base/libyacht_hip.so; ARGS[base]=""
+# a variant prebuilt in the container (tools/_variants/NAME/libyacht_hip.so, git-ignored) is used as is
+pre() { [ -f tools/_variants/$1/libyacht_hip.so ] && echo tools/_variants/$1/libyacht_hip.so; }
+if [ -d ab_base/csrc ] || [ -n "$(pre base)" ]; then
+  if [ -n "$(pre base)" ]; then LIB[base]=$(pre base); else bash tools/variant_lib.sh base > /dev/null || exit 3; LIB[base]=/tmp/yk_base/libyacht_hip.so; fi
+  names+=(base); ARGS[base]=""
 fi
 for v in "$@"; do
   n="${v%%=*}"; f="${v#*=}"
   names+=("$n")
   case "$f" in
-    --*) ARGS[$n]="$f"; LIB[$n]=""; case $n in base*) LIB[$n]=/tmp/yk_base/libyacht_hip.so ;; esac ;;
-    *) bash tools/variant_lib.sh "$n" $f > /dev/null || exit 3; LIB[$n]=/tmp/yk_$n/libyacht_hip.so; ARGS[$n]="" ;;
+    --*) ARGS[$n]="$f"; LIB[$n]=""; case $n in base*) LIB[$n]=${LIB[base]} ;; esac ;;
+    *) if [ -n "$(pre $n)" ]; then LIB[$n]=$(pre $n); else bash tools/variant_lib.sh "$n" $f > /dev/null || exit 3; LIB[$n]=/tmp/yk_$n/libyacht_hip.so; fi
+       ARGS[$n]="" ;;
   esac
 done
 B="python -u bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-arena --no-train --no-coach --no-shape"

@@ -29,12 +29,16 @@ lv = out[:, 4].sum()
 tot = out[:, 3].astype(np.float64)
 print(f"select kernel: {kt['select'][0] / kt['select'][1] * 1e3:.1f} us avg over {kt['select'][1]} launches")
 print(f"levels per game-sim: {lv / (E * st['sims']):.2f}; valid entries scanned per level: {out[:, 5].sum() / lv:.0f}")
-names = ["lookup (ended+hash+probe)", "UCB scan + argmax", "step + canonical", "whole descent"]
+names = ["lookup (ended+hash+probe)", "UCB scan + argmax (full scans)", "step + canonical", "whole descent"]
 per = tot.sum()
 for k, nm in enumerate(names):
     c = out[:, k].astype(np.float64).sum()
     print(f"  {nm:28s} {c / (E * st['sims']):9.0f} cycles per game-sim  ({100 * c / per:5.1f}% of descent)")
 print(f"  max descent per game-sim    {tot.max() / st['sims']:9.0f}")
+rs = out[:, 13].astype(np.float64).sum()
+print(f"  root incremental scan (root_scan) {rs / (E * st['sims']):9.0f} cycles per game-sim  "
+      f"({100 * rs / per:5.1f}% of descent); entries read {out[:, 14].astype(np.float64).sum() / (E * st['sims']):.0f} "
+      f"per game-sim vs {out[:, 5].astype(np.float64).sum() / (E * st['sims']):.0f} in full scans")
 ex = out[:, 6].astype(np.float64).sum()
 print(f"  expand + backup (fused kernel) {ex / (E * st['sims']):9.0f} cycles per game-sim")
 for k, nm in ((8, "expand: logits load, max, sum-exp"), (9, "expand: mask + pairwise sum"),
