@@ -14,10 +14,11 @@ from oracle import oracle as O
 # space (P x the valid mass, i.e. the pi that renormalises to it) at the north-star tolerance, and
 # directly against the reference's own f32 forward: P's worst relative error (entries > 1e-3) may be
 # at most REF_FACTOR times that of torch fp32 on the CPU over the same rows.  The engine's products
-# carry 22-bit operands (fp16 hi + lo planes) and drop lo*lo, so its tails sit about 2x torch fp32's
-# (measured 1.30e-4 vs 6.3e-5 over 14,628 arena leaves); the check prints both.
+# carry 22-bit operands (fp16 hi + lo planes, all four products incl. lo*lo) and the policy softmax
+# uses the accurate expf / logf, so its tails sit at torch fp32's (round 4: 3.73e-5 vs 4.49e-5 at
+# the bench size, 6.10e-6 vs 4.53e-6 for the config-5 kaiming net); the check prints both.
 RTOL_PI, ATOL_PI, ATOL_V = 3e-5, 1e-7, 1e-5
-REF_FACTOR = 3.0
+REF_FACTOR = 1.5
 _NETS = {}
 
 

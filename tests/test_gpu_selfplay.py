@@ -350,14 +350,19 @@ def test_sampled_kernel_timing_counts_and_results(Y):
             assert np.array_equal(rec[k], out[0][0][k]), k
 
 
-@pytest.mark.parametrize("prior,sims", [("hash", 40), ("net", 25), ("hash", 200)])
-def test_incremental_root_scan_equals_full_scan(Y, prior, sims, monkeypatch):
+@pytest.mark.parametrize("prior,sims,keep", [("hash", 40, None), ("net", 25, None), ("hash", 200, None),
+                                             ("hash", 60, "48"), ("net", 40, "5")])
+def test_incremental_root_scan_equals_full_scan(Y, prior, sims, keep, monkeypatch):
     """The root's UCB argmax from its P order and visited list (k_root_sort + root_scan, MCTS.py:117-135)
     picks exactly what scanning the whole compact set picks: identical trees, records and stream
-    counters with YK_ROOT_SCAN=0 (every descent a full scan) and the default."""
+    counters with YK_ROOT_SCAN=0 (every descent a full scan) and the default - also with a kept
+    order of only 48 / 5 entries (YK_ROOT_K), where the radix selection of the top entries runs on
+    every root and walks that outrun the kept order fall back to the full scan."""
     _, E, N = Y
     n, seed, base = 192, 707, 900
     net = N.YkNet(spec.closed_form_weights(256, 6), 256, 6) if prior == "net" else None
+    if keep:
+        monkeypatch.setenv("YK_ROOT_K", keep)
     out = []
     for mode in ("0", "1"):
         monkeypatch.setenv("YK_ROOT_SCAN", mode)

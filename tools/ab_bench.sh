@@ -36,7 +36,7 @@ d = json.load(open(f"gpurun_out/ab_{n}_{r}.json"))
 k = {a: round(b["avg_ms"] * 1000, 2) for a, b in d.get("kernel_ms", {}).items()}
 c = d.get("capacity_use", {})
 print(f"{n:8s} r{r} {d['value'] / 1e6:7.3f}M exp/s  fwd {k.get('forward')}  exp {k.get('expand_backup_select')}  "
-      f"sel {k.get('select')}  mb {k.get('move_begin')}  me {k.get('move_end')}  arena {c.get('max_arena')}/"
+      f"sel {k.get('select')}  rs {k.get('root_sort_select')}  mb {k.get('move_begin')}  me {k.get('move_end')}  arena {c.get('max_arena')}/"
       f"{c.get('arena_cap')}", flush=True)
 EOF
   done

@@ -105,10 +105,10 @@ int yk_diag_select(uint64_t* out, int n) {  // HOST out[n][16]; resets the accum
 # or the root's full scan), 2 step + canonical, 3 whole descent, 4 levels, 5 entries scanned, 6 expand
 # + backup, 8-10 expand phases, 12 backup, 13 the root's incremental scan (root_scan), 14 its entries
 ENGINE = [
-    (r"^constexpr int RS_N = 4096;.*\n", "after", ENGINE_GLOBALS),
+    (r"^constexpr uint32_t RV_OFF = .*\n", "after", ENGINE_GLOBALS),
     (r"^    PyV res\{0\.0, T_INT\};\n    // the root's pick", "before_line2", "    SEL_T0(t_all);\n"),
-    (r"^        if \(rvn != RV_OFF\) \{  // k_root_sort ran this move.*\n", "after", "            SEL_T0(t_rs);\n            const uint64_t sc0 = scanned;\n"),
-    (r"^            pre = true;\n", "after", "            SEL_ACC(13, t_rs);\n            SEL_ADD(14, scanned - sc0);\n"),
+    (r"^        if \(rc\.x != 0 && rc1\.z != RV_OFF\) \{  // k_root_sort ran this move.*\n", "after", "            SEL_T0(t_rs);\n            const uint64_t sc0 = scanned;\n"),
+    (r"^            pre = pre_bj != -1;\n", "after", "            SEL_ACC(13, t_rs);\n            SEL_ADD(14, scanned - sc0);\n"),
     (r"^        if \(known >= 0\) \{  // the cached child.*\n", "before", "        SEL_T0(t_lv);\n"),
     (r"^        if \(V == 0\) \{  // no valid action: MCTS.py:141-147.*\n", "before", "        SEL_ACC(0, t_lv);\n        SEL_T0(t_sc);\n"),
     (r"^        const int bj = bj_out;\n", "after", "        SEL_ACC(1, t_sc);\n        SEL_ADD(4, 1);\n        SEL_ADD(5, V);\n        SEL_T0(t_st);\n"),
