@@ -590,6 +590,20 @@ __device__ inline int greedy_heuristic_wave(const YkS& s, int lane) {
     return phase == 1 ? a : -1;  // valid only in the score phase
 }
 
+// ------------------------------------------------------------------ softmax exp
+// exp(x) for the policy softmax (x <= ~0): 2^t (1 + r ln 2) with t = x * log2e rounded and r its
+// residual (the product's exact error by fma, plus x times log2e's f32 tail), so the result stays
+// within about 1 ulp of exp(x) like the library expf / torch's CPU exp, where __expf's product
+// rounding costs up to |x| * 2^-24 relative.  Six instructions (one v_exp_f32) against the
+// library form's thirteen; results below 2^-126 are not needed (priors of that size are zeros to
+// MCTS.py's renormalisation at f32) and follow v_exp_f32; exp_acc(-inf) = 0, NaN stays NaN.
+__device__ __forceinline__ float exp_acc(float x) {
+    constexpr float L2E = 1.44269504088896340736f, L2E_LO = 1.9259629890910904e-08f, LN2 = 0.693147180559945309f;
+    const float t = x * L2E;
+    const float r = t > -150.f ? fmaf(x, L2E_LO, fmaf(x, L2E, -t)) : 0.f;  // (x = -inf: fma gives NaN)
+    const float e = __builtin_amdgcn_exp2f(t);
+    return fmaf(e, r * LN2, e);
+}
 // ------------------------------------------------------------------ features
 // c_tab.die_scale / round_feat recomputed in registers (IEEE double division, then the f32
 // rounding the host table applies - the same values bit for bit): a per-lane table index would

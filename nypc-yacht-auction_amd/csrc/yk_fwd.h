@@ -436,13 +436,13 @@ __device__ __forceinline__ uint32_t tile_word(uint32_t vd, int w) {
 }
 
 // Running softmax statistics (online form: max and sum exp(x - max)), merged over lanes and waves
-// at the end of the head.  The policy's exp / log are the accurate expf / logf (1 ulp), not the
-// native v_exp_f32 forms: with them the engine's priors track numpy's (divergence from
-// an independent f32 run 15.6% -> 9.4% of the games)
+// at the end of the head.  The native __expf suffices here: its relative error |y| 2^-24 on a term
+// exp(y) is largest where the term is small, so the log-sum-exp moves by < 1e-7 (the expand's
+// final exp(x - m - lse) is the accurate exp_acc, yk_common.h); the log is the library logf
 __device__ __forceinline__ void stat_merge(float& m, float& s, float m2, float s2) {
     const float mm = fmaxf(m, m2);
     if (mm == -INFINITY) return;
-    s = s * expf(m - mm) + s2 * expf(m2 - mm);
+    s = s * __expf(m - mm) + s2 * __expf(m2 - mm);
     m = mm;
 }
 // one chunk of policy tiles: a row's logits (+ bias) in the tiles it keeps a column in (`allc`:
@@ -477,9 +477,9 @@ __device__ __forceinline__ void pi_chunk(const _Float16* A, int sa, W2 (&ring)[R
 #pragma unroll
         for (int t = 0; t < NTL; t++) mn = fmaxf(mn, pa[t][j]);
         if (mn != -INFINITY) {
-            float acc = ss[j] > 0.f ? ss[j] * expf(sm[j] - mn) : 0.f;
+            float acc = ss[j] > 0.f ? ss[j] * __expf(sm[j] - mn) : 0.f;
 #pragma unroll
-            for (int t = 0; t < NTL; t++) acc += expf(pa[t][j] - mn);
+            for (int t = 0; t < NTL; t++) acc += __expf(pa[t][j] - mn);
             sm[j] = mn;
             ss[j] = acc;
         }

@@ -79,7 +79,7 @@ __global__ void k_leaf_prior(const float* __restrict__ logits, const float2* __r
     const float* x = logits + (long)row * PI_LD;
     const float2 ml = mlse[row];
     for (int a = lane; a < ASIZE; a += 64)
-        pi[(long)row * ASIZE + a] = action_valid(s, 1, a) ? expf(x[a] - ml.x - ml.y) : 0.f;  // the expand's exp
+        pi[(long)row * ASIZE + a] = action_valid(s, 1, a) ? exp_acc(x[a] - ml.x - ml.y) : 0.f;  // the expand's exp
 }
 
 // The submission bot's move (agent.py:248-280): softmax over all 3226 logits in f32, then the
