@@ -324,7 +324,7 @@ __device__ __forceinline__ void put_planes2(_Float16* planes, int sa, int r, int
 // chunk, NTL <= PCH in a wave's last chunk.  The ring (RD slices of PCH tiles) streams across
 // chunk boundaries: past the last slice it refills with the next chunk's first slices (NXT tiles).
 // Chunk shapes are template parameters, so the loop body has no branches.
-template <int PL, int KS, int NTL, int NXT, int PC = PCH, int RD = (pw_of(PL) < KS ? pw_of(PL) : KS)>
+template <int PL, int KS, int NTL, int NXT, int PC = PCH, int RD = (pw_of(PL) < KS ? pw_of(PL) : KS), bool LL = true>
 __device__ __forceinline__ void ring_chunk(const _Float16* A, int sa, W2 (&ring)[RD][PC], floatx4 (&pa)[NTL],
                                            const float* __restrict__ W, const int (&tile)[PC],
                                            const float* __restrict__ Wn, const int (&ntile)[PC]) {
@@ -346,9 +346,11 @@ __device__ __forceinline__ void ring_chunk(const _Float16* A, int sa, W2 (&ring)
             for (int t = 0; t < NTL; t++) c[t].c = mfma16(ah, w[t].l, c[t].c);
 #pragma unroll
             for (int t = 0; t < NTL; t++) c[t].c = mfma16(al, w[t].h, c[t].c);
-            const float4 als = lo_scaled(al);
+            if constexpr (LL) {
+                const float4 als = lo_scaled(al);
 #pragma unroll
-            for (int t = 0; t < NTL; t++) c[t].c = mfma16(als, w[t].l, c[t].c);
+                for (int t = 0; t < NTL; t++) c[t].c = mfma16(als, w[t].l, c[t].c);
+            }
         }
         const int g = ks + RD;
         if (g < KS) {
@@ -448,6 +450,10 @@ __device__ __forceinline__ void stat_merge(float& m, float& s, float m2, float s
 // one chunk of policy tiles: a row's logits (+ bias) in the tiles it keeps a column in (`allc`:
 // every real column) - a set that depends on the row alone - stored and folded into its running
 // (max, sum exp): one rescale per row and chunk.  Lane (q, c) holds rows 4 q + j, column c.
+// Three products, not four: the lo*lo term pays in the trunk, where its error compounds over 13
+// layers, and not in this one layer (tools/prior_error_emulation.py: P's max relative error
+// 3.59e-5 with lo*lo in the trunk only, 3.59e-5 everywhere, 7.47e-5 in the head only; torch f32
+// 4.79e-5), while the head holds most of the forward's MFMAs.
 template <int PL, int KS, int NTL, int NXT, int PC = PCH, int RD = (pw_of(PL) < KS ? pw_of(PL) : KS)>
 __device__ __forceinline__ void pi_chunk(const _Float16* A, int sa, W2 (&ring)[RD][PC], const float* __restrict__ W,
                                          const int (&tile)[PC], const int (&ntile)[PC], const float* bias,
@@ -455,7 +461,7 @@ __device__ __forceinline__ void pi_chunk(const _Float16* A, int sa, W2 (&ring)[R
                                          const uint16_t* trb, const bool (&allc)[4]) {
     const int lane = threadIdx.x & 63;
     floatx4 pa[NTL];
-    ring_chunk<PL, KS, NTL, NXT, PC, RD>(A, sa, ring, pa, W, tile, W, ntile);
+    ring_chunk<PL, KS, NTL, NXT, PC, RD, false>(A, sa, ring, pa, W, tile, W, ntile);  // no lo*lo (below)
     const int rr = lane & 15, q = lane >> 4;
 #pragma unroll
     for (int t = 0; t < NTL; t++) {

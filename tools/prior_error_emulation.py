@@ -116,21 +116,25 @@ def layernorm(x, g, b, cfg, H):
 
 def forward(sd, X, cfg, H=256, NB=6):
     L = lambda name: (np.asarray(sd[name + ".weight"], F32), np.asarray(sd[name + ".bias"], F32))
+    only = cfg.get("lolo_only")  # the lo*lo product in these layers only ("inp", "trunk", "head")
+
+    def G(A, W, where):
+        return gemm(A, W, cfg if only is None else dict(cfg, lolo=cfg["lolo"] if where in only else False))
     w, b = L("inp.0")
     g, be = L("inp.1")
-    h = silu(layernorm(gemm(X, w, cfg) + b, g, be, cfg, H), cfg)
+    h = silu(layernorm(G(X, w, "inp") + b, g, be, cfg, H), cfg)
     for k in range(NB):
         w1, b1 = L(f"blocks.{k}.fc1")
         g1, e1 = L(f"blocks.{k}.ln1")
         w2, b2 = L(f"blocks.{k}.fc2")
         g2, e2 = L(f"blocks.{k}.ln2")
-        t = layernorm(silu(gemm(h, w1, cfg) + b1, cfg), g1, e1, cfg, H)
-        t = layernorm(silu(gemm(t, w2, cfg) + b2, cfg), g2, e2, cfg, H)
+        t = layernorm(silu(G(h, w1, "trunk") + b1, cfg), g1, e1, cfg, H)
+        t = layernorm(silu(G(t, w2, "trunk") + b2, cfg), g2, e2, cfg, H)
         h = (h + t).astype(F32)
     gp, bp = L("pi_head.0")
     wp, bpi = L("pi_head.2")
     a = silu(layernorm(h, gp, bp, cfg, H), cfg)
-    return (gemm(a, wp, cfg) + bpi).astype(F32)
+    return (G(a, wp, "head") + bpi).astype(F32)
 
 
 def leaf_prior(logits, ok):
@@ -192,6 +196,9 @@ def main():
         ("IEEE SiLU + two-pass LN", dict(ieee_silu=True, twopass_ln=True)),
         ("lo*lo + IEEE SiLU + two-pass LN", dict(lolo=True, ieee_silu=True, twopass_ln=True)),
         ("lo*lo (scaled) + exact activations", dict(lolo="scaled", exact_a=True)),
+        ("lo*lo (scaled) in the policy head only", dict(lolo="scaled", lolo_only=("head",))),
+        ("lo*lo (scaled) in the input layer + policy head", dict(lolo="scaled", lolo_only=("inp", "head"))),
+        ("lo*lo (scaled) in the trunk only", dict(lolo="scaled", lolo_only=("inp", "trunk"))),
     ]
     e_r = err(Pr)
     print(f"{len(S)} fixture states with a valid action, weights {args.weights}, ulp noise {args.ulp_noise}; "
