@@ -141,17 +141,22 @@ struct KeepCache {
     int layer = -1;
     uint32_t m = 0;
 };
+// the keep bits of elements 4 g .. 4 g + 3 of a dropout layer: one Philox draw, four 16-bit uniforms
+__device__ inline uint32_t dropout_bits(uint64_t seed, int layer, uint64_t step, long g, float p) {
+    const uint64_t d = philox_draw(seed, 0x44524F50u + (uint32_t)layer, (step << 32) ^ (uint64_t)g);
+    uint32_t m = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++)  // (a 32-bit value into the conversion: a 64-bit one is a long sequence)
+        m |= ((float)(uint32_t)((d >> (16 * k)) & 0xFFFFu) * (1.0f / 65536.0f) >= p ? 1u : 0u) << k;
+    return m;
+}
 __device__ inline bool dropout_keep(KeepCache& kc, uint64_t seed, int layer, uint64_t step, long e, float p) {
     if (p <= 0.0f) return true;
     const long g = e >> 2;
     if (g != kc.g || layer != kc.layer) {
-        const uint64_t d = philox_draw(seed, 0x44524F50u + (uint32_t)layer, (step << 32) ^ (uint64_t)g);
-        uint32_t m = 0;
-#pragma unroll
-        for (int k = 0; k < 4; k++) m |= ((float)((d >> (16 * k)) & 0xFFFFu) * (1.0f / 65536.0f) >= p ? 1u : 0u) << k;
         kc.g = g;
         kc.layer = layer;
-        kc.m = m;
+        kc.m = dropout_bits(seed, layer, step, g, p);
     }
     return (kc.m >> (e & 3)) & 1u;
 }

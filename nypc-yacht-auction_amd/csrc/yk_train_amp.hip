@@ -76,6 +76,7 @@ struct AmpDev {
     float *z0, *u1, *u2, *hF, *stats;
     float *logits, *zv1, *lse;
     float2* mlq;
+    uint8_t* masks;                       // [1 + NB][Bmax][H / 4] the step's dropout keep bits (k_amp_masks)
     _Float16 *dz1_rm, *dz1T, *dlT, *dz0T, *du1T, *du2T;
     float *dz1f, *v2prod, *dzv2, *dpart, *dbpi_part, *colpart;
     Scaler* sc;
@@ -133,7 +134,11 @@ __device__ __forceinline__ void wsum2(float& a, float& b) {
     a = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, a), 63));
     b = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, b), 63));
 }
-__device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
+// the logistic as the inference forward computes it (yk_fwd.h silu): the native exp and reciprocal.
+// Autocast rounds SiLU's result to fp16 (or feeds it to an fp16 Linear), so their ~1e-6 relative
+// error moves only the rare value that sits within it of an fp16 rounding boundary; the library
+// expf + IEEE division cost 15 us of a 192 us step (k_amp_fwd 59.8 -> 51.3 us, k_amp_bwd 64.5 -> 58.7)
+__device__ __forceinline__ float sigm(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
 __device__ __forceinline__ float silu(float x) { return x * sigm(x); }
 __device__ __forceinline__ float silu_grad(float x) {
     const float s = sigm(x);
@@ -250,6 +255,21 @@ __device__ __forceinline__ void ln_bwd(const float (&xh)[VPL], float (&dx)[VPL],
 __device__ __forceinline__ float* stat_ptr(const AmpDev& d, int layer, int which) {
     return d.stats + ((long)layer * 2 + which) * d.Bmax;
 }
+// the keep bits of the lane's VPL elements c0 .. c0 + VPL - 1 (bit i: element c0 + i) of dropout
+// layer L (0: inp, 1 + b: block b's fc1) in row `row`, from the bytes k_amp_masks wrote (4 bits each)
+template <int VPL>
+__device__ __forceinline__ uint32_t mask_bits(const AmpDev& d, int L, int row, int c0) {
+    const int H = VPL * 64;
+    const uint8_t* m = d.masks + ((long)L * d.Bmax + row) * (H / 4) + (c0 >> 2);
+    if constexpr (VPL == 8) {
+        const uint32_t w = *reinterpret_cast<const uint16_t*>(m);
+        return (w & 15u) | ((w >> 4) & 0xF0u);
+    } else if constexpr (VPL == 4) {
+        return *m;
+    } else {
+        return ((uint32_t)*m >> (c0 & 3)) & ((1u << VPL) - 1u);
+    }
+}
 // per-wave column partials of up to 3 vectors (LDS CP[TW][3][H]) summed over the waves in wave
 // order into colpart[tile][v0 + k][H]
 template <int H>
@@ -260,6 +280,20 @@ __device__ __forceinline__ void colpart_flush(const AmpDev& d, const float* CP, 
         for (int w = 0; w < TW; w++) s += CP[w * 3 * H + i];
         d.colpart[((long)tile * d.NVEC + v0) * H + i] = s;
     }
+}
+
+// The step's dropout keep bits (the draws dropout_keep makes, yk_common.h) for every dropout layer,
+// generated across the whole chip before the forward: the 32 row tiles of k_amp_fwd / k_amp_bwd then
+// read 4 bits per byte instead of each running the Philox rounds in its row passes (~2K ticks per
+// dropout layer and tile, on 32 CUs).  One thread per byte: layer, row, 4-element group.
+__global__ __launch_bounds__(256) void k_amp_masks(AmpDev d, int B, float p, uint64_t seed, uint64_t step,
+                                                   int64_t row_base) {
+    const int q4 = d.H / 4;
+    const long i = (long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (long)(1 + d.NB) * B * q4) return;
+    const int q = (int)(i % q4), row = (int)((i / q4) % B), L = (int)(i / ((long)q4 * B));
+    d.masks[((long)L * d.Bmax + row) * q4 + q] =
+        (uint8_t)dropout_bits(seed, L, step, (row_base + row) * q4 + q, p);
 }
 
 // ------------------------------------------------------------------ forward (trunk)
@@ -285,10 +319,16 @@ __global__ __launch_bounds__(TTHR) void k_amp_fwd(AmpDev d, const yk_state_t* __
     const float sc = p > 0.f ? 1.0f / (1.0f - p) : 1.0f;
     const int NB = d.NB;
     const long HH8 = (long)H * H / 8;  // float4 per packed H x H matrix
-    KeepCache kc;  // dropout masks (yk_common.h), one Philox draw per 4 elements
+    const bool drop = p > 0.f;  // the keep bits: k_amp_masks
 
     // the input layer's vectors, its weights (K = 64: 2 slices), the first block's ring, then features
     for (int i = tid; i < 3 * H; i += TTHR) VL[i] = d.P[poff(H, d.NB, T_BIN + i / H) + i % H];
+    uint32_t mk[TRPW];  // the current dropout layer's keep bits of the wave's rows
+#pragma unroll
+    for (int rr = 0; rr < TRPW; rr++) {
+        const int row = row0 + wave * TRPW + rr;
+        mk[rr] = drop ? mask_bits<VPL>(d, 0, row < B ? row : 0, c0) : 0xFFu;
+    }
     float4 w0[2][NT];
     if (gw) {
 #pragma unroll
@@ -354,7 +394,7 @@ __global__ __launch_bounds__(TTHR) void k_amp_fwd(AmpDev d, const yk_state_t* __
 #pragma unroll
             for (int i = 0; i < VPL; i++) {
                 const float a = (x[i] - mu) * rs * VL[H + c0 + i] + VL[2 * H + c0 + i];
-                const bool k = dropout_keep(kc, seed, 0, step, (row_base + row) * H + c0 + i, p);
+                const bool k = (mk[rr] >> i) & 1u;
                 x[i] = k ? silu(a) * sc : 0.f;
             }
         } else {
@@ -380,6 +420,13 @@ __global__ __launch_bounds__(TTHR) void k_amp_fwd(AmpDev d, const yk_state_t* __
                 const int i = tid + TTHR * k;
                 const int ic = i < 3 * H ? i : 3 * H - 1;  // unconditional: no branch join before the ring
                 vr[k] = d.P[poff(H, d.NB, t_blk(b, kb + ic / H)) + ic % H];
+            }
+            if (half == 0) {  // block b's fc1 dropout bits, with the vectors (ahead of the ring's refills)
+#pragma unroll
+                for (int rr = 0; rr < TRPW; rr++) {
+                    const int row = row0 + wave * TRPW + rr;
+                    mk[rr] = drop ? mask_bits<VPL>(d, 1 + b, row < B ? row : 0, c0) : 0xFFu;
+                }
             }
             const float4* cur = (half == 0 ? d.w1f : d.w2f) + b * HH8;
             const float4* nxt = half == 0 ? d.w2f + b * HH8 : (b + 1 < NB ? d.w1f + (b + 1) * HH8 : nullptr);
@@ -414,7 +461,7 @@ __global__ __launch_bounds__(TTHR) void k_amp_fwd(AmpDev d, const yk_state_t* __
                     for (int i = 0; i < VPL; i++) {
                         const float l = (s[i] - mu) * rs * VL[H + c0 + i] + VL[2 * H + c0 + i];
                         if (half == 0) {
-                            const bool k = dropout_keep(kc, seed, 1 + b, step, (row_base + row) * H + c0 + i, p);
+                            const bool k = (mk[rr] >> i) & 1u;
                             x[i] = k ? l * sc : 0.f;
                         } else {
                             x[i] = Xs[r * LD + c0 + i] + l;  // residual (f32)
@@ -750,10 +797,11 @@ struct RowPre {
     float u[TRPW][VPL];  // the layer's saved pre-activation (block layers) or Z0 (input layer)
     float mu[TRPW], rs[TRPW];
     float g[VPL], be[VPL];
+    uint32_t mk[TRPW];  // the dropout layer's keep bits (k_amp_masks), when the pass has one
 };
 template <int H>
 __device__ __forceinline__ void row_prefetch(RowPre<H / 64>& R, const AmpDev& d, const float* U, int L, int tg, int tb,
-                                             int row0, int B) {
+                                             int row0, int B, int ML, bool drop) {
     constexpr int VPL = H / 64;
     const int wave = threadIdx.x >> 6, c0 = (threadIdx.x & 63) * VPL;
 #pragma unroll
@@ -764,6 +812,7 @@ __device__ __forceinline__ void row_prefetch(RowPre<H / 64>& R, const AmpDev& d,
         for (int i = 0; i < VPL; i++) R.u[rr][i] = U[(long)rc * H + c0 + i];
         R.mu[rr] = stat_ptr(d, L, 0)[rc];
         R.rs[rr] = stat_ptr(d, L, 1)[rc];
+        R.mk[rr] = drop ? mask_bits<VPL>(d, ML, rc, c0) : 0xFFu;
     }
     const float* g = d.P + poff(H, d.NB, tg);
     const float* be = d.P + poff(H, d.NB, tb);
@@ -810,7 +859,7 @@ __global__ __launch_bounds__(TTHR) void k_amp_bwd(AmpDev d, int B, float p, uint
     const float sc = p > 0.f ? 1.0f / (1.0f - p) : 1.0f;
     const int NB = d.NB;
     const long HH8 = (long)H * H / 8;
-    KeepCache kc;
+    const bool drop = p > 0.f;  // the keep bits: k_amp_masks
     const long TLH = (long)(H / 16) * d.RS * 512;  // halves per T-layout [32 RS][H] matrix
     float* cp = CP + wave * 3 * H;
 
@@ -869,7 +918,7 @@ __global__ __launch_bounds__(TTHR) void k_amp_bwd(AmpDev d, int B, float p, uint
     RowPre<VPL> R;  // (one call on selected operands, and the ring filled whatever NB is - from a large
                     // enough matrix when NB = 0 - so no branch joins before the heads pass's waits)
     row_prefetch<H>(R, d, NB > 0 ? d.u2 + (long)(NB - 1) * d.Bmax * H : d.z0, NB > 0 ? 2 * NB : 0,
-                    NB > 0 ? t_blk(NB - 1, 6) : (int)T_GIN, NB > 0 ? t_blk(NB - 1, 7) : (int)T_BEIN, row0, B);
+                    NB > 0 ? t_blk(NB - 1, 6) : (int)T_GIN, NB > 0 ? t_blk(NB - 1, 7) : (int)T_BEIN, row0, B, 0, drop);
     __builtin_amdgcn_sched_barrier(0);
     float4 ring[RW][NT];
     if (gw) ring_fill<KS, NT, RW>(ring, NB > 0 ? d.w2t + (NB - 1) * HH8 : d.wpit, nt0);
@@ -936,7 +985,7 @@ __global__ __launch_bounds__(TTHR) void k_amp_bwd(AmpDev d, int B, float p, uint
                         if (half == 1) {
                             dl = Xs[r * LD + c];
                         } else {
-                            const bool k = dropout_keep(kc, seed, 1 + b, step, (row_base + row) * H + c, p);
+                            const bool k = (R.mk[rr] >> i) & 1u;
                             dl = k ? r16(Ts[r * LD + c]) * sc : 0.f;
                         }
                     }
@@ -963,7 +1012,7 @@ __global__ __launch_bounds__(TTHR) void k_amp_bwd(AmpDev d, int B, float p, uint
                 const int Lp = h1 ? 1 + 2 * b : more ? 2 * b : 0;
                 const int tg = h1 ? t_blk(b, 2) : more ? t_blk(b - 1, 6) : (int)T_GIN;
                 const int tb = h1 ? t_blk(b, 3) : more ? t_blk(b - 1, 7) : (int)T_BEIN;
-                row_prefetch<H>(R, d, Up, Lp, tg, tb, row0, B);
+                row_prefetch<H>(R, d, Up, Lp, tg, tb, row0, B, h1 ? 1 + b : 0, drop);  // (next: b's fc1 dropout / inp's)
             }
             __builtin_amdgcn_sched_barrier(0);
             const float4* cur = (half == 1 ? d.w2t : d.w1t) + b * HH8;
@@ -995,7 +1044,7 @@ __global__ __launch_bounds__(TTHR) void k_amp_bwd(AmpDev d, int B, float p, uint
             xh[i] = (R.u[rr][i] - R.mu[rr]) * R.rs[rr];
             float ds = 0.f;
             if (row < B) {
-                const bool k = dropout_keep(kc, seed, 0, step, (row_base + row) * H + c, p);
+                const bool k = (R.mk[rr] >> i) & 1u;
                 const float da = k ? Xs[r * LD + c] * sc : 0.f;
                 ds = da * silu_grad(xh[i] * R.g[i] + R.be[i]);
             }
@@ -1412,6 +1461,7 @@ int amp_create(AmpTrain** out, int H, int NB, int Bmax, float* P, float* G, cons
     AA(d.zv1, Bm * VH);
     AA(d.lse, Bm);
     AA(d.mlq, (size_t)HQ * Bm);
+    AA(d.masks, (size_t)(1 + NB) * Bm * (H / 4));
     AA(d.dz1_rm, Bm * VH);
     AA(d.dz1T, (size_t)(VH / 16) * RS * 512);
     AA(d.dlT, (size_t)PT * RS * 512);
@@ -1564,6 +1614,12 @@ int amp_backward(AmpTrain* a, const yk_state_t* states, const int32_t* targets, 
         a->lsum = lsum;
     }
     const int T = (B + TR - 1) / TR, rsn = (B + 31) / 32;
+    if (dropout > 0.f) {
+        const long nm = (long)(1 + a->NB) * B * (a->H / 4);
+        hipLaunchKernelGGL(k_amp_masks, dim3((unsigned)((nm + 255) / 256)), dim3(256), 0, s, d, B, dropout, seed, step,
+                           row_base);
+        YK_LAUNCHED();
+    }
     switch (a->H) {
 #define YK_AMP_FWD(HH)                                                                                              \
     case HH:                                                                                                        \

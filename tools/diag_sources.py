@@ -10,6 +10,8 @@ The hooks, each active only under its define (tools/variant_lib.sh NAME -DYK_...
                  (yk_diag_xspan; tools/diag_xspan.py)
   YK_TIMING      per-phase stamps of k_forward's wave 0 and per-wave stamps of one trunk layer's
                  ring waits, A-fragment reads and MFMA groups (g_tstamp, tools/trunk_ablate.cpp)
+  YK_AMP_TIMING  per-wave stamps of residual block 2 in the AMP train forward / backward
+                 (k_amp_fwd / k_amp_bwd phases; yk_diag_amp_ts, tools/diag_amp.py)
 Every anchor must match exactly once; a source change that moves one fails loudly here."""
 import os
 import re
@@ -172,6 +174,50 @@ FWD = [
 ]
 
 
+AMP_GLOBALS = r'''
+// ---- diagnostic hooks (tools/diag_sources.py) ----
+#ifdef YK_AMP_TIMING
+__device__ unsigned long long g_amp_ts[2][64][8][16];  // [fwd, bwd][tile][wave][half * 8 + k]
+#define AMP_STAMP(kk, k)                                                                      \
+    if (b == 2 && (threadIdx.x & 63) == 0 && blockIdx.x < 64)                                 \
+    g_amp_ts[kk][blockIdx.x][threadIdx.x >> 6][half * 8 + (k)] = __builtin_amdgcn_s_memtime()
+extern "C" int yk_diag_amp_ts(void* dst) {
+    return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_amp_ts), sizeof(g_amp_ts)) == hipSuccess ? 0 : -2;
+}
+#else
+#define AMP_STAMP(kk, k)
+#endif
+'''
+# k_amp_fwd, block 2, per half: 0 before the GEMM, 1 GEMM + accumulator store done, 2 the barrier
+# passed, 3 the row pass done, 4 the next barrier passed, 5 the T-layout store done
+AMP = [
+    (r"^constexpr int SQ_BLOCKS = 1024;\n", "after", AMP_GLOBALS),
+    (r"^            const float4\* nxt = half == 0 \? d.w2f.*\n            if \(gw\) \{\n"
+     r"                gemm_ring<KS, NT, RW>\(Pa, SA, ring, acc, cur, nxt, nt0\);\n"
+     r"                store_acc<NT>\(Ts, LD, nt0, acc\);\n            \}\n", "around",
+     ("            AMP_STAMP(0, 0);\n", "            AMP_STAMP(0, 1);\n")),
+    (r"^            lds_barrier\(\);\n            float\* U = ", "after_line1", "            AMP_STAMP(0, 2);\n"),
+    (r"^            lds_barrier\(\);\n            if \(half == 0\) write_tl\(Pa, SA", "around_line1",
+     ("            AMP_STAMP(0, 3);\n", "            AMP_STAMP(0, 4);\n")),
+    (r"^                write_tl\(Pa, SA, 0, H, d.hT \+ \(long\)\(b \+ 1\).*\n", "after", "            AMP_STAMP(0, 5);\n"),
+    # k_amp_bwd, block 2, per half: 0 row pass start, 1 its end, 2 the barrier passed, 3 column
+    # partials flushed, 4 T-layout store done, 5 next row's operands issued, 6 GEMM + store done,
+    # 7 the barrier passed
+    (r"^            // row pass: \(half 1\) dL2 = dh; \(half 0\) dL1", "before", "            AMP_STAMP(1, 0);\n"),
+    (r"^            lds_barrier\(\);\n            flush_gbb<H>", "around_line1",
+     ("            AMP_STAMP(1, 1);\n", "            AMP_STAMP(1, 2);\n")),
+    (r"^            flush_gbb<H>\(d, CP, tile, CV_BLK.*\n", "after", "            AMP_STAMP(1, 3);\n"),
+    (r"^            write_tl\(Pa, SA, 0, H, \(half == 0 \? d.du1T.*\n", "after", "            AMP_STAMP(1, 4);\n"),
+    (r"^            __builtin_amdgcn_sched_barrier\(0\);\n            const float4\* cur = \(half == 1", "after_line1",
+     "            AMP_STAMP(1, 5);\n"),
+    (r"^            const float4\* nxt = half == 1 \? d.w1t.*\n            if \(gw\) \{\n"
+     r"                gemm_ring<KS, NT, RW>\(Pa, SA, ring, acc, cur, nxt, nt0\);\n"
+     r"                store_acc<NT>\(Ts, LD, nt0, acc\);\n            \}\n", "after", "            AMP_STAMP(1, 6);\n"),
+    (r"^            lds_barrier\(\);\n            if \(half == 0\) \{  // residual", "after_line1",
+     "            AMP_STAMP(1, 7);\n"),
+]
+
+
 def apply(text, rules, name):
     for pat, where, ins in rules:
         ms = list(re.finditer(pat, text, flags=re.M))
@@ -226,6 +272,12 @@ def main():
     with open(p) as f:
         text = f.read()
     text = apply(text, FWD, "yk_fwd.h")
+    with open(p, "w") as f:
+        f.write(text)
+    p = os.path.join(dst, "yk_train_amp.hip")
+    with open(p) as f:
+        text = f.read()
+    text = apply(text, AMP, "yk_train_amp.hip")
     with open(p, "w") as f:
         f.write(text)
     print(dst)

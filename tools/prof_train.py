@@ -18,7 +18,7 @@ n = 8192
 out, _ = K.init_board(0, np.arange(n), 0)
 tg = torch.tensor(rng.randint(0, 202, n), dtype=torch.int32, device="cuda")
 vv = torch.tensor(rng.rand(n) * 2 - 1, dtype=torch.float32, device="cuda")
-tr = Trainer(sd, 256, 6, max_batch=B, dropout=0.3, amp=os.environ.get("YK_AMP", "0") == "1")
+tr = Trainer(sd, 256, 6, max_batch=B, dropout=float(os.environ.get("YK_DROPOUT", "0.3")), amp=os.environ.get("YK_AMP", "0") == "1")
 for i in range(30):
     idx = torch.arange((i * B) % (n - B), (i * B) % (n - B) + B, dtype=torch.int32, device="cuda")
     tr.step(out, tg, vv, idx=idx)
