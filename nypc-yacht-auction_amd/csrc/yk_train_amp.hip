@@ -1503,11 +1503,14 @@ int amp_create(AmpTrain** out, int H, int NB, int Bmax, float* P, float* G, cons
     }
     jobs.push_back({tl4(d.dlT), tl4(d.apiT), G + off[t_head(NB, HP_W)], ASIZE, H});
     jobs.push_back({tl4(d.dz1T), tl4(d.avT), G + off[t_head(NB, HV_W1)], VH, H});
+    // a workgroup's four waves take four consecutive row tiles of the same 64 columns, so they read
+    // the same X slices together (one fetch from L2 for the four) - the policy head's dW (3226 x 256)
+    // re-read its 256 KB X once per 16-row tile before (202 x)
     std::vector<int4> items;
     for (size_t j = 0; j < jobs.size(); j++) {
         const int ntn = (jobs[j].N + 15) / 16, ntk = (jobs[j].K + 15) / 16;
-        for (int nt = 0; nt < ntn; nt++)
-            for (int k0 = 0; k0 < ntk; k0 += 4) items.push_back(make_int4((int)j, nt, k0, std::min(4, ntk - k0)));
+        for (int k0 = 0; k0 < ntk; k0 += 4)
+            for (int nt = 0; nt < ntn; nt++) items.push_back(make_int4((int)j, nt, k0, std::min(4, ntk - k0)));
     }
     a->n_dw_items = (int)items.size();
     // column-sum jobs: bias / LayerNorm gradients and the two loss sums
