@@ -30,11 +30,15 @@ sys.path.insert(0, REPO)
 
 METRIC = "MCTS node-expansions/sec/GPU @4096 envs x100 sims; episodes/sec 1-8 GPU"
 F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense f16 matrix peak (~2.5 PF)
-SPLIT_PRODUCTS = 4             # k_forward: each f32 product = 4 fp16 MFMA products (hi.hi, hi.lo, lo.hi, lo.lo)
-# the f32-equivalent peak of that arithmetic: what the forward's algorithmic FLOPs are priced against
-SPLIT_PEAK_TFLOPS = F16_MFMA_PEAK_TFLOPS / SPLIT_PRODUCTS
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E spec peak
 H, NB, A = 256, 6, 3226
+# k_forward runs each f32 product as fp16 MFMA products on hi / lo planes: four in the input layer,
+# the trunk and the value head (hi.hi, hi.lo, lo.hi, (lo 2^-11).lo), three in the policy head (no
+# lo.lo: yk_fwd.h pi_chunk).  The f32-equivalent peak the forward's algorithmic FLOPs are priced
+# against is the f16 dense peak over the FLOP-weighted product count (the full 3226-wide head).
+_TRUNK_MAC, _HEAD_MAC = 59 * H + 2 * NB * H * H + H * 128 + 128, H * A
+SPLIT_PRODUCTS = (4 * _TRUNK_MAC + 3 * _HEAD_MAC) / (_TRUNK_MAC + _HEAD_MAC)  # = 3.50
+SPLIT_PEAK_TFLOPS = F16_MFMA_PEAK_TFLOPS / SPLIT_PRODUCTS
 GAME_MOVES = 48  # every Yacht Auction game has exactly 48 real moves: the record image's size
 # algorithmic FLOPs per expansion (one predicted row), YachtNNet.py:24-70 at hidden 256, 6 blocks
 PREDICT_FLOP = 2 * (59 * H + 2 * NB * H * H + H * 128 + 128 + H * A)  # = 3,320,576
@@ -587,8 +591,9 @@ def main():
                    "traffic": tr[0] if tr else None,
                    "traffic_source": tr[1] if tr else None,
                    "work_per_launch": f"{exp_per_launch:.0f} expansions x {PREDICT_FLOP} FLOP (f32)",
-                   "peak_basis": "f16 dense MFMA peak / 4: every f32 product runs as hi*hi + hi*lo + lo*hi + "
-                                 "(lo 2^-11)*lo on fp16 planes with f32 accumulation",
+                   "peak_basis": f"f16 dense MFMA peak / {SPLIT_PRODUCTS:.2f}: every f32 product runs as hi*hi + "
+                                 "hi*lo + lo*hi (+ (lo 2^-11)*lo outside the policy head) on fp16 planes with f32 "
+                                 "accumulation; the product count FLOP-weighted over the layers",
                    "limiter": "per-CU weight stream: each 16-row tile streams all 6.7 MB of weight "
                               "planes through its CU, and one CU streams a weight set shared by all CUs "
                               "at 110-123 GB/s at any CU count; the fp16 MFMAs overlap the stream "

@@ -877,47 +877,31 @@ __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int l
             // score actions at 10 dice (most leaves): a group a .. a + 3 (a = 0 mod 4) holds at
             // most two categories, a's and a + 2's (category starts are 202 + 252 c = 2 mod 4)
             static_assert(NBID % 4 == 2 && NCOMB % 4 == 0, "category starts are 2 mod 4");
-            static_assert(4 * PW_GMAX + PW_TMAX <= 64, "the lane's valid bits fit one mask");
             const bool score10 = valid.mode == 0 && valid.n >= 10;
-            // three passes - the valid bits, every logits load, then the priors - so that all of
-            // the lane's loads are in flight together (a load behind a branch is not moved past
-            // the next group's branch: a fused loop waited for each group's load in turn)
-            uint64_t vm = 0;  // bit 4 j + k: action st + 8 j + 4 h + k; bit 4 PW_GMAX + r: tail r
 #pragma unroll
             for (int j = 0; j < PW_GMAX; j++) {
                 const int a = st + 8 * j + 4 * h;
-                uint32_t b = 0;
+                bool v0, v1, v2, v3;
                 if (score10) {
                     const int b0 = a - NBID, b2 = a + 2 - NBID;
                     const bool lo = j < G && b0 >= 0 && !((valid.used >> ((unsigned)b0 / NCOMB)) & 1u);
                     const bool hi = j < G && b2 >= 0 && !((valid.used >> ((unsigned)b2 / NCOMB)) & 1u);
-                    b = (lo ? 3u : 0u) | (hi ? 12u : 0u);
-                } else if (j < G) {
-                    b = (valid(a) ? 1u : 0u) | (valid(a + 1) ? 2u : 0u) | (valid(a + 2) ? 4u : 0u) | (valid(a + 3) ? 8u : 0u);
+                    v0 = v1 = lo;
+                    v2 = v3 = hi;
+                } else {
+                    v0 = j < G && valid(a);
+                    v1 = j < G && valid(a + 1);
+                    v2 = j < G && valid(a + 2);
+                    v3 = j < G && valid(a + 3);
                 }
-                vm |= (uint64_t)b << (4 * j);
+                float4 x4 = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (v0 || v1 || v2 || v3) x4 = *reinterpret_cast<const float4*>(x + 8 * j + 4 * h);
+                q[j] = make_float4(v0 ? softmax_p(x4.x, mx, lse) : 0.f, v1 ? softmax_p(x4.y, mx, lse) : 0.f,
+                                   v2 ? softmax_p(x4.z, mx, lse) : 0.f, v3 ? softmax_p(x4.w, mx, lse) : 0.f);
             }
 #pragma unroll
             for (int r = 0; r < PW_TMAX; r++)
-                if (h == 0 && r < R && valid(st + 8 * G + r)) vm |= 1ull << (4 * PW_GMAX + r);
-            // (unconditional loads: a group without a valid action reads the lane's first group
-            // again, a line already on its way, instead of a branch per load)
-#pragma unroll
-            for (int j = 0; j < PW_GMAX; j++) {
-                const int o = ((vm >> (4 * j)) & 15u) ? 8 * j + 4 * h : 4 * h;
-                q[j] = *reinterpret_cast<const float4*>(x + o);
-            }
-#pragma unroll
-            for (int r = 0; r < PW_TMAX; r++) qt[r] = x[((vm >> (4 * PW_GMAX + r)) & 1u) ? 8 * G + r : 0];
-#pragma unroll
-            for (int j = 0; j < PW_GMAX; j++) {
-                const uint32_t b = (uint32_t)(vm >> (4 * j));
-                q[j] = make_float4((b & 1u) ? softmax_p(q[j].x, mx, lse) : 0.f, (b & 2u) ? softmax_p(q[j].y, mx, lse) : 0.f,
-                                   (b & 4u) ? softmax_p(q[j].z, mx, lse) : 0.f, (b & 8u) ? softmax_p(q[j].w, mx, lse) : 0.f);
-            }
-#pragma unroll
-            for (int r = 0; r < PW_TMAX; r++)
-                qt[r] = ((vm >> (4 * PW_GMAX + r)) & 1u) ? softmax_p(qt[r], mx, lse) : 0.f;
+                qt[r] = (h == 0 && r < R && valid(st + 8 * G + r)) ? softmax_p(x[8 * G + r], mx, lse) : 0.f;
             v = d.vpred[e];
             masked = true;
         } else {
