@@ -816,7 +816,8 @@ int yk_trainer_apply(yk_trainer_t* t, void* stream) {
     t->step += 1;  // (amp: the dropout stream's step; the optimiser's count of steps taken is on the device)
     if (t->amp)
         return yk::amp_apply(t->amp, t->nparams, t->M, t->V, t->acc + 2, t->cfg.max_grad_norm, t->cfg.lr,
-                             t->cfg.weight_decay, t->cfg.beta1, t->cfg.beta2, t->cfg.eps, s);
+                             t->cfg.weight_decay, t->cfg.beta1, t->cfg.beta2, t->cfg.eps, t->cfg.dropout, t->cfg.seed,
+                             t->step, s);
     const double b1 = t->cfg.beta1, b2 = t->cfg.beta2, st = (double)t->step;
     const double bc1 = 1.0 - std::pow(b1, st), bc2 = 1.0 - std::pow(b2, st);
     const float step_size = (float)(t->cfg.lr / bc1), bc2_sqrt = (float)std::sqrt(bc2);

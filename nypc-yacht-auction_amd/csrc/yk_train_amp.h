@@ -26,9 +26,10 @@ int amp_backward(AmpTrain* a, const yk_state_t* states, const int32_t* targets, 
                  float vloss_weight, float2* lrow, float* lsum, hipStream_t s);
 // GradScaler.unscale_ + clip_grad_norm_(max_norm) + AdamW step (skipped, with the scale halved,
 // when a gradient is inf / nan) + GradScaler.update + fp16 repack.  sq_out: the unscaled grad
-// sq-norm (double).
+// sq-norm (double).  dropout / seed / next_step: the next backward's dropout draws, which the
+// update launch makes ahead (for row offset 0) so that backward needs no mask launch of its own.
 int amp_apply(AmpTrain* a, long nparams, float* M, float* V, double* sq_out, float max_norm, float lr, float wd,
-              float b1, float b2, float eps, hipStream_t s);
+              float b1, float b2, float eps, float dropout, uint64_t seed, uint64_t next_step, hipStream_t s);
 // HOST out[4]: loss scale, growth tracker, optimiser steps taken, whether the last step found inf
 int amp_state(AmpTrain* a, double* out);
 int amp_set_steps(AmpTrain* a, int64_t steps);

@@ -1236,8 +1236,18 @@ __device__ __forceinline__ void adamw_elem(float& p, float& g, float& m, float& 
 __global__ __launch_bounds__(256) void k_amp_update(const UpdJob* __restrict__ jobs, const UpdItem* __restrict__ items,
                                                     const double* __restrict__ part, double* sq_out,
                                                     const Scaler* __restrict__ sc, Scaler* __restrict__ sc_next,
-                                                    float max_norm, float lr, float wd, float b1, float b2, float eps) {
+                                                    float max_norm, float lr, float wd, float b1, float b2, float eps,
+                                                    int n_upd, AmpDev d, float mp, uint64_t mseed, uint64_t mstep) {
     __shared__ _Float16 Tl[32][40];
+    if ((int)blockIdx.x >= n_upd) {  // the blocks past the update's: the next step's dropout draws
+        const int q4 = d.H / 4;       // (k_amp_masks' work for row offset 0 and every row of Bmax)
+        const long i = (long)(blockIdx.x - n_upd) * 256 + threadIdx.x;
+        if (i < (long)(1 + d.NB) * d.Bmax * q4) {
+            const int q = (int)(i % q4), row = (int)((i / q4) % d.Bmax), L = (int)(i / ((long)q4 * d.Bmax));
+            d.masks[((long)L * d.Bmax + row) * q4 + q] = (uint8_t)dropout_bits(mseed, L, mstep, (long)row * q4 + q, mp);
+        }
+        return;
+    }
     const double total = sq_total(part);
     const Scaler s0 = *sc;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -1377,6 +1387,12 @@ struct AmpTrain {
     double* sqpart = nullptr;
     Scaler* sc = nullptr;       // the current GradScaler state
     Scaler* sc_next = nullptr;  // k_amp_update writes the next one here; the host swaps the two
+    // what d.masks holds: the draws of (seed, step, row offset, p) for rows 0 .. mask_rows - 1
+    bool mask_valid = false;
+    uint64_t mask_seed = 0, mask_step = 0;
+    int64_t mask_row_base = 0;
+    float mask_p = 0.f;
+    int mask_rows = 0;
     UpdJob* upd_jobs = nullptr;
     UpdItem* upd_items = nullptr;
     int n_upd_items = 0;
@@ -1617,12 +1633,14 @@ int amp_backward(AmpTrain* a, const yk_state_t* states, const int32_t* targets, 
         a->lsum = lsum;
     }
     const int T = (B + TR - 1) / TR, rsn = (B + 31) / 32;
-    if (dropout > 0.f) {
+    if (dropout > 0.f && !(a->mask_valid && a->mask_seed == seed && a->mask_step == step && a->mask_row_base == row_base &&
+                           a->mask_p == dropout && a->mask_rows >= B)) {  // (not made ahead by the last update)
         const long nm = (long)(1 + a->NB) * B * (a->H / 4);
         hipLaunchKernelGGL(k_amp_masks, dim3((unsigned)((nm + 255) / 256)), dim3(256), 0, s, d, B, dropout, seed, step,
                            row_base);
         YK_LAUNCHED();
     }
+    a->mask_valid = false;  // consumed by this step: the next update writes the next step's
     switch (a->H) {
 #define YK_AMP_FWD(HH)                                                                                              \
     case HH:                                                                                                        \
@@ -1699,16 +1717,24 @@ static int build_update_jobs(AmpTrain* a, long nparams, float* M, float* V) {
 }
 
 int amp_apply(AmpTrain* a, long nparams, float* M, float* V, double* sq_out, float max_norm, float lr, float wd,
-              float b1, float b2, float eps, hipStream_t s) {
+              float b1, float b2, float eps, float dropout, uint64_t seed, uint64_t next_step, hipStream_t s) {
     if (a->upd_M != M || a->upd_V != V) {  // the update jobs address the trainer's moment buffers
         const int rc = build_update_jobs(a, nparams, M, V);
         if (rc != YK_OK) return rc;
     }
     hipLaunchKernelGGL(k_amp_sq, dim3(SQ_BLOCKS), dim3(256), 0, s, a->d.G, nparams, a->sc, a->sqpart);
     YK_LAUNCHED();
-    hipLaunchKernelGGL(k_amp_update, dim3((unsigned)a->n_upd_items), dim3(256), 0, s, a->upd_jobs, a->upd_items,
-                       a->sqpart, sq_out, a->sc, a->sc_next, max_norm, lr, wd, b1, b2, eps);
+    const long nm = dropout > 0.f ? (long)(1 + a->NB) * a->Bmax * (a->H / 4) : 0;
+    hipLaunchKernelGGL(k_amp_update, dim3((unsigned)(a->n_upd_items + (nm + 255) / 256)), dim3(256), 0, s, a->upd_jobs,
+                       a->upd_items, a->sqpart, sq_out, a->sc, a->sc_next, max_norm, lr, wd, b1, b2, eps, a->n_upd_items,
+                       a->d, dropout, seed, next_step);
     YK_LAUNCHED();
+    a->mask_valid = nm > 0;
+    a->mask_seed = seed;
+    a->mask_step = next_step;
+    a->mask_row_base = 0;
+    a->mask_p = dropout;
+    a->mask_rows = a->Bmax;
     std::swap(a->sc, a->sc_next);  // the next launches read the updated GradScaler state
     a->d.sc = a->sc;
     return YK_OK;
