@@ -44,10 +44,14 @@ typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 
 namespace {
 
-constexpr int TR = 16;          // rows per tile (the MFMA M)
+constexpr int TR = 16;          // rows per tile (the MFMA M): the heads' row tiles
+constexpr int TRV = 8;          // rows per trunk workgroup (k_amp_fwd / k_amp_bwd): the MFMAs still
+                                // run 16 rows, the last 8 of them ignored, so a 512-example step
+                                // spreads its row passes (the VALU-bound part of a layer) over 64
+                                // CUs instead of 32 (each still streams the whole weight set)
 constexpr int TW = 8;           // waves per trunk workgroup
 constexpr int TTHR = 64 * TW;
-constexpr int TRPW = TR / TW;   // rows per wave in the row passes
+constexpr int TRPW = TRV / TW;  // rows per wave in the row passes
 constexpr int LDL = 3264;       // logits row stride: 204 tiles of 16 columns
 constexpr int PT = LDL / 16;    // policy column tiles
 constexpr int PKS = LDL / 32;   // 32-deep action slices
@@ -153,21 +157,24 @@ __device__ __forceinline__ void stat_merge(float& m, float& s, float m2, float s
     m = mm;
 }
 
-// The tile's 16 rows of an fp16 plane (LDS, row stride sa halves; columns col0 .. col0 + C) into
-// the T layout at column tile offset ct0; the last tile of an odd tile count also zeroes the
-// slice's other half (rows past the batch must not enter a weight gradient).
+// The tile's R rows (R = 8 or 16) of an fp16 plane (LDS, row stride sa halves; columns col0 ..
+// col0 + C) into the T layout at column tile offset ct0: a 32-row slice holds 32 / R tiles, lane
+// group q = lane >> 4 rows 8 q .. 8 q + 7 of it.  The batch's last tile (zero_rest) also zeroes
+// the rest of its slice (rows past the batch must not enter a weight gradient).
+template <int R>
 __device__ __forceinline__ void write_tl(const _Float16* A, int sa, int col0, int C, _Float16* dst, int RS, int ct0,
-                                         int tile, bool zero_half) {
+                                         int tile, bool zero_rest) {
+    constexpr int QPT = R / 8, TPS = 32 / R;  // lane groups per tile, tiles per slice
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    const int h = tile & 1, rs = tile >> 1, q = lane >> 4;
-    const bool mine = (q >> 1) == h;
+    const int h = tile % TPS, rs = tile / TPS, q = lane >> 4;
+    const bool mine = q / QPT == h, after = q / QPT > h;
     for (int ct = wave; ct < C / 16; ct += nw) {
         half8 v = {};
         if (mine) {
 #pragma unroll
-            for (int j = 0; j < 8; j++) v[j] = A[(8 * (q - 2 * h) + j) * sa + col0 + 16 * ct + (lane & 15)];
+            for (int j = 0; j < 8; j++) v[j] = A[(8 * (q - QPT * h) + j) * sa + col0 + 16 * ct + (lane & 15)];
         }
-        if (mine || zero_half)
+        if (mine || (zero_rest && after))
             *reinterpret_cast<half8*>(dst + (((long)(ct0 + ct) * RS + rs) * 64 + lane) * 8) = v;
     }
 }
@@ -308,14 +315,14 @@ __global__ __launch_bounds__(TTHR) void k_amp_fwd(AmpDev d, const yk_state_t* __
     __shared__ __attribute__((aligned(16))) float Ts[TR * LD];
     __shared__ __attribute__((aligned(16))) _Float16 Pa[TR * SA];
     __shared__ __attribute__((aligned(16))) float VL[(3 * H + TTHR - 1) / TTHR * TTHR];  // (padded: unconditional writes)
-    const int tile = blockIdx.x, row0 = tile * TR;
+    const int tile = blockIdx.x, row0 = tile * TRV;
     const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     // every wave owns columns when NACT == TW (hidden >= 128): a compile-time true, so no branch
     // around the weight ring (at a branch join the wait counters merge to the stricter count, and
     // a vmcnt(0) there would drain the ring's in-flight refills)
     const bool gw = NACT == TW || wave < NACT;
     const int nt0 = wave * NT, c0 = lane * VPL;
-    const bool zero_half = row0 + TR >= B && (tile & 1) == 0;
+    const bool zero_rest = row0 + TRV >= B;
     const float sc = p > 0.f ? 1.0f / (1.0f - p) : 1.0f;
     const int NB = d.NB;
     const long HH8 = (long)H * H / 8;  // float4 per packed H x H matrix
@@ -345,10 +352,10 @@ __global__ __launch_bounds__(TTHR) void k_amp_fwd(AmpDev d, const yk_state_t* __
     float4 ring[RW][NT];
     if (gw) ring_fill<KS, NT, RW>(ring, NB > 0 ? d.w1f : d.wpif, nt0);  // (whatever NB is: no branch join)
 #pragma unroll
-    for (int k = 0; k < 2; k++) {  // state_to_vec (NNet.py:65-86), K padded to 64
+    for (int k = 0; k < 2; k++) {  // state_to_vec (NNet.py:65-86), K padded to 64 (rows past TRV: zeros)
         const int r = wave + TW * k, row = row0 + r;
         float x = 0.f;
-        if (row < B) {
+        if (row < B && r < TRV) {
             const int src = __builtin_amdgcn_readfirstlane(idx ? idx[row] : row);
             YkS s;
             const uint64_t* q = reinterpret_cast<const uint64_t*>(states + src);
@@ -359,7 +366,7 @@ __global__ __launch_bounds__(TTHR) void k_amp_fwd(AmpDev d, const yk_state_t* __
         Pa[r * SA + lane] = (_Float16)x;
     }
     lds_barrier();
-    write_tl(Pa, SA, 0, 64, d.xT, d.RS, 0, tile, zero_half);
+    write_tl<TRV>(Pa, SA, 0, 64, d.xT, d.RS, 0, tile, zero_rest);
     floatx4 acc[NT];
     if (gw) {  // inp.0: Z0 = fp16(x16 W_in^T + b16)
         const _Float16* ap = Pa + (lane & 15) * SA + 8 * (lane >> 4);
@@ -408,7 +415,7 @@ __global__ __launch_bounds__(TTHR) void k_amp_fwd(AmpDev d, const yk_state_t* __
         }
     }
     lds_barrier();
-    if (NB > 0) write_tl(Pa, SA, 0, H, d.hT, d.RS, 0, tile, zero_half);
+    if (NB > 0) write_tl<TRV>(Pa, SA, 0, H, d.hT, d.RS, 0, tile, zero_rest);
 
     // ResidualBlock x NB: h = LN1(SiLU(fc1 x)); h = Dropout(h); h = LN2(SiLU(fc2 h)); x + h  YachtNNet.py:8-21
     for (int b = 0; b < NB; b++) {
@@ -478,9 +485,9 @@ __global__ __launch_bounds__(TTHR) void k_amp_fwd(AmpDev d, const yk_state_t* __
                 }
             }
             lds_barrier();
-            if (half == 0) write_tl(Pa, SA, 0, H, d.r1T + (long)b * (H / 16) * d.RS * 512, d.RS, 0, tile, zero_half);
+            if (half == 0) write_tl<TRV>(Pa, SA, 0, H, d.r1T + (long)b * (H / 16) * d.RS * 512, d.RS, 0, tile, zero_rest);
             else if (b + 1 < NB)
-                write_tl(Pa, SA, 0, H, d.hT + (long)(b + 1) * (H / 16) * d.RS * 512, d.RS, 0, tile, zero_half);
+                write_tl<TRV>(Pa, SA, 0, H, d.hT + (long)(b + 1) * (H / 16) * d.RS * 512, d.RS, 0, tile, zero_rest);
         }
     }
 
@@ -517,9 +524,9 @@ __global__ __launch_bounds__(TTHR) void k_amp_fwd(AmpDev d, const yk_state_t* __
         }
     }
     lds_barrier();
-    write_tl(Pa, SA, 0, H, d.apiT, d.RS, 0, tile, zero_half);
-    write_tl(Pv, SA, 0, H, d.avT, d.RS, 0, tile, zero_half);
-    for (int i = tid; i < TR * H / 8; i += TTHR) {  // row-major copies: the head kernel's A operands
+    write_tl<TRV>(Pa, SA, 0, H, d.apiT, d.RS, 0, tile, zero_rest);
+    write_tl<TRV>(Pv, SA, 0, H, d.avT, d.RS, 0, tile, zero_rest);
+    for (int i = tid; i < TRV * H / 8; i += TTHR) {  // row-major copies: the head kernel's A operands
         const int r = i / (H / 8), c8 = i % (H / 8), row = row0 + r;
         if (row < B) {
             reinterpret_cast<float4*>(d.api_rm + (long)row * H)[c8] = *reinterpret_cast<const float4*>(Pa + r * SA + 8 * c8);
@@ -749,7 +756,7 @@ __global__ __launch_bounds__(TTHR) void k_amp_headbwd(AmpDev d, const int32_t* _
         }
     }
     lds_barrier();
-    write_tl(DL, SD, 0, W, d.dlT, d.RS, 2 * ks0, tile, row0 + TR >= B && (tile & 1) == 0);
+    write_tl<TR>(DL, SD, 0, W, d.dlT, d.RS, 2 * ks0, tile, row0 + TR >= B);
     for (int c = tid; c < W; c += TTHR) {  // the bias gradient's partial over these 16 rows
         float s = 0.f;
 #pragma unroll
@@ -848,14 +855,14 @@ __global__ __launch_bounds__(TTHR) void k_amp_bwd(AmpDev d, int B, float p, uint
     __shared__ __attribute__((aligned(16))) float Ts[TR * LD];
     __shared__ __attribute__((aligned(16))) _Float16 Pa[TR * (SA > SV ? SA : SV)];
     __shared__ __attribute__((aligned(16))) float CP[TW * 3 * H];
-    const int tile = blockIdx.x, row0 = tile * TR;
+    const int tile = blockIdx.x, row0 = tile * TRV;
     const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     // every wave owns columns when NACT == TW (hidden >= 128): a compile-time true, so no branch
     // around the weight ring (at a branch join the wait counters merge to the stricter count, and
     // a vmcnt(0) there would drain the ring's in-flight refills)
     const bool gw = NACT == TW || wave < NACT;
     const int nt0 = wave * NT, c0 = lane * VPL;
-    const bool zero_half = row0 + TR >= B && (tile & 1) == 0;
+    const bool zero_rest = row0 + TRV >= B;
     const float sc = p > 0.f ? 1.0f / (1.0f - p) : 1.0f;
     const int NB = d.NB;
     const long HH8 = (long)H * H / 8;
@@ -871,10 +878,10 @@ __global__ __launch_bounds__(TTHR) void k_amp_bwd(AmpDev d, int B, float p, uint
 #pragma unroll
             for (int t = 0; t < NT; t++) wv[s][t] = d.wv1t[((long)(nt0 + t) * 4 + s) * 64 + lane];
     }
-    for (int i = tid; i < TR * VH / 8; i += TTHR) {  // (clamped loads, zeroed by a select: no branch)
-        const int r = i / (VH / 8), c8 = i % (VH / 8), row = row0 + r;
+    for (int i = tid; i < TR * VH / 8; i += TTHR) {  // (clamped loads, zeroed by a select: no branch;
+        const int r = i / (VH / 8), c8 = i % (VH / 8), row = row0 + r;  // rows past TRV: zeros)
         const float4 v = reinterpret_cast<const float4*>(d.dz1_rm + (long)min(row, B - 1) * VH)[c8];
-        *reinterpret_cast<float4*>(Pa + r * SV + 8 * c8) = row < B ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+        *reinterpret_cast<float4*>(Pa + r * SV + 8 * c8) = row < B && r < TRV ? v : make_float4(0.f, 0.f, 0.f, 0.f);
     }
     lds_barrier();
     floatx4 acc[NT];
@@ -1003,7 +1010,7 @@ __global__ __launch_bounds__(TTHR) void k_amp_bwd(AmpDev d, int B, float p, uint
             }
             lds_barrier();
             flush_gbb<H>(d, CP, tile, CV_BLK + 6 * b + (half == 0 ? 0 : 3));
-            write_tl(Pa, SA, 0, H, (half == 0 ? d.du1T : d.du2T) + b * TLH, d.RS, 0, tile, zero_half);
+            write_tl<TRV>(Pa, SA, 0, H, (half == 0 ? d.du1T : d.du2T) + b * TLH, d.RS, 0, tile, zero_rest);
             // the next row pass's operands, then dX = fp16(dU16 W16) (W2 of half 1, W1 of half 0)
             // (one call on selected operands: loads in one code path keep the wait counters exact)
             {
@@ -1062,7 +1069,7 @@ __global__ __launch_bounds__(TTHR) void k_amp_bwd(AmpDev d, int B, float p, uint
     }
     lds_barrier();
     flush_gbb<H>(d, CP, tile, CV_BIN);
-    write_tl(Pa, SA, 0, H, d.dz0T, d.RS, 0, tile, zero_half);
+    write_tl<TRV>(Pa, SA, 0, H, d.dz0T, d.RS, 0, tile, zero_rest);
 }
 
 // ------------------------------------------------------------------ weight gradients
@@ -1109,16 +1116,16 @@ __global__ __launch_bounds__(256) void k_amp_dw(const DwJob* __restrict__ jobs, 
 struct VsJob {
     const float* src;
     float* dst;
-    int ld, N, per_example, round16;
+    int ld, N, per_example, round16;  // per_example: rows are 0 trunk tiles, 1 examples, 2 head tiles
 };
 __global__ __launch_bounds__(256) void k_amp_vecsum(const VsJob* __restrict__ jobs, const int2* __restrict__ items,
-                                                    int nitems, int ntiles, int B) {
+                                                    int nitems, int ntiles, int nhtiles, int B) {
     __shared__ float part[16][17];
     if ((int)blockIdx.x >= nitems) return;
     const int2 it = items[blockIdx.x];
     const VsJob jb = jobs[it.x];
     const int c = it.y + (threadIdx.x & 15), g = threadIdx.x >> 4;
-    const int rows = jb.per_example ? B : ntiles;
+    const int rows = jb.per_example == 1 ? B : jb.per_example == 2 ? nhtiles : ntiles;
     float a0 = 0.f, a1 = 0.f;
     if (c < jb.N) {
         int r = g;
@@ -1428,7 +1435,7 @@ int amp_create(AmpTrain** out, int H, int NB, int Bmax, float* P, float* G, cons
     a->NB = NB;
     a->Bmax = Bmax;
     a->RS = (Bmax + 31) / 32;
-    a->TMAX = (Bmax + TR - 1) / TR;
+    a->TMAX = (Bmax + TRV - 1) / TRV;  // (>= the heads' 16-row tiles: dbpi_part shares the size)
     AmpDev& d = a->d;
     d.H = H;
     d.NB = NB;
@@ -1549,7 +1556,7 @@ int amp_create(AmpTrain** out, int H, int NB, int Bmax, float* P, float* G, cons
     vj.push_back({colv(CV_BEPI), G + off[t_head(NB, HP_B)], ldc, H, 0, 0});
     vj.push_back({colv(CV_GV), G + off[t_head(NB, HV_G)], ldc, H, 0, 0});
     vj.push_back({colv(CV_BEV), G + off[t_head(NB, HV_B)], ldc, H, 0, 0});
-    vj.push_back({d.dbpi_part, G + off[t_head(NB, HP_BIAS)], LDL, ASIZE, 0, 1});
+    vj.push_back({d.dbpi_part, G + off[t_head(NB, HP_BIAS)], LDL, ASIZE, 2, 1});
     vj.push_back({d.dz1f, G + off[t_head(NB, HV_B1)], VH, VH, 1, 1});
     vj.push_back({d.v2prod, G + off[t_head(NB, HV_W2)], VH, VH, 1, 1});
     vj.push_back({d.dzv2, G + off[t_head(NB, HV_B2)], 1, 1, 1, 1});
@@ -1632,7 +1639,8 @@ int amp_backward(AmpTrain* a, const yk_state_t* states, const int32_t* targets, 
         a->lrow = lrow;
         a->lsum = lsum;
     }
-    const int T = (B + TR - 1) / TR, rsn = (B + 31) / 32;
+    // T: the heads' 16-row tiles; TT: the trunk's TRV-row workgroups
+    const int T = (B + TR - 1) / TR, TT = (B + TRV - 1) / TRV, rsn = (B + 31) / 32;
     if (dropout > 0.f && !(a->mask_valid && a->mask_seed == seed && a->mask_step == step && a->mask_row_base == row_base &&
                            a->mask_p == dropout && a->mask_rows >= B)) {  // (not made ahead by the last update)
         const long nm = (long)(1 + a->NB) * B * (a->H / 4);
@@ -1644,7 +1652,7 @@ int amp_backward(AmpTrain* a, const yk_state_t* states, const int32_t* targets, 
     switch (a->H) {
 #define YK_AMP_FWD(HH)                                                                                              \
     case HH:                                                                                                        \
-        hipLaunchKernelGGL(k_amp_fwd<HH>, dim3(T), dim3(TTHR), 0, s, d, states, idx, B, dropout, seed, step, row_base); \
+        hipLaunchKernelGGL(k_amp_fwd<HH>, dim3(TT), dim3(TTHR), 0, s, d, states, idx, B, dropout, seed, step, row_base); \
         YK_LAUNCHED();                                                                                              \
         hipLaunchKernelGGL(k_amp_head<HH>, dim3(T, HQ + 1), dim3(TTHR), 0, s, d, B);                               \
         YK_LAUNCHED();                                                                                              \
@@ -1653,7 +1661,7 @@ int amp_backward(AmpTrain* a, const yk_state_t* states, const int32_t* targets, 
         YK_LAUNCHED();                                                                                              \
         hipLaunchKernelGGL(k_amp_headbwd<HH>, dim3(T, BQ), dim3(TTHR), 0, s, d, targets, idx, B);                  \
         YK_LAUNCHED();                                                                                              \
-        hipLaunchKernelGGL(k_amp_bwd<HH>, dim3(T), dim3(TTHR), 0, s, d, B, dropout, seed, step, row_base);         \
+        hipLaunchKernelGGL(k_amp_bwd<HH>, dim3(TT), dim3(TTHR), 0, s, d, B, dropout, seed, step, row_base);        \
         YK_LAUNCHED();                                                                                              \
         break;
         YK_AMP_FWD(64)
@@ -1667,7 +1675,7 @@ int amp_backward(AmpTrain* a, const yk_state_t* states, const int32_t* targets, 
                        a->n_dw_items, a->RS, rsn);
     YK_LAUNCHED();
     hipLaunchKernelGGL(k_amp_vecsum, dim3((unsigned)a->n_vs_items), dim3(256), 0, s, a->vs_jobs, a->vs_items,
-                       a->n_vs_items, T, B);
+                       a->n_vs_items, TT, T, B);
     YK_LAUNCHED();
     return YK_OK;
 }

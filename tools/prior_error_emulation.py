@@ -120,6 +120,7 @@ def forward(sd, X, cfg, H=256, NB=6):
 
     def G(A, W, where):
         return gemm(A, W, cfg if only is None else dict(cfg, lolo=cfg["lolo"] if where in only else False))
+    blocks = cfg.get("lolo_blocks")  # with "trunk" in lolo_only: the blocks (0 .. NB-1) that get it
     w, b = L("inp.0")
     g, be = L("inp.1")
     h = silu(layernorm(G(X, w, "inp") + b, g, be, cfg, H), cfg)
@@ -128,8 +129,9 @@ def forward(sd, X, cfg, H=256, NB=6):
         g1, e1 = L(f"blocks.{k}.ln1")
         w2, b2 = L(f"blocks.{k}.fc2")
         g2, e2 = L(f"blocks.{k}.ln2")
-        t = layernorm(silu(G(h, w1, "trunk") + b1, cfg), g1, e1, cfg, H)
-        t = layernorm(silu(G(t, w2, "trunk") + b2, cfg), g2, e2, cfg, H)
+        tw = "trunk" if blocks is None or k in blocks else "-"
+        t = layernorm(silu(G(h, w1, tw) + b1, cfg), g1, e1, cfg, H)
+        t = layernorm(silu(G(t, w2, tw) + b2, cfg), g2, e2, cfg, H)
         h = (h + t).astype(F32)
     gp, bp = L("pi_head.0")
     wp, bpi = L("pi_head.2")
@@ -184,6 +186,7 @@ def main():
         return float(r.max()), float(np.sqrt((r * r).mean()))
 
     base = dict(exact_a=False, exact_w=False, lolo=False, ieee_silu=False, twopass_ln=False)
+    only = os.environ.get("YK_EMU_ONLY")  # a substring: run the matching variants only
     variants = [
         ("kernel (r03: hi/lo planes, no lo*lo, hw SiLU, one-pass LN + rsq)", {}),
         ("+ lo*lo product (own accumulator)", dict(lolo=True)),
@@ -199,12 +202,22 @@ def main():
         ("lo*lo (scaled) in the policy head only", dict(lolo="scaled", lolo_only=("head",))),
         ("lo*lo (scaled) in the input layer + policy head", dict(lolo="scaled", lolo_only=("inp", "head"))),
         ("lo*lo (scaled) in the trunk only", dict(lolo="scaled", lolo_only=("inp", "trunk"))),
+        ("lo*lo (scaled) in the input layer only", dict(lolo="scaled", lolo_only=("inp",))),
+        ("lo*lo (scaled) in the input layer + blocks 0-2", dict(lolo="scaled", lolo_only=("inp", "trunk"), lolo_blocks=(0, 1, 2))),
+        ("lo*lo (scaled) in the input layer + blocks 3-5", dict(lolo="scaled", lolo_only=("inp", "trunk"), lolo_blocks=(3, 4, 5))),
+        ("lo*lo (scaled) in blocks 0-5, not the input layer", dict(lolo="scaled", lolo_only=("trunk",))),
+        ("lo*lo (scaled) in block 0 only", dict(lolo="scaled", lolo_only=("trunk",), lolo_blocks=(0,))),
+        ("lo*lo (scaled) in blocks 0-1 only", dict(lolo="scaled", lolo_only=("trunk",), lolo_blocks=(0, 1))),
+        ("lo*lo (scaled) in block 1 only", dict(lolo="scaled", lolo_only=("trunk",), lolo_blocks=(1,))),
+        ("lo*lo (scaled) in block 2 only", dict(lolo="scaled", lolo_only=("trunk",), lolo_blocks=(2,))),
     ]
     e_r = err(Pr)
     print(f"{len(S)} fixture states with a valid action, weights {args.weights}, ulp noise {args.ulp_noise}; "
           f"{int(big.sum())} priors > 1e-3")
     print(f"{'torch float32 (CPU, the reference arithmetic)':62s} max {e_r[0]:.3e}  rms {e_r[1]:.3e}")
     for name, over in variants:
+        if only and only not in name:
+            continue
         cfg = dict(base, **over)
         lg = forward(sd, X, cfg)
         P = O.mcts_prior(leaf_prior(lg, ok), S).astype(F64)
