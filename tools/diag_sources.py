@@ -197,9 +197,9 @@ AMP = [
      r"                store_acc<NT>\(Ts, LD, nt0, acc\);\n            \}\n", "around",
      ("            AMP_STAMP(0, 0);\n", "            AMP_STAMP(0, 1);\n")),
     (r"^            lds_barrier\(\);\n            float\* U = ", "after_line1", "            AMP_STAMP(0, 2);\n"),
-    (r"^            lds_barrier\(\);\n            if \(half == 0\) write_tl\(Pa, SA", "around_line1",
+    (r"^            lds_barrier\(\);\n            if \(half == 0\) write_tl<TRV>\(Pa, SA", "around_line1",
      ("            AMP_STAMP(0, 3);\n", "            AMP_STAMP(0, 4);\n")),
-    (r"^                write_tl\(Pa, SA, 0, H, d.hT \+ \(long\)\(b \+ 1\).*\n", "after", "            AMP_STAMP(0, 5);\n"),
+    (r"^                write_tl<TRV>\(Pa, SA, 0, H, d.hT \+ \(long\)\(b \+ 1\).*\n", "after", "            AMP_STAMP(0, 5);\n"),
     # k_amp_bwd, block 2, per half: 0 row pass start, 1 its end, 2 the barrier passed, 3 column
     # partials flushed, 4 T-layout store done, 5 next row's operands issued, 6 GEMM + store done,
     # 7 the barrier passed
@@ -207,7 +207,7 @@ AMP = [
     (r"^            lds_barrier\(\);\n            flush_gbb<H>", "around_line1",
      ("            AMP_STAMP(1, 1);\n", "            AMP_STAMP(1, 2);\n")),
     (r"^            flush_gbb<H>\(d, CP, tile, CV_BLK.*\n", "after", "            AMP_STAMP(1, 3);\n"),
-    (r"^            write_tl\(Pa, SA, 0, H, \(half == 0 \? d.du1T.*\n", "after", "            AMP_STAMP(1, 4);\n"),
+    (r"^            write_tl<TRV>\(Pa, SA, 0, H, \(half == 0 \? d.du1T.*\n", "after", "            AMP_STAMP(1, 4);\n"),
     (r"^            __builtin_amdgcn_sched_barrier\(0\);\n            const float4\* cur = \(half == 1", "after_line1",
      "            AMP_STAMP(1, 5);\n"),
     (r"^            const float4\* nxt = half == 1 \? d.w1t.*\n            if \(gw\) \{\n"
