@@ -41,6 +41,7 @@ using namespace yk;
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef _Float16 half4 __attribute__((ext_vector_type(4)));
 
 namespace {
 
@@ -168,6 +169,19 @@ __device__ __forceinline__ void write_tl(const _Float16* A, int sa, int col0, in
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
     const int h = tile % TPS, rs = tile / TPS, q = lane >> 4;
     const bool mine = q / QPT == h, after = q / QPT > h;
+    if constexpr (R == 8) {  // one 8-row piece per column: every thread takes half of one (4 rows, 8 bytes)
+        for (int i = threadIdx.x; i < C * 2; i += blockDim.x) {
+            const int cc = i >> 1, hf = i & 1, ct = cc >> 4, cl = cc & 15;
+            half4 v;
+#pragma unroll
+            for (int j = 0; j < 4; j++) v[j] = A[(4 * hf + j) * sa + col0 + cc];
+            *reinterpret_cast<half4*>(dst + (((long)(ct0 + ct) * RS + rs) * 64 + cl + 16 * h) * 8 + 4 * hf) = v;
+        }
+        if (!zero_rest) return;  // the batch's last tile: the slice's later pieces are zeros
+        for (int ct = wave; ct < C / 16; ct += nw)
+            if (after) *reinterpret_cast<half8*>(dst + (((long)(ct0 + ct) * RS + rs) * 64 + lane) * 8) = half8{};
+        return;
+    }
     for (int ct = wave; ct < C / 16; ct += nw) {
         half8 v = {};
         if (mine) {
