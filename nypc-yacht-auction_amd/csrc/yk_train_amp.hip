@@ -6,25 +6,25 @@
 // arithmetic - the fp16 rounding points included - on hand-written v_mfma_f32_16x16x32_f16
 // kernels instead of library GEMMs (yk_train.hip keeps the f32 rocBLAS step for the f32 mode).
 //
-// A step is nine launches (yk_train_amp.h):
-//   k_amp_fwd      one 512-thread workgroup per 16-row tile: features -> input layer -> the
-//                  residual blocks -> the heads' LayerNorms, every dense layer from a register
-//                  ring of fp16 weight fragments that streams the next layer during the row pass;
-//                  saves what the backward needs (fp16 pre-activations, LayerNorm statistics, the
-//                  GEMM inputs in the T layout the weight-gradient GEMMs read)
-//   k_amp_head     row tile x column part: the policy logits (fp16-rounded) and their per-part
+// A step is eight launches (yk_train_amp.h):
+//   k_amp_fwd      one 512-thread workgroup per 8 rows (TRV; the MFMAs run 16): features -> input
+//                  layer -> the residual blocks -> the heads' LayerNorms, every dense layer from a
+//                  register ring of fp16 weight fragments that streams the next layer during the
+//                  row pass; saves what the backward needs (fp16 pre-activations, LayerNorm
+//                  statistics, the GEMM inputs in the T layout the weight-gradient GEMMs read)
+//   k_amp_head     16-row tile x column part: the policy logits (fp16-rounded) and their per-part
 //                  softmax statistics; one more part per tile computes v_head.2
-//   k_amp_loss     one wave per example: cross-entropy, the value head's tail, the MSE and their
-//                  scaled gradients
-//   k_amp_headbwd  row tile x action slice: the scaled fp16 logits gradient, its T layout, and a
-//                  split-K slice of pi_head.2's input gradient
-//   k_amp_bwd      one workgroup per row tile: the heads' LayerNorm backward and the trunk's
+//   k_amp_headbwd  16-row tile x action slice: the scaled fp16 logits gradient, its T layout, and a
+//                  split-K slice of pi_head.2's input gradient; one more part per tile the loss rows
+//                  (a wave per example: cross-entropy, the value head's tail, the MSE, gradients)
+//   k_amp_bwd      one workgroup per 8 rows: the heads' LayerNorm backward and the trunk's
 //                  backward chain (LayerNorm / SiLU / dropout backward, the dX GEMMs) to the input
 //   k_amp_dw       every weight gradient (13 + 2 GEMMs, K = the batch) in one grouped launch
 //   k_amp_vecsum   bias / LayerNorm gradients and the loss sums: fixed-order column sums
 //   k_amp_sq       unscale + the gradient norm
 //   k_amp_update   clip + AdamW (or skip), GradScaler update and the fp16 weight copies for the
-//                  next step, a 32 x 32 weight tile (or a vector slice) per workgroup
+//                  next step, a 32 x 32 weight tile (or a vector slice) per workgroup; extra blocks
+//                  make the next step's dropout keep bits (k_amp_masks when they could not)
 // Weight fragments use yk_net.h's packing (one plane): for W[N][K], the 1 KB piece (nt, ks) holds
 // W[16 nt + (l & 15)][32 ks + 8 (l >> 4) + j] for lane l, j < 8.  The T layout of an activation
 // matrix X[rows][C] is the same packing of X^T (piece (ct, rs): X[32 rs + 8 (l >> 4) + j][16 ct +
@@ -653,10 +653,21 @@ __global__ __launch_bounds__(TTHR) void k_amp_head(AmpDev d, int B) {
 // Linear(128, 1) -> tanh), MSE (f32), and the scaled gradients of both: d v_head.2 output (dz1,
 // fp16) and the rows whose column sums are v_head.4's gradients.  Rows past the batch (up to the
 // last 32-row slice) only zero their dz1 T-layout entries.
-__global__ __launch_bounds__(256) void k_amp_loss(AmpDev d, const int32_t* __restrict__ tgt_all,
-                                                  const float* __restrict__ v_all, const int32_t* __restrict__ idx,
-                                                  int B, float vw, float2* __restrict__ lrow) {
-    const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+// The row's log-sum-exp from the head parts' (max, sum exp), merged in part order
+__device__ __forceinline__ float row_lse(const AmpDev& d, int row) {
+    float m = -INFINITY, s = 0.f;
+    for (int qq = 0; qq < HQ; qq++) {
+        const float2 ms = d.mlq[(long)qq * d.Bmax + row];
+        stat_merge(m, s, ms.x, ms.y);
+    }
+    return m + logf(s);
+}
+// One example's losses (one wave): cross-entropy from the row's log-sum-exp; the fp16 value-head
+// tail (SiLU, Linear(128, 1), tanh), the MSE and their backward into dz1 / v_head.4's product
+// terms; rows past the batch (up to the 32-row slice) zero their dz1 T-layout entries.
+__device__ __forceinline__ void loss_row(const AmpDev& d, const int32_t* __restrict__ tgt_all,
+                                         const float* __restrict__ v_all, const int32_t* __restrict__ idx, int B,
+                                         float vw, float2* __restrict__ lrow, int row, int lane) {
     if (row >= d.RS * 32) return;
     if (row >= B) {
 #pragma unroll
@@ -671,13 +682,7 @@ __global__ __launch_bounds__(256) void k_amp_loss(AmpDev d, const int32_t* __res
     const int src = idx ? idx[row] : row;
     const int t = tgt_all[src];
     const float z = v_all[src];
-    float m = -INFINITY, s = 0.f;
-    for (int qq = 0; qq < HQ; qq++) {
-        const float2 ms = d.mlq[(long)qq * d.Bmax + row];
-        stat_merge(m, s, ms.x, ms.y);
-    }
-    const float lse = m + logf(s);
-    if (lane == 0) d.lse[row] = lse;
+    const float lse = row_lse(d, row);
     const float ce = lse - d.logits[(long)row * LDL + t];
     const float* wv2 = d.P + poff(d.H, d.NB, t_head(d.NB, HV_W2));
     const float bv2 = r16(d.P[poff(d.H, d.NB, t_head(d.NB, HV_B2))]);
@@ -715,10 +720,13 @@ __global__ __launch_bounds__(256) void k_amp_loss(AmpDev d, const int32_t* __res
 
 // dlogits = fp16(S (softmax - onehot(t)) / B) for the tile's rows over this part's action slices
 // (LDS); their T layout (pi_head.2 weight gradient), their column sums over the 16 rows (bias
-// gradient partial), and dA_pi's split-K partial = dlogits16 Wpi16 over these slices
+// gradient partial), and dA_pi's split-K partial = dlogits16 Wpi16 over these slices.  One more
+// part per tile runs its loss rows (loss_row, a wave per row; the last tile the slice's rows past
+// it too) beside them - one launch fewer than a separate loss kernel.
 template <int H>
 __global__ __launch_bounds__(TTHR) void k_amp_headbwd(AmpDev d, const int32_t* __restrict__ tgt_all,
-                                                      const int32_t* __restrict__ idx, int B) {
+                                                      const float* __restrict__ v_all, const int32_t* __restrict__ idx,
+                                                      int B, float vw, float2* __restrict__ lrow) {
     constexpr int NT = H >= 128 ? H / 128 : 1, NACT = H / (16 * NT);
     constexpr int SPMAX = (PKS + BQ - 1) / BQ;
     constexpr int SD = SPMAX * 32 + 8;
@@ -728,6 +736,12 @@ __global__ __launch_bounds__(TTHR) void k_amp_headbwd(AmpDev d, const int32_t* _
     __shared__ int TG[TR];
     const int tile = blockIdx.x, part = blockIdx.y, row0 = tile * TR;
     const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    if (part == BQ) {  // the loss part: the tile's rows (and, in the last tile, the slice's rows past it)
+#pragma unroll
+        for (int k = 0; k < 2 * TR / TW; k++)
+            if (k < TR / TW || tile == (int)gridDim.x - 1) loss_row(d, tgt_all, v_all, idx, B, vw, lrow, row0 + TW * k + wave, lane);
+        return;
+    }
     const int ks0 = part * PKS / BQ, ks1 = (part + 1) * PKS / BQ, ns = ks1 - ks0;
     // every wave owns columns when NACT == TW (hidden >= 128): a compile-time true, so no branch
     // around the weight ring (at a branch join the wait counters merge to the stricter count, and
@@ -736,7 +750,7 @@ __global__ __launch_bounds__(TTHR) void k_amp_headbwd(AmpDev d, const int32_t* _
     const int nt0 = wave * NT;
     if (tid < TR) {
         const int row = row0 + tid;
-        LSE[tid] = row < B ? d.lse[row] : 0.f;
+        LSE[tid] = row < B ? row_lse(d, row) : 0.f;
         TG[tid] = row < B ? tgt_all[idx ? idx[row] : row] : -1;
     }
     // this part's logits first (every thread's, unconditionally, clamped), then the first slices
@@ -1670,10 +1684,8 @@ int amp_backward(AmpTrain* a, const yk_state_t* states, const int32_t* targets, 
         YK_LAUNCHED();                                                                                              \
         hipLaunchKernelGGL(k_amp_head<HH>, dim3(T, HQ + 1), dim3(TTHR), 0, s, d, B);                               \
         YK_LAUNCHED();                                                                                              \
-        hipLaunchKernelGGL(k_amp_loss, dim3((rsn * 32 + 3) / 4), dim3(256), 0, s, d, targets, values, idx, B,      \
+        hipLaunchKernelGGL(k_amp_headbwd<HH>, dim3(T, BQ + 1), dim3(TTHR), 0, s, d, targets, values, idx, B,       \
                            vloss_weight, lrow);                                                                     \
-        YK_LAUNCHED();                                                                                              \
-        hipLaunchKernelGGL(k_amp_headbwd<HH>, dim3(T, BQ), dim3(TTHR), 0, s, d, targets, idx, B);                  \
         YK_LAUNCHED();                                                                                              \
         hipLaunchKernelGGL(k_amp_bwd<HH>, dim3(TT), dim3(TTHR), 0, s, d, B, dropout, seed, step, row_base);        \
         YK_LAUNCHED();                                                                                              \
