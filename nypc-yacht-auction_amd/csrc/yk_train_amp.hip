@@ -823,6 +823,48 @@ __global__ __launch_bounds__(TTHR) void k_amp_headbwd(AmpDev d, const int32_t* _
         }
 }
 
+struct DwJob {
+    const float4* A;  // T layout of dU [B][N]
+    const float4* X;  // T layout of X [B][K]
+    float* dst;       // gradient [N][K] in the flat buffer
+    int N, K;
+};
+// one weight-gradient item for one wave: (job, 16-row tile of W, up to 4 column tiles), summed over
+// the batch's 32-row slices
+__device__ __forceinline__ void dw_item(const DwJob* __restrict__ jobs, const int4 it, int RS, int rsn, int lane) {
+    const DwJob jb = jobs[it.x];
+    const int nt = it.y, kt0 = it.z, nk = it.w;
+    floatx4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
+    for (int rs = 0; rs < rsn; rs++) {
+        const float4 a = jb.A[((long)nt * RS + rs) * 64 + lane];
+        float4 x[4];
+#pragma unroll
+        for (int t = 0; t < 4; t++)
+            x[t] = t < nk ? jb.X[((long)(kt0 + t) * RS + rs) * 64 + lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int t = 0; t < 4; t++)
+            if (t < nk) acc[t] = mfma(a, x[t], acc[t]);
+    }
+    const int q = lane >> 4, c = lane & 15;
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+        if (t >= nk) break;
+        const int k = 16 * (kt0 + t) + c;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int n = 16 * nt + 4 * q + j;
+            if (n < jb.N && k < jb.K) jb.dst[(long)n * jb.K + k] = r16(acc[t][j]);  // fp16 grad_weight
+        }
+    }
+}
+// the trunk's weight gradients, after k_amp_bwd (the heads' run inside k_amp_bwd's launch)
+__global__ __launch_bounds__(256) void k_amp_dw(const DwJob* __restrict__ jobs, const int4* __restrict__ items,
+                                                int nitems, int RS, int rsn) {
+    const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (w >= nitems) return;
+    dw_item(jobs, items[w], RS, rsn, threadIdx.x & 63);
+}
+
 // ------------------------------------------------------------------ backward (trunk)
 // What one row pass of k_amp_bwd reads from memory, loaded into registers BEFORE the GEMM that
 // precedes it: the GEMM's weight-ring refills are issued after these loads, and vmcnt retires in
@@ -873,7 +915,8 @@ __device__ __forceinline__ void flush_gbb(const AmpDev& d, const float* CP, int 
 
 template <int H>
 __global__ __launch_bounds__(TTHR) void k_amp_bwd(AmpDev d, int B, float p, uint64_t seed, uint64_t step,
-                                                  int64_t row_base) {
+                                                  int64_t row_base, const DwJob* __restrict__ jobs,
+                                                  const int4* __restrict__ hitems, int nhitems, int rsn) {
     constexpr int LD = H + 4, SA = H + 8, VPL = H / 64, KS = H / 32;
     constexpr int NT = H >= 128 ? H / 128 : 1, NACT = H / (16 * NT);
     constexpr int RW = KS * NT <= 16 ? KS : 16 / NT;
@@ -885,6 +928,12 @@ __global__ __launch_bounds__(TTHR) void k_amp_bwd(AmpDev d, int B, float p, uint
     __shared__ __attribute__((aligned(16))) float CP[TW * 3 * H];
     const int tile = blockIdx.x, row0 = tile * TRV;
     const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    if (row0 >= B) {  // the blocks past the row tiles: the heads' weight gradients (their operands are
+                      // done before this launch), on the CUs the trunk's 8-row workgroups leave idle
+        const int w = (tile - (B + TRV - 1) / TRV) * TW + wave;
+        if (w < nhitems) dw_item(jobs, hitems[w], d.RS, rsn, lane);
+        return;
+    }
     // every wave owns columns when NACT == TW (hidden >= 128): a compile-time true, so no branch
     // around the weight ring (at a branch join the wait counters merge to the stricter count, and
     // a vmcnt(0) there would drain the ring's in-flight refills)
@@ -1101,43 +1150,6 @@ __global__ __launch_bounds__(TTHR) void k_amp_bwd(AmpDev d, int B, float p, uint
 }
 
 // ------------------------------------------------------------------ weight gradients
-struct DwJob {
-    const float4* A;  // T layout of dU [B][N]
-    const float4* X;  // T layout of X [B][K]
-    float* dst;       // gradient [N][K] in the flat buffer
-    int N, K;
-};
-// one wave per (job, 16-row tile of W, up to 4 column tiles): sum over the batch's 32-row slices
-__global__ __launch_bounds__(256) void k_amp_dw(const DwJob* __restrict__ jobs, const int4* __restrict__ items,
-                                                int nitems, int RS, int rsn) {
-    const int w = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (w >= nitems) return;
-    const int4 it = items[w];
-    const DwJob jb = jobs[it.x];
-    const int nt = it.y, kt0 = it.z, nk = it.w;
-    floatx4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
-    for (int rs = 0; rs < rsn; rs++) {
-        const float4 a = jb.A[((long)nt * RS + rs) * 64 + lane];
-        float4 x[4];
-#pragma unroll
-        for (int t = 0; t < 4; t++)
-            x[t] = t < nk ? jb.X[((long)(kt0 + t) * RS + rs) * 64 + lane] : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-        for (int t = 0; t < 4; t++)
-            if (t < nk) acc[t] = mfma(a, x[t], acc[t]);
-    }
-    const int q = lane >> 4, c = lane & 15;
-#pragma unroll
-    for (int t = 0; t < 4; t++) {
-        if (t >= nk) break;
-        const int k = 16 * (kt0 + t) + c;
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const int n = 16 * nt + 4 * q + j;
-            if (n < jb.N && k < jb.K) jb.dst[(long)n * jb.K + k] = r16(acc[t][j]);  // fp16 grad_weight
-        }
-    }
-}
 
 // fixed-order column sums: dst[c] = sum_r src[r * ld + c] over `rows` rows (tiles or examples).
 // Block = one job's 16 columns x 16 row groups (row r to group r % 16), the groups added in order.
@@ -1410,6 +1422,7 @@ struct AmpTrain {
     DwJob* dw_jobs = nullptr;
     int4* dw_items = nullptr;
     int n_dw_items = 0;
+    int n_dw_trunk = 0;  // items [0, n_dw_trunk): k_amp_dw; the rest (the heads'): inside k_amp_bwd
     std::vector<int4> dw_items_host;
     std::vector<int> dw_job_rows;  // for each item: unused (all jobs span the batch)
     VsJob* vs_jobs = nullptr;
@@ -1564,6 +1577,8 @@ int amp_create(AmpTrain** out, int H, int NB, int Bmax, float* P, float* G, cons
             for (int nt = 0; nt < ntn; nt++) items.push_back(make_int4((int)j, nt, k0, std::min(4, ntk - k0)));
     }
     a->n_dw_items = (int)items.size();
+    a->n_dw_trunk = 0;  // the items of the input layer's and the blocks' matrices come first
+    while (a->n_dw_trunk < a->n_dw_items && items[a->n_dw_trunk].x < 1 + 2 * NB) a->n_dw_trunk++;
     // column-sum jobs: bias / LayerNorm gradients and the two loss sums
     std::vector<VsJob> vj;
     const int ldc = d.NVEC * H;
@@ -1687,7 +1702,9 @@ int amp_backward(AmpTrain* a, const yk_state_t* states, const int32_t* targets, 
         hipLaunchKernelGGL(k_amp_headbwd<HH>, dim3(T, BQ + 1), dim3(TTHR), 0, s, d, targets, values, idx, B,       \
                            vloss_weight, lrow);                                                                     \
         YK_LAUNCHED();                                                                                              \
-        hipLaunchKernelGGL(k_amp_bwd<HH>, dim3(TT), dim3(TTHR), 0, s, d, B, dropout, seed, step, row_base);        \
+        hipLaunchKernelGGL(k_amp_bwd<HH>, dim3(TT + (a->n_dw_items - a->n_dw_trunk + TW - 1) / TW), dim3(TTHR), 0, s, \
+                           d, B, dropout, seed, step, row_base, a->dw_jobs, a->dw_items + a->n_dw_trunk,          \
+                           a->n_dw_items - a->n_dw_trunk, rsn);                                                    \
         YK_LAUNCHED();                                                                                              \
         break;
         YK_AMP_FWD(64)
@@ -1697,8 +1714,8 @@ int amp_backward(AmpTrain* a, const yk_state_t* states, const int32_t* targets, 
 #undef YK_AMP_FWD
         default: return YK_ERR_ARG;
     }
-    hipLaunchKernelGGL(k_amp_dw, dim3((unsigned)((a->n_dw_items + 3) / 4)), dim3(256), 0, s, a->dw_jobs, a->dw_items,
-                       a->n_dw_items, a->RS, rsn);
+    hipLaunchKernelGGL(k_amp_dw, dim3((unsigned)((a->n_dw_trunk + 3) / 4)), dim3(256), 0, s, a->dw_jobs, a->dw_items,
+                       a->n_dw_trunk, a->RS, rsn);
     YK_LAUNCHED();
     hipLaunchKernelGGL(k_amp_vecsum, dim3((unsigned)a->n_vs_items), dim3(256), 0, s, a->vs_jobs, a->vs_items,
                        a->n_vs_items, TT, T, B);
