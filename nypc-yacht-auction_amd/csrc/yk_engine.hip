@@ -1108,7 +1108,8 @@ __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int l
 // descending, ascending index on ties (a bitonic sort of 64-bit keys P bits << 32 | 0xFFFF - j in
 // LDS; P >= 0, so its bits order as unsigned), and the list of the edges already visited.  One
 // workgroup per game.  Leaves the root in full-scan mode when c <= 0 (the order is then not the
-// UCB order), when the root has no valid action, or when its visited list would overflow.
+// UCB order), when the root has at most 256 valid actions (every bid node), or when its visited
+// list would overflow.
 __global__ __launch_bounds__(256) void k_root_sort(EngDev d) {
     constexpr int PT = (RO_CAP + 255) / 256;  // keys per thread
     __shared__ uint64_t sk[RO_K];
@@ -1140,7 +1141,8 @@ __global__ __launch_bounds__(256) void k_root_sort(EngDev d) {
     const NodeRec& nd = d.nodes[g][(long)t * d.NCAP + nid];
     const int V = (int)nd.nvalid;
     const uint32_t p_off = nd.p_off;
-    if (V == 0 || V > RO_CAP) return;
+    // (a root of <= 256 entries is one pass of the full scan, 4 entries per lane: no order pays)
+    if (V <= 256 || V > RO_CAP) return;
     const float* P = d.arenaP + (long)t * d.AE + p_off;
     const uint16_t* S = d.arenaS + (long)t * d.AE + p_off;
     uint32_t* rv = d.rv + (long)t * RV_CAP;
