@@ -6,7 +6,7 @@
 // arithmetic - the fp16 rounding points included - on hand-written v_mfma_f32_16x16x32_f16
 // kernels instead of library GEMMs (yk_train.hip keeps the f32 rocBLAS step for the f32 mode).
 //
-// A step is eight launches (yk_train_amp.h):
+// A step is seven launches (yk_train_amp.h):
 //   k_amp_fwd      one 512-thread workgroup per 8 rows (TRV; the MFMAs run 16): features -> input
 //                  layer -> the residual blocks -> the heads' LayerNorms, every dense layer from a
 //                  register ring of fp16 weight fragments that streams the next layer during the
@@ -19,8 +19,9 @@
 //                  (a wave per example: cross-entropy, the value head's tail, the MSE, gradients)
 //   k_amp_bwd      one workgroup per 8 rows: the heads' LayerNorm backward and the trunk's
 //                  backward chain (LayerNorm / SiLU / dropout backward, the dX GEMMs) to the input
-//   k_amp_dw       every weight gradient (13 + 2 GEMMs, K = the batch) in one grouped launch
-//   k_amp_vecsum   bias / LayerNorm gradients and the loss sums: fixed-order column sums
+//   k_amp_grads    the trunk's weight gradients (13 GEMMs, K = the batch; the heads' 2 run in
+//                  k_amp_bwd's launch) and, in more blocks, the bias / LayerNorm gradients and the
+//                  loss sums: fixed-order column sums
 //   k_amp_sq       unscale + the gradient norm
 //   k_amp_update   clip + AdamW (or skip), GradScaler update and the fp16 weight copies for the
 //                  next step, a 32 x 32 weight tile (or a vector slice) per workgroup; extra blocks
@@ -857,13 +858,6 @@ __device__ __forceinline__ void dw_item(const DwJob* __restrict__ jobs, const in
         }
     }
 }
-// the trunk's weight gradients, after k_amp_bwd (the heads' run inside k_amp_bwd's launch)
-__global__ __launch_bounds__(256) void k_amp_dw(const DwJob* __restrict__ jobs, const int4* __restrict__ items,
-                                                int nitems, int RS, int rsn) {
-    const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (w >= nitems) return;
-    dw_item(jobs, items[w], RS, rsn, threadIdx.x & 63);
-}
 
 // ------------------------------------------------------------------ backward (trunk)
 // What one row pass of k_amp_bwd reads from memory, loaded into registers BEFORE the GEMM that
@@ -1158,11 +1152,9 @@ struct VsJob {
     float* dst;
     int ld, N, per_example, round16;  // per_example: rows are 0 trunk tiles, 1 examples, 2 head tiles
 };
-__global__ __launch_bounds__(256) void k_amp_vecsum(const VsJob* __restrict__ jobs, const int2* __restrict__ items,
-                                                    int nitems, int ntiles, int nhtiles, int B) {
-    __shared__ float part[16][17];
-    if ((int)blockIdx.x >= nitems) return;
-    const int2 it = items[blockIdx.x];
+// one column-sum item for a 256-thread block: 16 columns of a job, 16 row groups, fixed order
+__device__ __forceinline__ void vecsum_item(const VsJob* __restrict__ jobs, const int2 it, int ntiles, int nhtiles,
+                                            int B, float (&part)[16][17]) {
     const VsJob jb = jobs[it.x];
     const int c = it.y + (threadIdx.x & 15), g = threadIdx.x >> 4;
     const int rows = jb.per_example == 1 ? B : jb.per_example == 2 ? nhtiles : ntiles;
@@ -1183,6 +1175,24 @@ __global__ __launch_bounds__(256) void k_amp_vecsum(const VsJob* __restrict__ jo
         for (int k = 0; k < 16; k++) s += part[k][threadIdx.x];
         jb.dst[c] = jb.round16 ? r16(s) : s;
     }
+}
+// after k_amp_bwd: the trunk's weight gradients (dw_item, a wave each; the heads' ran inside
+// k_amp_bwd's launch) and, in the blocks past them, the bias / LayerNorm gradients and loss sums
+// (vecsum_item, a block each) - one launch for both
+__global__ __launch_bounds__(256) void k_amp_grads(const DwJob* __restrict__ jobs, const int4* __restrict__ items,
+                                                   int nitems, int RS, int rsn, const VsJob* __restrict__ vjobs,
+                                                   const int2* __restrict__ vitems, int nvitems, int ntiles,
+                                                   int nhtiles, int B) {
+    __shared__ float part[16][17];
+    const int ndb = (nitems + 3) / 4;
+    if ((int)blockIdx.x >= ndb) {
+        const int v = (int)blockIdx.x - ndb;
+        if (v < nvitems) vecsum_item(vjobs, vitems[v], ntiles, nhtiles, B, part);
+        return;
+    }
+    const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (w >= nitems) return;
+    dw_item(jobs, items[w], RS, rsn, threadIdx.x & 63);
 }
 
 // ------------------------------------------------------------------ optimiser
@@ -1422,7 +1432,7 @@ struct AmpTrain {
     DwJob* dw_jobs = nullptr;
     int4* dw_items = nullptr;
     int n_dw_items = 0;
-    int n_dw_trunk = 0;  // items [0, n_dw_trunk): k_amp_dw; the rest (the heads'): inside k_amp_bwd
+    int n_dw_trunk = 0;  // items [0, n_dw_trunk): k_amp_grads; the rest (the heads'): inside k_amp_bwd
     std::vector<int4> dw_items_host;
     std::vector<int> dw_job_rows;  // for each item: unused (all jobs span the batch)
     VsJob* vs_jobs = nullptr;
@@ -1714,11 +1724,9 @@ int amp_backward(AmpTrain* a, const yk_state_t* states, const int32_t* targets, 
 #undef YK_AMP_FWD
         default: return YK_ERR_ARG;
     }
-    hipLaunchKernelGGL(k_amp_dw, dim3((unsigned)((a->n_dw_trunk + 3) / 4)), dim3(256), 0, s, a->dw_jobs, a->dw_items,
-                       a->n_dw_trunk, a->RS, rsn);
-    YK_LAUNCHED();
-    hipLaunchKernelGGL(k_amp_vecsum, dim3((unsigned)a->n_vs_items), dim3(256), 0, s, a->vs_jobs, a->vs_items,
-                       a->n_vs_items, TT, T, B);
+    hipLaunchKernelGGL(k_amp_grads, dim3((unsigned)((a->n_dw_trunk + 3) / 4 + a->n_vs_items)), dim3(256), 0, s,
+                       a->dw_jobs, a->dw_items, a->n_dw_trunk, a->RS, rsn, a->vs_jobs, a->vs_items, a->n_vs_items, TT, T,
+                       B);
     YK_LAUNCHED();
     return YK_OK;
 }
