@@ -416,11 +416,15 @@ def main():
                     help="game groups on their own streams (0: the engine's auto choice)")
     ap.add_argument("--root-scan", type=int, default=1,
                     help="0: every descent scans the root's whole compact set (YK_ROOT_SCAN=0; A/B only)")
+    ap.add_argument("--root-k", type=int, default=0,
+                    help="entries of the root's P order kept (YK_ROOT_K; 0: the engine's 512; A/B only)")
     ap.add_argument("--arena-entries", type=int, default=0,
                     help="P-arena entries per game (0: the engine's overflow-free default)")
     args = ap.parse_args()
     if not args.root_scan:
         os.environ["YK_ROOT_SCAN"] = "0"
+    if args.root_k:
+        os.environ["YK_ROOT_K"] = str(args.root_k)
 
     import torch
     import torch.distributed as dist
