@@ -181,7 +181,7 @@ def train_leg(model_sd, eng, steps=40, batch=512, seed=0):
         flop = 3 * PREDICT_FLOP * batch  # forward + backward (2x) per example
         key = "amp" if amp else "f32"
         out[key] = {"config": f"minibatch {batch} of {n} self-play examples, YachtNNet hidden {H} x {NB}, " +
-                              ("autocast('cuda') + GradScaler arithmetic on hand-written fp16 MFMA kernels (7 launches)"
+                              ("autocast('cuda') + GradScaler arithmetic on hand-written fp16 MFMA kernels (6 launches)"
                                if amp else "f32 (rocBLAS GEMMs + fused HIP row kernels)") +
                               ", AdamW + clip 5.0, dropout 0.3",
                     "ms_per_step": 1000.0 * dt, "examples_per_s": batch / dt, "achieved_tflops": flop / dt / 1e12,

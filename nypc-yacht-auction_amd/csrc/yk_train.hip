@@ -757,10 +757,10 @@ int yk_trainer_buffers(yk_trainer_t* t, float** params, float** grads, int64_t* 
 }
 
 static int backward_impl(yk_trainer_t* t, const yk_state_t* states, const int32_t* targets, const float* values,
-                         const int32_t* batch_idx, int batch, hipStream_t s) {
+                         const int32_t* batch_idx, int batch, bool fuse_norm, hipStream_t s) {
     if (t->amp)
         return yk::amp_backward(t->amp, states, targets, values, batch_idx, batch, t->cfg.dropout, t->cfg.seed, t->step,
-                                t->row_base, t->cfg.vloss_weight, t->lrow, t->lsum, s);
+                                t->row_base, t->cfg.vloss_weight, t->lrow, t->lsum, fuse_norm, s);
     if (rocblas_set_stream(t->blas, s) != rocblas_status_success) return YK_ERR_HIP;
     switch (t->H) {
         case 64: return step_impl<1>(t, states, targets, values, batch_idx, batch, s);
@@ -780,18 +780,23 @@ __global__ void k_epoch_loss(const float* lsum, double* eloss, double b, double 
     }
 }
 
-int yk_trainer_backward(yk_trainer_t* t, const yk_state_t* states, const int32_t* targets, const float* values,
-                        const int32_t* batch_idx, int batch, void* stream) {
+static int backward_call(yk_trainer_t* t, const yk_state_t* states, const int32_t* targets, const float* values,
+                         const int32_t* batch_idx, int batch, bool fuse_norm, void* stream) {
     if (!t || !states || !targets || !values) return YK_ERR_ARG;
     if (batch <= 0 || batch > t->Bmax) return YK_ERR_ARG;
     hipStream_t s = as_stream(stream);
-    int rc = backward_impl(t, states, targets, values, batch_idx, batch, s);
+    int rc = backward_impl(t, states, targets, values, batch_idx, batch, fuse_norm, s);
     t->row_base = 0;  // the offset applies to the one backward it was set for (yk_trainer_set_row_offset)
     if (rc == YK_OK && t->eloss_on) {
         hipLaunchKernelGGL(k_epoch_loss, dim3(1), dim3(64), 0, s, t->lsum, t->eloss, (double)batch, t->eloss_vw);
         YK_LAUNCHED();
     }
     return rc;
+}
+
+int yk_trainer_backward(yk_trainer_t* t, const yk_state_t* states, const int32_t* targets, const float* values,
+                        const int32_t* batch_idx, int batch, void* stream) {
+    return backward_call(t, states, targets, values, batch_idx, batch, false, stream);
 }
 
 int yk_trainer_epoch_loss_begin(yk_trainer_t* t, double vloss_weight) {
@@ -832,7 +837,8 @@ int yk_trainer_apply(yk_trainer_t* t, void* stream) {
 
 int yk_trainer_step(yk_trainer_t* t, const yk_state_t* states, const int32_t* targets, const float* values,
                     const int32_t* batch_idx, int batch, void* stream) {
-    int rc = yk_trainer_backward(t, states, targets, values, batch_idx, batch, stream);
+    // (one call, nothing between backward and apply: the gradient launches sum the norm themselves)
+    int rc = backward_call(t, states, targets, values, batch_idx, batch, true, stream);
     if (rc) return rc;
     return yk_trainer_apply(t, stream);
 }

@@ -20,10 +20,12 @@ void amp_destroy(AmpTrain* a);
 int amp_pack(AmpTrain* a, hipStream_t s);
 // forward + backward of `B` examples into G (gradients of loss_scale x loss, each fp16-rounded as
 // autocast's fp16 GEMMs return them); lrow[i] = (cross-entropy, squared value error) of row i,
-// lsum = their column sums.  Dropout masks: rows are numbered row_base + i.
+// lsum = their column sums.  Dropout masks: rows are numbered row_base + i.  fuse_norm: the
+// gradient launches also sum the unscaled sq-norm, and the next amp_apply uses it instead of
+// re-reading G (only when nothing changes G in between: yk_trainer_step, not the DDP split).
 int amp_backward(AmpTrain* a, const yk_state_t* states, const int32_t* targets, const float* values,
                  const int32_t* idx, int B, float dropout, uint64_t seed, uint64_t step, int64_t row_base,
-                 float vloss_weight, float2* lrow, float* lsum, hipStream_t s);
+                 float vloss_weight, float2* lrow, float* lsum, bool fuse_norm, hipStream_t s);
 // GradScaler.unscale_ + clip_grad_norm_(max_norm) + AdamW step (skipped, with the scale halved,
 // when a gradient is inf / nan) + GradScaler.update + fp16 repack.  sq_out: the unscaled grad
 // sq-norm (double).  dropout / seed / next_step: the next backward's dropout draws, which the

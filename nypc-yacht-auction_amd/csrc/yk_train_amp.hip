@@ -832,7 +832,15 @@ struct DwJob {
 };
 // one weight-gradient item for one wave: (job, 16-row tile of W, up to 4 column tiles), summed over
 // the batch's 32-row slices
-__device__ __forceinline__ void dw_item(const DwJob* __restrict__ jobs, const int4 it, int RS, int rsn, int lane) {
+// norm: returns the item's sum of (g / scale)^2 over what it writes, in every lane (yk_trainer_step's
+// fused gradient norm: the grads k_amp_sq would read, summed where they are made); else 0
+__device__ __forceinline__ double wave_dsum(double x) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o, 64);
+    return x;
+}
+__device__ __forceinline__ double dw_item(const DwJob* __restrict__ jobs, const int4 it, int RS, int rsn, int lane,
+                                          bool norm = false, float inv = 1.f) {
     const DwJob jb = jobs[it.x];
     const int nt = it.y, kt0 = it.z, nk = it.w;
     floatx4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
@@ -847,6 +855,7 @@ __device__ __forceinline__ void dw_item(const DwJob* __restrict__ jobs, const in
             if (t < nk) acc[t] = mfma(a, x[t], acc[t]);
     }
     const int q = lane >> 4, c = lane & 15;
+    double ss = 0.0;
 #pragma unroll
     for (int t = 0; t < 4; t++) {
         if (t >= nk) break;
@@ -854,8 +863,27 @@ __device__ __forceinline__ void dw_item(const DwJob* __restrict__ jobs, const in
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             const int n = 16 * nt + 4 * q + j;
-            if (n < jb.N && k < jb.K) jb.dst[(long)n * jb.K + k] = r16(acc[t][j]);  // fp16 grad_weight
+            if (n < jb.N && k < jb.K) {
+                const float g = r16(acc[t][j]);  // fp16 grad_weight
+                jb.dst[(long)n * jb.K + k] = g;
+                const double x = (double)(g * inv);
+                ss += x * x;
+            }
         }
+    }
+    return norm ? wave_dsum(ss) : 0.0;
+}
+// a block's waves' norm partials -> sqp[slot] (wave order: fixed bits); every thread calls it
+template <int NW>
+__device__ __forceinline__ void block_norm(double ss, double* __restrict__ sqp, int slot) {
+    __shared__ double red[NW];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+#pragma unroll
+        for (int k = 0; k < NW; k++) t += red[k];
+        sqp[slot] = t;
     }
 }
 
@@ -910,7 +938,8 @@ __device__ __forceinline__ void flush_gbb(const AmpDev& d, const float* CP, int 
 template <int H>
 __global__ __launch_bounds__(TTHR) void k_amp_bwd(AmpDev d, int B, float p, uint64_t seed, uint64_t step,
                                                   int64_t row_base, const DwJob* __restrict__ jobs,
-                                                  const int4* __restrict__ hitems, int nhitems, int rsn) {
+                                                  const int4* __restrict__ hitems, int nhitems, int rsn,
+                                                  double* __restrict__ sqp, int slot0) {
     constexpr int LD = H + 4, SA = H + 8, VPL = H / 64, KS = H / 32;
     constexpr int NT = H >= 128 ? H / 128 : 1, NACT = H / (16 * NT);
     constexpr int RW = KS * NT <= 16 ? KS : 16 / NT;
@@ -924,8 +953,10 @@ __global__ __launch_bounds__(TTHR) void k_amp_bwd(AmpDev d, int B, float p, uint
     const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     if (row0 >= B) {  // the blocks past the row tiles: the heads' weight gradients (their operands are
                       // done before this launch), on the CUs the trunk's 8-row workgroups leave idle
-        const int w = (tile - (B + TRV - 1) / TRV) * TW + wave;
-        if (w < nhitems) dw_item(jobs, hitems[w], d.RS, rsn, lane);
+        const int hb = tile - (B + TRV - 1) / TRV, w = hb * TW + wave;
+        double ss = 0.0;
+        if (w < nhitems) ss = dw_item(jobs, hitems[w], d.RS, rsn, lane, sqp != nullptr, sqp ? 1.0f / d.sc->scale : 1.f);
+        if (sqp) block_norm<TW>(ss, sqp, slot0 + hb);
         return;
     }
     // every wave owns columns when NACT == TW (hidden >= 128): a compile-time true, so no branch
@@ -1151,10 +1182,12 @@ struct VsJob {
     const float* src;
     float* dst;
     int ld, N, per_example, round16;  // per_example: rows are 0 trunk tiles, 1 examples, 2 head tiles
+    int in_grad;                      // dst is part of the gradient buffer (not the loss sums)
 };
 // one column-sum item for a 256-thread block: 16 columns of a job, 16 row groups, fixed order
 __device__ __forceinline__ void vecsum_item(const VsJob* __restrict__ jobs, const int2 it, int ntiles, int nhtiles,
-                                            int B, float (&part)[16][17]) {
+                                            int B, float (&part)[16][17], double* __restrict__ sqp = nullptr,
+                                            int slot = 0, float inv = 1.f) {
     const VsJob jb = jobs[it.x];
     const int c = it.y + (threadIdx.x & 15), g = threadIdx.x >> 4;
     const int rows = jb.per_example == 1 ? B : jb.per_example == 2 ? nhtiles : ntiles;
@@ -1169,30 +1202,45 @@ __device__ __forceinline__ void vecsum_item(const VsJob* __restrict__ jobs, cons
     }
     part[g][threadIdx.x & 15] = a0 + a1;
     __syncthreads();
+    double ss = 0.0;
     if (g == 0 && c < jb.N) {
         float s = 0.f;
 #pragma unroll
         for (int k = 0; k < 16; k++) s += part[k][threadIdx.x];
-        jb.dst[c] = jb.round16 ? r16(s) : s;
+        const float v = jb.round16 ? r16(s) : s;
+        jb.dst[c] = v;
+        const double x = jb.in_grad ? (double)(v * inv) : 0.0;
+        ss = x * x;
+    }
+    if (sqp && threadIdx.x < 64) {  // (the 16 column threads are wave 0's lanes 0-15)
+        ss = wave_dsum(ss);
+        if (threadIdx.x == 0) sqp[slot] = ss;
     }
 }
 // after k_amp_bwd: the trunk's weight gradients (dw_item, a wave each; the heads' ran inside
 // k_amp_bwd's launch) and, in the blocks past them, the bias / LayerNorm gradients and loss sums
 // (vecsum_item, a block each) - one launch for both
+// With sqp (yk_trainer_step): every block's norm partial into its slot (this launch's dW blocks
+// 0 .., k_amp_bwd's dW blocks after them, the column sums after all nall dW blocks);
+// k_amp_update sums the slots (a last-block reduction here instead would need an agent-scope
+// release per block - an L2 writeback on this multi-XCD part: 12 -> 96 us measured).
 __global__ __launch_bounds__(256) void k_amp_grads(const DwJob* __restrict__ jobs, const int4* __restrict__ items,
                                                    int nitems, int RS, int rsn, const VsJob* __restrict__ vjobs,
                                                    const int2* __restrict__ vitems, int nvitems, int ntiles,
-                                                   int nhtiles, int B) {
+                                                   int nhtiles, int B, double* __restrict__ sqp, int nall,
+                                                   const Scaler* __restrict__ sc) {
     __shared__ float part[16][17];
+    const float inv = sqp ? 1.0f / sc->scale : 1.f;
     const int ndb = (nitems + 3) / 4;
     if ((int)blockIdx.x >= ndb) {
         const int v = (int)blockIdx.x - ndb;
-        if (v < nvitems) vecsum_item(vjobs, vitems[v], ntiles, nhtiles, B, part);
-        return;
+        if (v < nvitems) vecsum_item(vjobs, vitems[v], ntiles, nhtiles, B, part, sqp, nall + v, inv);
+    } else {
+        const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
+        double ss = 0.0;
+        if (w < nitems) ss = dw_item(jobs, items[w], RS, rsn, threadIdx.x & 63, sqp != nullptr, inv);
+        if (sqp) block_norm<4>(ss, sqp, blockIdx.x);
     }
-    const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (w >= nitems) return;
-    dw_item(jobs, items[w], RS, rsn, threadIdx.x & 63);
 }
 
 // ------------------------------------------------------------------ optimiser
@@ -1211,14 +1259,13 @@ __global__ void k_amp_sq(const float* __restrict__ g, long n, const Scaler* sc, 
     __syncthreads();
     if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
 }
-// the SQ_BLOCKS partials summed by a 256-thread block in one fixed order (every caller gets the
-// same bits): 4 per thread, the wave butterflies, the 4 waves in order
-__device__ __forceinline__ double sq_total(const double* part) {
+// n norm partials summed by a 256-thread block in one fixed order (every caller gets the same
+// bits): strided per thread, the wave butterflies, the 4 waves in order
+__device__ __forceinline__ double sq_total(const double* part, int n) {
     __shared__ double red[4];
-    static_assert(SQ_BLOCKS == 4 * 256, "4 partials per thread");
     double t = 0.0;
-#pragma unroll
-    for (int k = 0; k < 4; k++) t += part[threadIdx.x + 256 * k];
+#pragma unroll 8
+    for (int i = threadIdx.x; i < n; i += 256) t += part[i];
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) t += __shfl_xor(t, o, 64);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = t;
@@ -1294,7 +1341,8 @@ __global__ __launch_bounds__(256) void k_amp_update(const UpdJob* __restrict__ j
                                                     const double* __restrict__ part, double* sq_out,
                                                     const Scaler* __restrict__ sc, Scaler* __restrict__ sc_next,
                                                     float max_norm, float lr, float wd, float b1, float b2, float eps,
-                                                    int n_upd, AmpDev d, float mp, uint64_t mseed, uint64_t mstep) {
+                                                    int n_upd, AmpDev d, float mp, uint64_t mseed, uint64_t mstep,
+                                                    int npart) {
     __shared__ _Float16 Tl[32][40];
     if ((int)blockIdx.x >= n_upd) {  // the blocks past the update's: the next step's dropout draws
         const int q4 = d.H / 4;       // (k_amp_masks' work for row offset 0 and every row of Bmax)
@@ -1305,7 +1353,7 @@ __global__ __launch_bounds__(256) void k_amp_update(const UpdJob* __restrict__ j
         }
         return;
     }
-    const double total = sq_total(part);
+    const double total = sq_total(part, npart);  // (k_amp_sq's SQ_BLOCKS partials or the fused norm's slots)
     const Scaler s0 = *sc;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         *sq_out = total;
@@ -1433,6 +1481,7 @@ struct AmpTrain {
     int4* dw_items = nullptr;
     int n_dw_items = 0;
     int n_dw_trunk = 0;  // items [0, n_dw_trunk): k_amp_grads; the rest (the heads'): inside k_amp_bwd
+    int n_norm_dw = 0;   // the fused norm's slots of the dW blocks (k_amp_grads' 4-wave, k_amp_bwd's TW-wave)
     std::vector<int4> dw_items_host;
     std::vector<int> dw_job_rows;  // for each item: unused (all jobs span the batch)
     VsJob* vs_jobs = nullptr;
@@ -1443,6 +1492,8 @@ struct AmpTrain {
     int n_pk_jobs = 0;
     long pk_total = 0;
     double* sqpart = nullptr;
+    double* sq_items = nullptr;     // the fused norm's per-item partials (yk_trainer_step)
+    bool norm_ready = false;        // the last backward left the total in sq_tot
     Scaler* sc = nullptr;       // the current GradScaler state
     Scaler* sc_next = nullptr;  // k_amp_update writes the next one here; the host swaps the two
     // what d.masks holds: the draws of (seed, step, row offset, p) for rows 0 .. mask_rows - 1
@@ -1589,32 +1640,33 @@ int amp_create(AmpTrain** out, int H, int NB, int Bmax, float* P, float* G, cons
     a->n_dw_items = (int)items.size();
     a->n_dw_trunk = 0;  // the items of the input layer's and the blocks' matrices come first
     while (a->n_dw_trunk < a->n_dw_items && items[a->n_dw_trunk].x < 1 + 2 * NB) a->n_dw_trunk++;
+    a->n_norm_dw = (a->n_dw_trunk + 3) / 4 + (a->n_dw_items - a->n_dw_trunk + TW - 1) / TW;
     // column-sum jobs: bias / LayerNorm gradients and the two loss sums
     std::vector<VsJob> vj;
     const int ldc = d.NVEC * H;
     auto colv = [&](int v) { return d.colpart + (size_t)v * H; };
-    vj.push_back({colv(CV_BIN), G + off[T_BIN], ldc, H, 0, 1});
-    vj.push_back({colv(CV_GIN), G + off[T_GIN], ldc, H, 0, 0});
-    vj.push_back({colv(CV_BEIN), G + off[T_BEIN], ldc, H, 0, 0});
+    vj.push_back({colv(CV_BIN), G + off[T_BIN], ldc, H, 0, 1, 1});
+    vj.push_back({colv(CV_GIN), G + off[T_GIN], ldc, H, 0, 0, 1});
+    vj.push_back({colv(CV_BEIN), G + off[T_BEIN], ldc, H, 0, 0, 1});
     for (int b = 0; b < NB; b++) {
         const int vb = CV_BLK + 6 * b;
-        vj.push_back({colv(vb + 0), G + off[t_blk(b, 1)], ldc, H, 0, 1});
-        vj.push_back({colv(vb + 1), G + off[t_blk(b, 2)], ldc, H, 0, 0});
-        vj.push_back({colv(vb + 2), G + off[t_blk(b, 3)], ldc, H, 0, 0});
-        vj.push_back({colv(vb + 3), G + off[t_blk(b, 5)], ldc, H, 0, 1});
-        vj.push_back({colv(vb + 4), G + off[t_blk(b, 6)], ldc, H, 0, 0});
-        vj.push_back({colv(vb + 5), G + off[t_blk(b, 7)], ldc, H, 0, 0});
+        vj.push_back({colv(vb + 0), G + off[t_blk(b, 1)], ldc, H, 0, 1, 1});
+        vj.push_back({colv(vb + 1), G + off[t_blk(b, 2)], ldc, H, 0, 0, 1});
+        vj.push_back({colv(vb + 2), G + off[t_blk(b, 3)], ldc, H, 0, 0, 1});
+        vj.push_back({colv(vb + 3), G + off[t_blk(b, 5)], ldc, H, 0, 1, 1});
+        vj.push_back({colv(vb + 4), G + off[t_blk(b, 6)], ldc, H, 0, 0, 1});
+        vj.push_back({colv(vb + 5), G + off[t_blk(b, 7)], ldc, H, 0, 0, 1});
     }
-    vj.push_back({colv(CV_GPI), G + off[t_head(NB, HP_G)], ldc, H, 0, 0});
-    vj.push_back({colv(CV_BEPI), G + off[t_head(NB, HP_B)], ldc, H, 0, 0});
-    vj.push_back({colv(CV_GV), G + off[t_head(NB, HV_G)], ldc, H, 0, 0});
-    vj.push_back({colv(CV_BEV), G + off[t_head(NB, HV_B)], ldc, H, 0, 0});
-    vj.push_back({d.dbpi_part, G + off[t_head(NB, HP_BIAS)], LDL, ASIZE, 2, 1});
-    vj.push_back({d.dz1f, G + off[t_head(NB, HV_B1)], VH, VH, 1, 1});
-    vj.push_back({d.v2prod, G + off[t_head(NB, HV_W2)], VH, VH, 1, 1});
-    vj.push_back({d.dzv2, G + off[t_head(NB, HV_B2)], 1, 1, 1, 1});
+    vj.push_back({colv(CV_GPI), G + off[t_head(NB, HP_G)], ldc, H, 0, 0, 1});
+    vj.push_back({colv(CV_BEPI), G + off[t_head(NB, HP_B)], ldc, H, 0, 0, 1});
+    vj.push_back({colv(CV_GV), G + off[t_head(NB, HV_G)], ldc, H, 0, 0, 1});
+    vj.push_back({colv(CV_BEV), G + off[t_head(NB, HV_B)], ldc, H, 0, 0, 1});
+    vj.push_back({d.dbpi_part, G + off[t_head(NB, HP_BIAS)], LDL, ASIZE, 2, 1, 1});
+    vj.push_back({d.dz1f, G + off[t_head(NB, HV_B1)], VH, VH, 1, 1, 1});
+    vj.push_back({d.v2prod, G + off[t_head(NB, HV_W2)], VH, VH, 1, 1, 1});
+    vj.push_back({d.dzv2, G + off[t_head(NB, HV_B2)], 1, 1, 1, 1, 1});
     const size_t loss_job = vj.size();  // (the trainer's lrow / lsum: filled in per call)
-    vj.push_back({nullptr, nullptr, 2, 2, 1, 0});
+    vj.push_back({nullptr, nullptr, 2, 2, 1, 0, 0});
     std::vector<int2> vitems;
     for (size_t j = 0; j < vj.size(); j++)
         for (int c = 0; c < vj[j].N; c += 16) vitems.push_back(make_int2((int)j, c));
@@ -1650,7 +1702,8 @@ int amp_create(AmpTrain** out, int H, int NB, int Bmax, float* P, float* G, cons
     }
     if (aalloc(a, &a->dw_jobs, jobs.size()) || aalloc(a, &a->dw_items, items.size()) ||
         aalloc(a, &a->vs_jobs, vj.size()) || aalloc(a, &a->vs_items, vitems.size()) ||
-        aalloc(a, &a->pk_jobs, pj.size()) || aalloc(a, &a->pk_blk, pblk.size())) {
+        aalloc(a, &a->pk_jobs, pj.size()) || aalloc(a, &a->pk_blk, pblk.size()) ||
+        aalloc(a, &a->sq_items, (size_t)(a->n_dw_items + a->n_vs_items))) {  // (>= the blocks')
         amp_destroy(a);
         return YK_ERR_NOMEM;
     }
@@ -1682,12 +1735,14 @@ int amp_pack(AmpTrain* a, hipStream_t s) {
 
 int amp_backward(AmpTrain* a, const yk_state_t* states, const int32_t* targets, const float* values,
                  const int32_t* idx, int B, float dropout, uint64_t seed, uint64_t step, int64_t row_base,
-                 float vloss_weight, float2* lrow, float* lsum, hipStream_t s) {
+                 float vloss_weight, float2* lrow, float* lsum, bool fuse_norm, hipStream_t s) {
     if (B <= 0 || B > a->Bmax) return YK_ERR_ARG;
+    a->norm_ready = false;
+    double* sqp = fuse_norm ? a->sq_items : nullptr;
     AmpDev& d = a->d;
     if (a->lrow != lrow || a->lsum != lsum) {  // the loss-sum job reads the trainer's row losses
         const int j = 3 + 6 * a->NB + 4 + 4;
-        VsJob jb{reinterpret_cast<const float*>(lrow), lsum, 2, 2, 1, 0};
+        VsJob jb{reinterpret_cast<const float*>(lrow), lsum, 2, 2, 1, 0, 0};
         YK_HIP(hipMemcpy(a->vs_jobs + j, &jb, sizeof(VsJob), hipMemcpyHostToDevice));
         a->lrow = lrow;
         a->lsum = lsum;
@@ -1714,7 +1769,7 @@ int amp_backward(AmpTrain* a, const yk_state_t* states, const int32_t* targets, 
         YK_LAUNCHED();                                                                                              \
         hipLaunchKernelGGL(k_amp_bwd<HH>, dim3(TT + (a->n_dw_items - a->n_dw_trunk + TW - 1) / TW), dim3(TTHR), 0, s, \
                            d, B, dropout, seed, step, row_base, a->dw_jobs, a->dw_items + a->n_dw_trunk,          \
-                           a->n_dw_items - a->n_dw_trunk, rsn);                                                    \
+                           a->n_dw_items - a->n_dw_trunk, rsn, sqp, (a->n_dw_trunk + 3) / 4);                      \
         YK_LAUNCHED();                                                                                              \
         break;
         YK_AMP_FWD(64)
@@ -1726,8 +1781,9 @@ int amp_backward(AmpTrain* a, const yk_state_t* states, const int32_t* targets, 
     }
     hipLaunchKernelGGL(k_amp_grads, dim3((unsigned)((a->n_dw_trunk + 3) / 4 + a->n_vs_items)), dim3(256), 0, s,
                        a->dw_jobs, a->dw_items, a->n_dw_trunk, a->RS, rsn, a->vs_jobs, a->vs_items, a->n_vs_items, TT, T,
-                       B);
+                       B, sqp, a->n_norm_dw, a->sc);
     YK_LAUNCHED();
+    a->norm_ready = fuse_norm;
     return YK_OK;
 }
 
@@ -1781,12 +1837,16 @@ int amp_apply(AmpTrain* a, long nparams, float* M, float* V, double* sq_out, flo
         const int rc = build_update_jobs(a, nparams, M, V);
         if (rc != YK_OK) return rc;
     }
-    hipLaunchKernelGGL(k_amp_sq, dim3(SQ_BLOCKS), dim3(256), 0, s, a->d.G, nparams, a->sc, a->sqpart);
-    YK_LAUNCHED();
+    const bool fused = a->norm_ready;  // (yk_trainer_step: k_amp_grads summed the norm; no all-reduce between)
+    a->norm_ready = false;
+    if (!fused) {
+        hipLaunchKernelGGL(k_amp_sq, dim3(SQ_BLOCKS), dim3(256), 0, s, a->d.G, nparams, a->sc, a->sqpart);
+        YK_LAUNCHED();
+    }
     const long nm = dropout > 0.f ? (long)(1 + a->NB) * a->Bmax * (a->H / 4) : 0;
     hipLaunchKernelGGL(k_amp_update, dim3((unsigned)(a->n_upd_items + (nm + 255) / 256)), dim3(256), 0, s, a->upd_jobs,
-                       a->upd_items, a->sqpart, sq_out, a->sc, a->sc_next, max_norm, lr, wd, b1, b2, eps, a->n_upd_items,
-                       a->d, dropout, seed, next_step);
+                       a->upd_items, fused ? a->sq_items : a->sqpart, sq_out, a->sc, a->sc_next, max_norm, lr, wd, b1, b2, eps, a->n_upd_items,
+                       a->d, dropout, seed, next_step, fused ? a->n_norm_dw + a->n_vs_items : SQ_BLOCKS);
     YK_LAUNCHED();
     a->mask_valid = nm > 0;
     a->mask_seed = seed;

@@ -408,3 +408,39 @@ def test_amp_skipped_step_leaves_unscaled_gradients(T, golden):
     assert np.array_equal(tr.params().cpu().numpy(), p0)
     want = g_scaled * np.float32(2.0 ** -40)
     np.testing.assert_array_equal(tr.grads().cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("H,NB,B,scale", [(256, 6, 512, None), (64, 1, 32, 2.0 ** 40)])
+def test_amp_fused_norm_step_equals_backward_then_apply(T, golden, H, NB, B, scale):
+    """yk_trainer_step (one call) sums the gradient norm inside the gradient launches instead of
+    re-reading G; backward() + apply() (the DDP split, an all-reduce may sit between) re-reads it.
+    Same grad sq-norm (double sums in another order: rel 1e-12), same GradScaler state and the same
+    parameters (the clip coefficient may move by an ulp: rtol 1e-6) over 3 steps, and an overflowing
+    step (scale 2^40) is skipped the same way."""
+    K, N, TR = T
+    W = golden("states.npz")["states"]
+    W = np.concatenate([W] * (3 * B // len(W) + 1))[:3 * B]
+    rng = np.random.RandomState(9)
+    S = K.states_to_device(W)
+    tg = torch.tensor(rng.randint(0, 3226, 3 * B), dtype=torch.int32, device="cuda")
+    vv = torch.tensor(rng.rand(3 * B) * 2 - 1, dtype=torch.float32, device="cuda")
+    kw = dict(max_batch=B, dropout=0.1, amp=True)
+    if scale:
+        kw["init_scale"] = scale
+    fused = TR.Trainer(_sd(H, NB), H, NB, **kw)
+    split = TR.Trainer(_sd(H, NB), H, NB, **kw)
+    for k in range(3):
+        idx = torch.arange(k * B, (k + 1) * B, dtype=torch.int32, device="cuda")
+        fused.step(S, tg, vv, idx=idx)
+        split.backward(S, tg, vv, idx=idx)
+        split.apply()
+        lf, ls = fused.losses(), split.losses()
+        assert lf[0] == ls[0] and lf[1] == ls[1], k
+        if np.isfinite(ls[2]):
+            assert abs(lf[2] - ls[2]) <= 1e-12 * ls[2], (k, lf[2], ls[2])
+        else:
+            assert not np.isfinite(lf[2]), k
+        assert fused.amp_state() == split.amp_state(), k
+        np.testing.assert_allclose(fused.params().cpu().numpy(), split.params().cpu().numpy(), rtol=1e-6, atol=1e-9)
+    if scale:
+        assert fused.amp_state()["steps"] < 3
