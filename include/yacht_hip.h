@@ -310,7 +310,8 @@ int yk_trainer_backward(yk_trainer_t* t, const yk_state_t* states, const int32_t
                         const int32_t* batch_idx, int batch, void* stream);
 /* clip_grad_norm_ + AdamW on the (possibly all-reduced) gradient buffer; advances the step */
 int yk_trainer_apply(yk_trainer_t* t, void* stream);
-/* yk_trainer_backward + yk_trainer_apply */
+/* yk_trainer_backward + yk_trainer_apply; in amp mode the gradient launches also sum the unscaled
+ * grad norm (nothing can change the buffer between the two), so apply does not re-read it */
 int yk_trainer_step(yk_trainer_t* t, const yk_state_t* states, const int32_t* targets, const float* values,
                     const int32_t* batch_idx, int batch, void* stream);
 /* HOST out[3]: sum over the last batch of cross-entropy, of squared value error; grad sq-norm */
