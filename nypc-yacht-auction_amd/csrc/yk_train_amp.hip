@@ -1470,6 +1470,9 @@ __global__ __launch_bounds__(256) void k_amp_update(const UpdJob* __restrict__ j
 }  // namespace
 
 // ------------------------------------------------------------------ host
+#ifndef YK_DW_KG
+#define YK_DW_KG 2
+#endif
 namespace yk {
 
 struct AmpTrain {
@@ -1634,8 +1637,9 @@ int amp_create(AmpTrain** out, int H, int NB, int Bmax, float* P, float* G, cons
     std::vector<int4> items;
     for (size_t j = 0; j < jobs.size(); j++) {
         const int ntn = (jobs[j].N + 15) / 16, ntk = (jobs[j].K + 15) / 16;
-        for (int k0 = 0; k0 < ntk; k0 += 4)
-            for (int nt = 0; nt < ntn; nt++) items.push_back(make_int4((int)j, nt, k0, std::min(4, ntk - k0)));
+        const int kg = (int)j < 1 + 2 * NB ? YK_DW_KG : 4;  // (k tiles per item: the trunk's fill more SIMDs with fewer)
+        for (int k0 = 0; k0 < ntk; k0 += kg)
+            for (int nt = 0; nt < ntn; nt++) items.push_back(make_int4((int)j, nt, k0, std::min(kg, ntk - k0)));
     }
     a->n_dw_items = (int)items.size();
     a->n_dw_trunk = 0;  // the items of the input layer's and the blocks' matrices come first
