@@ -494,6 +494,82 @@ __device__ __host__ inline bool action_valid(const YkS& s, int player, int a) {
     return !((wa_used(wa) >> cat) & 1) && T.comb_max[ci] < n;
 }
 
+// ------------------------------------------------------------------ cross-lane exchange
+// xlane<O>(x): the value lane l ^ O holds, without __shfl_xor's LDS round trip (ds_bpermute,
+// ~100+ cycles, on the LDS pipe every wave of the CU shares): DPP quad permutes for O = 1, 2,
+// the quad reversal then the half-row mirror for O = 4, a row rotation by 8 for O = 8, and
+// gfx950's permlane swaps for O = 16, 32.  Exact for any contents of the wave, so a butterfly
+// on it gives __shfl_xor's results bit for bit (tools/xlane_check.hip checks every O).
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_mov(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, 0xF, 0xF, false);
+}
+template <int O>
+__device__ __forceinline__ uint32_t xlane_u(uint32_t v) {
+    static_assert(O == 1 || O == 2 || O == 4 || O == 8 || O == 16 || O == 32, "xor offsets 1 .. 32");
+    if constexpr (O == 1) return dpp_mov<0xB1>(v);                   // quad_perm [1,0,3,2]
+    else if constexpr (O == 2) return dpp_mov<0x4E>(v);              // quad_perm [2,3,0,1]
+    else if constexpr (O == 4) return dpp_mov<0x141>(dpp_mov<0x1B>(v));  // quad_perm [3,2,1,0], row_half_mirror
+    else if constexpr (O == 8) return dpp_mov<0x128>(v);             // row_ror:8
+    else {
+        // v_permlane{16,32}_swap(v, v): the first result holds the lower row / half in both
+        // positions, the second the upper
+        const bool upper = (threadIdx.x & O) != 0;
+        if constexpr (O == 16) {
+            const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+            return upper ? r[0] : r[1];
+        } else {
+            const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+            return upper ? r[0] : r[1];
+        }
+    }
+}
+template <int O>
+__device__ __forceinline__ float xlane(float v) { return __builtin_bit_cast(float, xlane_u<O>(__builtin_bit_cast(uint32_t, v))); }
+template <int O>
+__device__ __forceinline__ int xlane(int v) { return (int)xlane_u<O>((uint32_t)v); }
+template <int O>
+__device__ __forceinline__ double xlane(double v) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    return __builtin_bit_cast(double, (uint64_t)xlane_u<O>((uint32_t)b) | (uint64_t)xlane_u<O>((uint32_t)(b >> 32)) << 32);
+}
+// the sum over the wave in __shfl_xor's butterfly order (o = 32 .. 1), bit for bit
+template <typename T>
+__device__ __forceinline__ T xlane_sum(T v) {
+    v += xlane<32>(v);
+    v += xlane<16>(v);
+    v += xlane<8>(v);
+    v += xlane<4>(v);
+    v += xlane<2>(v);
+    return v + xlane<1>(v);
+}
+// lane f's value (f wave-uniform): v_readlane instead of a ds_bpermute
+__device__ __forceinline__ float lane_val(float v, int f) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), f));
+}
+// argmax butterfly over the wave: the largest value, the lowest index among equals, on every lane
+// (the same pairs as a __shfl_xor butterfly, so the same result)
+template <int O = 32>
+__device__ __forceinline__ void wave_argmax_step(float& best, int& bj) {
+    const float ob = xlane<O>(best);
+    const int oj = xlane<O>(bj);
+    if (ob > best || (ob == best && oj < bj)) {
+        best = ob;
+        bj = oj;
+    }
+    if constexpr (O > 1) wave_argmax_step<O / 2>(best, bj);
+}
+template <int O = 32>
+__device__ __forceinline__ void wave_argmax_step(int& best, int& bj) {
+    const int ob = xlane<O>(best);
+    const int oj = xlane<O>(bj);
+    if (ob > best || (ob == best && oj < bj)) {
+        best = ob;
+        bj = oj;
+    }
+    if constexpr (O > 1) wave_argmax_step<O / 2>(best, bj);
+}
+
 // ------------------------------------------------------------------ GreedyYachtPlayer
 // Best immediate gain (score + the basic bonus when it crosses 63,000) over unused categories x
 // combos of `dice` (nibbles, n of them), all 64 lanes together; *best_t = the first maximum in
@@ -519,14 +595,7 @@ __device__ inline int greedy_best_wave(uint64_t dice, int n, uint32_t used, int 
             bt = t;
         }
     }
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-        const int ob = __shfl_xor(best, o, 64), ot = __shfl_xor(bt, o, 64);
-        if (ob > best || (ob == best && ot < bt)) {
-            best = ob;
-            bt = ot;
-        }
-    }
+    wave_argmax_step(best, bt);
     *best_t = bt;
     return best;
 }

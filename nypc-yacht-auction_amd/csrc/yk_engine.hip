@@ -337,15 +337,29 @@ __device__ __forceinline__ void wave_sync() {
 }
 
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-    return v;
+    v = fmaxf(v, xlane<32>(v));
+    v = fmaxf(v, xlane<16>(v));
+    v = fmaxf(v, xlane<8>(v));
+    v = fmaxf(v, xlane<4>(v));
+    v = fmaxf(v, xlane<2>(v));
+    return fmaxf(v, xlane<1>(v));
 }
 __device__ __forceinline__ float softmax_p(float x, float m, float lse) { return exp_acc(x - m - lse); }  // yk_common.h
-__device__ __forceinline__ float wave_sumf(float v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+__device__ __forceinline__ float wave_sumf(float v) {  // __shfl_xor's butterfly, bit for bit
+    v += xlane<32>(v);
+    v += xlane<16>(v);
+    v += xlane<8>(v);
+    v += xlane<4>(v);
+    v += xlane<2>(v);
+    return v + xlane<1>(v);
+}
+__device__ __forceinline__ int wave_min_i(int v) {
+    v = min(v, xlane<32>(v));
+    v = min(v, xlane<16>(v));
+    v = min(v, xlane<8>(v));
+    v = min(v, xlane<4>(v));
+    v = min(v, xlane<2>(v));
+    return min(v, xlane<1>(v));
 }
 
 // ------------------------------------------------------------------ python-typed arithmetic
@@ -561,21 +575,18 @@ __device__ __forceinline__ int root_scan(const EngDev& d, int t, int lane, uint3
             const uint64_t bal = __ballot(unv);
             if (!bal) continue;  // every entry of this piece is visited
             const int f = __builtin_ctzll(bal);
-            ub = __shfl(u, f, 64);
+            ub = lane_val(u, f);
             found = true;
             first = k0 + f;
             cand = unv && lane >= f && u == ub;
         } else {
             cand = unv && u == ub;
         }
-        int cj = cand ? jj : 0x7FFFFFFF;
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) cj = min(cj, __shfl_xor(cj, o, 64));
-        uj = min(uj, cj);
+        uj = min(uj, wave_min_i(cand ? jj : 0x7FFFFFFF));
         // u is non-increasing along the order: the band goes on into the next piece only if the
         // piece's last entry still has u == ub
-        if (!(k0 + 64 < nk && __shfl(u, 63, 64) == ub)) {
-            done = k0 + 64 < nk || nk == V || __shfl(u, (nk - 1 - k0) & 63, 64) != ub;
+        if (!(k0 + 64 < nk && lane_val(u, 63) == ub)) {
+            done = k0 + 64 < nk || nk == V || lane_val(u, (nk - 1 - k0) & 63) != ub;
             break;
         }
     }
@@ -590,15 +601,7 @@ __device__ __forceinline__ int root_scan(const EngDev& d, int t, int lane, uint3
         btag = 0;
     }
     const int mine = bj;
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-        const float ob = __shfl_xor(best, o, 64);
-        const int oj2 = __shfl_xor(bj, o, 64);
-        if (ob > best || (ob == best && oj2 < bj)) {
-            best = ob;
-            bj = oj2;
-        }
-    }
+    wave_argmax_step(best, bj);
     const uint64_t own = __ballot(mine == bj);  // the lane whose own candidate won holds its tag
     wtag = own ? __builtin_amdgcn_readlane(btag, (int)__builtin_ctzll(own)) : 0u;
     scanned += (uint64_t)nv + (uint64_t)walked;
@@ -746,15 +749,7 @@ __device__ __forceinline__ void select_game(const EngDev& d, int e, int lane, co
                     }
                 }
             }
-#pragma unroll
-            for (int o = 32; o >= 1; o >>= 1) {
-                const float ob = __shfl_xor(best, o, 64);
-                const int oj = __shfl_xor(bj, o, 64);
-                if (ob > best || (ob == best && oj < bj)) {
-                    best = ob;
-                    bj = oj;
-                }
-            }
+            wave_argmax_step(best, bj);
             scanned += (uint64_t)V;
             bj_out = bj;
             // the winner's lane holds its tag: its own best is the wave's (lowest j among equals)
@@ -955,18 +950,23 @@ __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int l
                 racc.w += q[j].w;
             }
         const float half = (racc.x + racc.y) + (racc.z + racc.w);
-        const float other = __shfl_xor(half, 1, 64);
+        const float other = xlane<1>(half);
         float lsum = h == 0 ? half + other : other + half;
 #pragma unroll
         for (int r = 0; r < PW_TMAX; r++)
             if (r < R) lsum += qt[r];  // h = 0 holds the tail
-        lsum = __shfl(lsum, lane & ~1, 64);
+        lsum = __builtin_bit_cast(float, dpp_mov<0xA0>(__builtin_bit_cast(uint32_t, lsum)));  // quad_perm [0,0,2,2]: the even lane's
         // the perfect tree over the 32 leaves, left + right at every level
-#pragma unroll
-        for (int o = 2; o <= 32; o <<= 1) {
-            const float y = __shfl_xor(lsum, o, 64);
-            lsum = (lane & o) ? y + lsum : lsum + y;
-        }
+        float y = xlane<2>(lsum);
+        lsum = (lane & 2) ? y + lsum : lsum + y;
+        y = xlane<4>(lsum);
+        lsum = (lane & 4) ? y + lsum : lsum + y;
+        y = xlane<8>(lsum);
+        lsum = (lane & 8) ? y + lsum : lsum + y;
+        y = xlane<16>(lsum);
+        lsum = (lane & 16) ? y + lsum : lsum + y;
+        y = xlane<32>(lsum);
+        lsum = (lane & 32) ? y + lsum : lsum + y;
         const float sum = lsum;
         // ---- allocate + write P over the compact valid set, zero edge slots
         const int VP = pad4(V);

@@ -213,6 +213,11 @@ __device__ __forceinline__ void layernorm(float (&x)[VPL], const float* g, const
 // v_cvt_pk_f16_f32) for even VPL: the same operations per element as silu / layernorm /
 // put_planes, except that each lane's partial sums pair its values ((x0 + x2) + (x1 + x3)).
 // The trunk's LayerNorm phases are VALU-bound and on the forward's critical path.
+#ifdef XP_CONTRACT
+#define YK_ROW_CONTRACT _Pragma("clang fp contract(fast)")
+#else
+#define YK_ROW_CONTRACT
+#endif
 typedef float f2v __attribute__((ext_vector_type(2)));
 typedef _Float16 h2v __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f2v ld2(const float* p) { return *reinterpret_cast<const f2v*>(p); }
@@ -244,8 +249,8 @@ __device__ __forceinline__ void wave_sum4(float (&v)[4]) {
     k += dpp_f<0x4E, 0xF>(sd);  // quad_perm [2,3,0,1]: lane & 3 = 0 -> v0, 2 -> v1, 1 -> v2, 3 -> v3
     k += dpp_f<0x124, 0xF>(k);  // row_ror:4 and row_ror:8: the row's four quads (lane & 3 kept)
     k += dpp_f<0x128, 0xF>(k);
-    k += __shfl_xor(k, 16, 64);  // the wave's four rows
-    k += __shfl_xor(k, 32, 64);
+    k += xlane<16>(k);  // the wave's four rows (permlane swaps: no LDS round trip)
+    k += xlane<32>(k);
     const int ki = __builtin_bit_cast(int, k);
     v[0] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(ki, 0));
     v[1] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(ki, 2));
@@ -255,6 +260,7 @@ __device__ __forceinline__ void wave_sum4(float (&v)[4]) {
 
 template <int NP, int R>
 __device__ __forceinline__ void ln_stats2(const f2v (&x)[R][NP], float (&mean)[R], float (&rstd)[R], int H) {
+    YK_ROW_CONTRACT
     float sh[R], s[R], q[R];
 #pragma unroll
     for (int r = 0; r < R; r++) {
@@ -294,6 +300,7 @@ __device__ __forceinline__ void ln_stats2(const f2v (&x)[R][NP], float (&mean)[R
 template <int NP, int R>
 __device__ __forceinline__ void ln_apply2(f2v (&x)[R][NP], const float (&mean)[R], const float (&rstd)[R],
                                           const float* g, const float* b, int c0) {
+    YK_ROW_CONTRACT
 #pragma unroll
     for (int r = 0; r < R; r++)
 #pragma unroll
@@ -548,6 +555,9 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
         if (!amask) return;
     }
     const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+#ifdef XP_PRIO
+    if (NW == 8 && wave >= 4) __builtin_amdgcn_s_setprio(1);
+#endif
     // owns columns of the H-wide layers: every wave when NACT == NW (hidden >= 128), as a
     // compile-time true - a branch around the weight ring would make the wait counters merge at its
     // join, and the resulting vmcnt(0) drains the ring's in-flight refills of the next layer
@@ -957,8 +967,10 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
     if (mlse) {  // over the 16 column lanes
 #pragma unroll
         for (int j = 0; j < 4; j++) {
-#pragma unroll
-            for (int o = 1; o < 16; o <<= 1) stat_merge(sm[j], ss[j], __shfl_xor(sm[j], o, 64), __shfl_xor(ss[j], o, 64));
+            stat_merge(sm[j], ss[j], xlane<1>(sm[j]), xlane<1>(ss[j]));
+            stat_merge(sm[j], ss[j], xlane<2>(sm[j]), xlane<2>(ss[j]));
+            stat_merge(sm[j], ss[j], xlane<4>(sm[j]), xlane<4>(ss[j]));
+            stat_merge(sm[j], ss[j], xlane<8>(sm[j]), xlane<8>(ss[j]));
         }
     }
     lds_barrier();  // every wave is done with v_head.2 (reads of T) and stored its av columns

@@ -119,11 +119,7 @@ __device__ __forceinline__ floatx4 mfma(float4 a, float4 b, floatx4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, a), __builtin_bit_cast(half8, b), c, 0, 0, 0);
 }
 __device__ __forceinline__ floatx4 zero4() { return floatx4{0.f, 0.f, 0.f, 0.f}; }
-__device__ __forceinline__ float wsum(float v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
+__device__ __forceinline__ float wsum(float v) { return xlane_sum(v); }
 // two full-wave sums at once on the DPP path (quad / row shuffles, row broadcasts, lane 63 read):
 // the row passes' reductions, whose latency is on every layer's critical path
 template <int CTRL, int ROW_MASK>
@@ -634,9 +630,12 @@ __global__ __launch_bounds__(TTHR) void k_amp_head(AmpDev d, int B) {
         do_tile(wb, bb, n2);
     }
 #pragma unroll
-    for (int j = 0; j < 4; j++)
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) stat_merge(m[j], s[j], __shfl_xor(m[j], o, 64), __shfl_xor(s[j], o, 64));
+    for (int j = 0; j < 4; j++) {
+        stat_merge(m[j], s[j], xlane<1>(m[j]), xlane<1>(s[j]));
+        stat_merge(m[j], s[j], xlane<2>(m[j]), xlane<2>(s[j]));
+        stat_merge(m[j], s[j], xlane<4>(m[j]), xlane<4>(s[j]));
+        stat_merge(m[j], s[j], xlane<8>(m[j]), xlane<8>(s[j]));
+    }
     if ((lane & 15) == 0) {
 #pragma unroll
         for (int j = 0; j < 4; j++) red[wave][4 * q + j] = make_float2(m[j], s[j]);
@@ -834,11 +833,7 @@ struct DwJob {
 // the batch's 32-row slices
 // norm: returns the item's sum of (g / scale)^2 over what it writes, in every lane (yk_trainer_step's
 // fused gradient norm: the grads k_amp_sq would read, summed where they are made); else 0
-__device__ __forceinline__ double wave_dsum(double x) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o, 64);
-    return x;
-}
+__device__ __forceinline__ double wave_dsum(double x) { return xlane_sum(x); }
 __device__ __forceinline__ double dw_item(const DwJob* __restrict__ jobs, const int4 it, int RS, int rsn, int lane,
                                           bool norm = false, float inv = 1.f) {
     const DwJob jb = jobs[it.x];
@@ -1253,8 +1248,7 @@ __global__ void k_amp_sq(const float* __restrict__ g, long n, const Scaler* sc, 
         const double x = (double)(g[i] * inv);
         s += x * x;
     }
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
+    s = xlane_sum(s);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
     __syncthreads();
     if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
@@ -1266,8 +1260,7 @@ __device__ __forceinline__ double sq_total(const double* part, int n) {
     double t = 0.0;
 #pragma unroll 8
     for (int i = threadIdx.x; i < n; i += 256) t += part[i];
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) t += __shfl_xor(t, o, 64);
+    t = xlane_sum(t);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = t;
     __syncthreads();
     const double tot = (red[0] + red[1]) + (red[2] + red[3]);

@@ -36,6 +36,13 @@ def rank_world():
     return 0, 1
 
 
+def _group():
+    """True when a process group is initialised.  The collectives below short-circuit only
+    without one: a group of world size 1 still issues its RCCL call (the one-GPU box's test of
+    the code path the 8-GPU run takes)."""
+    return dist.is_available() and dist.is_initialized()
+
+
 def barrier():
     if rank_world()[1] > 1:
         dist.barrier()
@@ -57,7 +64,7 @@ def shard(n_total: int, rank: int, world: int):
 
 def allgather_records(buf: torch.Tensor) -> torch.Tensor:
     """Every rank contributes an equal-size uint8 record image -> [world, nbytes] on all ranks."""
-    if not dist.is_initialized() or dist.get_world_size() == 1:
+    if not _group():
         return buf.reshape(1, -1)
     world = dist.get_world_size()
     out = torch.empty((world, buf.numel()), dtype=buf.dtype, device=buf.device)
@@ -77,7 +84,7 @@ def allreduce_grads(trainer, weight: float = None) -> None:
     of the ranks' gradients; else each rank's gradient is scaled by `weight` (its share of the
     minibatch) and the results summed - the gradient of the whole minibatch when the shares
     are unequal.  RCCL works on the device buffer in place; gloo goes through a host copy."""
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not _group():
         return
     g = trainer.grads()
     w = dist.get_world_size()
@@ -96,7 +103,7 @@ def allreduce_grads(trainer, weight: float = None) -> None:
 
 def allreduce_counts(counts, device=None):
     """Sum of small integer tallies over the ranks (the gating arena's wins / losses / draws)."""
-    if rank_world()[1] == 1:
+    if not _group():
         return [int(x) for x in counts]
     nccl = dist.get_backend() == "nccl"  # RCCL reduces device tensors only
     t = torch.tensor([int(x) for x in counts], dtype=torch.int64, device=(device or "cuda") if nccl else "cpu")

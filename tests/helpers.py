@@ -83,3 +83,34 @@ def check_recorded_priors(pi, v, cnt, leaves, sd, hidden=256, nblocks=6, every=1
           f"max |v err| {verr_e:.2e} (torch fp32 {verr_r:.2e})")
     assert err_e <= REF_FACTOR * err_r, (err_e, err_r)
     return len(rs)
+
+
+# ---- the trainers' dropout keep masks on the host (yk_common.h dropout_bits), for torch references
+_M32 = np.uint64(0xFFFFFFFF)
+
+
+def philox_draw64_np(seed, env, ctr):
+    """Philox4x32-10 of (ctr lo, ctr hi, env, 0) under key (seed lo, seed hi), the first two words:
+    yk_common.h philox_draw / oracle/spec.py draw64, vectorised over ctr (uint64 array)."""
+    ctr = np.asarray(ctr, dtype=np.uint64)
+    c0, c1 = ctr & _M32, ctr >> np.uint64(32)
+    c2 = np.full_like(ctr, np.uint64(int(env) & 0xFFFFFFFF))
+    c3 = np.zeros_like(ctr)
+    k0, k1 = np.uint64(int(seed) & 0xFFFFFFFF), np.uint64((int(seed) >> 32) & 0xFFFFFFFF)
+    for _ in range(10):
+        p0, p1 = np.uint64(0xD2511F53) * c0, np.uint64(0xCD9E8D57) * c2
+        c0, c1, c2, c3 = (p1 >> np.uint64(32)) ^ c1 ^ k0, p1 & _M32, (p0 >> np.uint64(32)) ^ c3 ^ k1, p0 & _M32
+        k0, k1 = (k0 + np.uint64(0x9E3779B9)) & _M32, (k1 + np.uint64(0xBB67AE85)) & _M32
+    return c0 | (c1 << np.uint64(32))
+
+
+def dropout_keep_np(seed, layer, step, rows, H, p, row_base=0):
+    """The keep mask [rows, H] of dropout layer `layer` (0: inp, 1 + b: block b) at dropout step
+    `step`: element e = (row_base + row) H + col is kept iff the 16-bit uniform (bits 16 (e % 4) ..)
+    of the draw of its group e // 4 is >= p (yk_common.h dropout_bits / dropout_keep)."""
+    g = (np.arange(rows, dtype=np.uint64)[:, None] + np.uint64(row_base)) * np.uint64(H // 4) + \
+        np.arange(H // 4, dtype=np.uint64)[None, :]
+    d = philox_draw64_np(seed, 0x44524F50 + layer, (np.uint64(step) << np.uint64(32)) ^ g)
+    u = (d[:, :, None] >> (np.uint64(16) * np.arange(4, dtype=np.uint64))) & np.uint64(0xFFFF)
+    keep = u.astype(np.float32) * np.float32(1.0 / 65536.0) >= np.float32(p)
+    return keep.reshape(rows, H)
