@@ -84,33 +84,56 @@ def cpu_baseline(state_dict, sims, seconds_target=15.0, threads=None):
                                 "survey container (SURVEY.md section 6); it is not on the GPU box"}
 
 
-def measured_traffic(args, kind="forward"):
-    """HBM bytes per k_forward (kind "forward") / k_expand_backup ("expand") launch from the
-    committed rocprofv3 PMC passes of this exact configuration (profiles/*_{kind}_traffic.json,
-    tools/profile_bench.sh); None otherwise."""
+def kernel_sources_sha16():
+    """The kernels' identity: sha256 over the sources libyacht_hip.so is built from (csrc, the
+    C-ABI header, the Makefile), 16 hex digits.  tools/profile_bench.sh records it with every
+    rocprofv3 summary, so the bench line cites counters of the tree it runs, or says they are stale."""
+    import hashlib
+    h = hashlib.sha256()
+    pkg = os.path.join(REPO, "nypc-yacht-auction_amd")
+    files = sorted(os.path.join(pkg, "csrc", f) for f in os.listdir(os.path.join(pkg, "csrc"))
+                   if f.endswith((".hip", ".h")))
+    for f in files + [os.path.join(REPO, "include", "yacht_hip.h"), os.path.join(pkg, "Makefile")]:
+        h.update(os.path.basename(f).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def _measured(args, pattern):
+    """The committed rocprofv3 summary (profiles/<pattern>) of this configuration measured on these
+    kernel sources; without one, the last of another tree's, marked stale.  -> (json, relpath, stale)."""
     import glob
-    best = None
-    for f in sorted(glob.glob(os.path.join(REPO, "profiles", f"*_{kind}_traffic.json"))):
+    cur = kernel_sources_sha16()
+    match = other = None
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", pattern))):
         with open(f) as fh:
             t = json.load(fh)
         c = t.get("config", {})
-        if (c.get("envs"), c.get("sims"), c.get("hidden"), c.get("nblocks")) == (args.envs, args.sims, H, NB):
-            best = (t["hbm_bytes_per_launch"], os.path.relpath(f, REPO))
-    return best
+        if (c.get("envs"), c.get("sims"), c.get("hidden"), c.get("nblocks")) != (args.envs, args.sims, H, NB):
+            continue
+        if t.get("kernel_src_sha16") == cur:
+            match = (t, os.path.relpath(f, REPO))
+        else:
+            other = (t, os.path.relpath(f, REPO))
+    if match:
+        return match[0], match[1], False
+    return (other[0], other[1], True) if other else None
+
+
+def measured_traffic(args, kind="forward"):
+    """HBM bytes per k_forward (kind "forward") / k_expand_backup ("expand") launch from the
+    committed rocprofv3 PMC passes of this configuration (profiles/*_{kind}_traffic.json,
+    tools/profile_bench.sh): (bytes, source, stale) or None."""
+    m = _measured(args, f"*_{kind}_traffic.json")
+    return (m[0]["hbm_bytes_per_launch"], m[1], m[2]) if m else None
 
 
 def measured_mfma(args):
-    """k_forward's MFMA busy fraction from the committed rocprofv3 SQ/GRBM pass of this exact
+    """k_forward's MFMA busy fraction from the committed rocprofv3 SQ/GRBM pass of this
     configuration (profiles/*_forward_mfma.json, tools/profile_bench.sh); None otherwise."""
-    import glob
-    best = None
-    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_forward_mfma.json"))):
-        with open(f) as fh:
-            t = json.load(fh)
-        c = t.get("config", {})
-        if (c.get("envs"), c.get("sims"), c.get("hidden"), c.get("nblocks")) == (args.envs, args.sims, H, NB):
-            best = dict(t, source=os.path.relpath(f, REPO))
-    return best
+    m = _measured(args, "*_forward_mfma.json")
+    return dict(m[0], source=m[1], stale=m[2]) if m else None
 
 
 def arena_leg(net, games=1000, sims=25, seed=0, reps=3):
@@ -551,6 +574,7 @@ def main():
         "expansions_per_episode_batch": exps / args.steps,
         "game_groups": st["groups"],
         "forward_parts": st["forward_parts"],
+        "kernel_src_sha16": kernel_sources_sha16(),
         "capacity_use": {k: int(st[k]) for k in ("max_nodes", "node_cap", "max_edges", "edge_cap", "max_arena",
                                                  "arena_cap")},
     }
@@ -594,6 +618,7 @@ def main():
                    "peak": SPLIT_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": ach / SPLIT_PEAK_TFLOPS,
                    "traffic": tr[0] if tr else None,
                    "traffic_source": tr[1] if tr else None,
+                   "traffic_stale": tr[2] if tr else None,
                    "work_per_launch": f"{exp_per_launch:.0f} expansions x {PREDICT_FLOP} FLOP (f32)",
                    "peak_basis": f"f16 dense MFMA peak / {SPLIT_PRODUCTS:.2f}: every f32 product runs as hi*hi + "
                                  "hi*lo + lo*hi (+ (lo 2^-11)*lo outside the policy head) on fp16 planes with f32 "
@@ -604,20 +629,27 @@ def main():
                               "(tools/stream_bench.hip, profiles/r02_stream_sweep.txt, DESIGN.md section 6)"}
             mf = measured_mfma(args)
             if mf:
-                fwd["mfma_busy"] = {k: mf[k] for k in ("busy_frac", "formula", "source") if k in mf}
+                fwd["mfma_busy"] = {k: mf[k] for k in ("busy_frac", "formula", "source", "stale") if k in mf}
         if "expand_backup_select" in per and per["expand_backup_select"][1]:
-            # k_expand_backup (HBM): algorithmic bytes = 4*S_scan + 16*D + 4*V_new + 364 per
-            # expansion, from the engine's own counters of the last batch, per launch
-            scan_b = 4 * st["scanned"] + 16 * st["path_edges"] + 4 * st["vnew"] + 364 * st["expansions"]
-            b = scan_b / max(st["sims"] * st["groups"], 1)
+            # k_expand_backup (HBM): algorithmic bytes from the engine's own counters of the last batch,
+            # per launch.  SURVEY 8d's formula (4 S_scan + 16 D + 4 V_new + 364 per expansion) counts 4 B
+            # per UCB entry; what the kernel must read and write is 6 B per scanned entry (P f32 + the
+            # u16 edge slot), 16 B per visited entry's edge, 32 B per backed-up path edge (read +
+            # write), 10 B per new valid entry (its logit read, P and slot written), 364 B per expansion
+            launches = max(st["sims"] * st["groups"], 1)
+            survey_b = (4 * st["scanned"] + 16 * st["path_edges"] + 4 * st["vnew"] + 364 * st["expansions"]) / launches
+            b = (6 * st["scanned"] + 16 * st.get("scan_edges", 0) + 32 * st["path_edges"] + 10 * st["vnew"]
+                 + 364 * st["expansions"]) / launches
             ach = b / (per["expand_backup_select"][0] * 1e-3) / 1e9
             tr = measured_traffic(args, "expand")
             env = {"kernel": "k_expand_backup", "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS,
                    "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "traffic": tr[0] if tr else None,
-                   "traffic_source": tr[1] if tr else None,
-                   "work_per_launch": f"{b:.0f} algorithmic bytes = (4 x {st['scanned']} UCB entries scanned + "
-                                      f"16 x {st['path_edges']} path edges + 4 x {st['vnew']} new valid entries + "
-                                      f"364 x {st['expansions']} expansions) / {st['sims'] * st['groups']} launches"}
+                   "traffic_source": tr[1] if tr else None, "traffic_stale": tr[2] if tr else None,
+                   "work_per_launch": f"{b:.0f} algorithmic bytes = (6 x {st['scanned']} UCB entries scanned + "
+                                      f"16 x {st.get('scan_edges', 0)} edges gathered + 32 x {st['path_edges']} path "
+                                      f"edges + 10 x {st['vnew']} new valid entries + 364 x {st['expansions']} "
+                                      f"expansions) / {launches} launches",
+                   "survey_formula_bytes_per_launch": survey_b}
         if dom == "forward":
             out["roofline"], out["roofline_env"] = fwd, env
         else:

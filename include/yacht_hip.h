@@ -188,6 +188,10 @@ int yk_engine_kernel_times(yk_engine_t* eng, double* ms, int64_t* launches);
  * 7 new-node valid entries written, 8 search path edges backed up, 9 lock-step sims run,
  * 10-13 node / edge / arena / visit capacities, 14 game groups, 15 forward head parts (workgroups per 16-row tile) */
 int yk_engine_stats(yk_engine_t* eng, int64_t* out);
+/* Further counters of the last batch, summed over games; writes out[0 .. n-1] of:
+ * 0 edges gathered by the UCB scans (one 16-B edge per visited entry scanned, MCTS.py:122-133; with
+ *   stats 1 and 7-8 the expand's algorithmic bytes, bench.py roofline_env) */
+int yk_engine_counters(yk_engine_t* eng, int64_t* out, int n);
 /* Copies the last episode batch to HOST arrays (any may be NULL):
  *   states[n][max_moves][8]  canonical board of each example (Coach.py:57,61)
  *   info[n][max_moves][8]    temp, player, action, expansions-so-far, root Ns, n visited, status, 0

@@ -68,6 +68,7 @@ __device__ __forceinline__ uint32_t edge_kind(uint32_t tag) { return tag & 3u; }
 constexpr uint32_t PATH_DET = 0x80000000u;  // path entry low word: node id | PATH_DET when the
                                             // level's transition consumed no random draw
 
+constexpr int GST = 16;  // per-game counters (gstats)
 struct EngDev {
     int E, NCAP, HCAP, ECAP, M, VCAP;
     int e_lo, e_hi;        // the game group a per-game launch covers ([0, E) unless pipelined)
@@ -139,7 +140,8 @@ struct EngDev {
     float* rec_v;          // [R][max_exp]
     yk_state_t* rec_leaf;  // [R][max_exp] the expanded leaf (canonical state)
     // stats
-    uint64_t* gstats;      // [E][8]: expansions, scanned, path edges, vnew, max nodes, max edges, max arena, sims
+    uint64_t* gstats;      // [E][GST]: expansions, scanned, path edges, vnew, max nodes, max edges, max arena, sims,
+                           // edge gathers of the UCB scans
     uint32_t* err;         // [1] error bits
 };
 
@@ -404,7 +406,7 @@ __global__ void k_reset(EngDev d, int start_games, uint32_t env_base) {
         d.root_c[2 * t + 1] = make_uint4(0, 0, RV_OFF, 0);
     }
 #pragma unroll
-    for (int k = 0; k < 8; k++) d.gstats[(long)e * 8 + k] = 0;
+    for (int k = 0; k < GST; k++) d.gstats[(long)e * GST + k] = 0;
     if (!start_games) return;
     d.env_id[e] = env_base + (uint32_t)e;
     Stream rs{d.seed, d.env_id[e], 0};
@@ -532,7 +534,7 @@ __global__ __launch_bounds__(256) void k_move_begin(EngDev d, int move, int exte
 // (the caller then scans the whole set); `scanned` counts the entries read.
 __device__ __forceinline__ int root_scan(const EngDev& d, int t, int lane, uint32_t nv, const float* P,
                                          const uint16_t* S, const Edge* edges, int V, int nk, int ws, float sq,
-                                         float sqe, uint32_t& wtag, uint64_t& scanned) {
+                                         float sqe, uint32_t& wtag, uint64_t& scanned, uint64_t& gathered) {
     const uint16_t* oj = d.ro_j + (long)t * RO_K;
     const float* op = d.ro_p + (long)t * RO_K;
     const uint32_t* rv = d.rv + (long)t * RV_CAP;
@@ -593,6 +595,7 @@ __device__ __forceinline__ int root_scan(const EngDev& d, int t, int lane, uint3
     if (lane == 0 && first != ws) d.root_c[2 * t + 1].w = (uint32_t)first;
     if (!done && nk < V) {  // the stored order ended first: no unvisited entry among the top nk, or
         scanned += (uint64_t)nv + (uint64_t)walked;  // a band of equal u that may go on past them
+        gathered += (uint64_t)nv;                     // (one edge per visited-list entry)
         return -1;
     }
     if (lane == 0 && found && (ub > best || (ub == best && uj < bj))) {
@@ -605,6 +608,7 @@ __device__ __forceinline__ int root_scan(const EngDev& d, int t, int lane, uint3
     const uint64_t own = __ballot(mine == bj);  // the lane whose own candidate won holds its tag
     wtag = own ? __builtin_amdgcn_readlane(btag, (int)__builtin_ctzll(own)) : 0u;
     scanned += (uint64_t)nv + (uint64_t)walked;
+    gathered += (uint64_t)nv;
     return bj;
 }
 
@@ -629,7 +633,8 @@ __device__ __forceinline__ void select_game(const EngDev& d, int e, int lane, co
     const uint16_t* Sbase = d.arenaS + (long)t * d.AE;
     uint64_t* path = d.path + (long)e * MAXD;
     int depth = 0;
-    uint64_t scanned = 0;
+    uint64_t scanned = 0, gathered = 0;  // UCB entries read; their edges gathered (visited entries)
+    int ngl = 0;                          // this lane's edge gathers in full scans
     int leaf = 0;
     int known = -1;        // the node this level's state is, when the edge taken to it cached it
     uint32_t end_id = 0;   // id + 1 of a node the descent stops at
@@ -645,7 +650,8 @@ __device__ __forceinline__ void select_game(const EngDev& d, int e, int lane, co
             const uint32_t Ns = nodes[rc.x - 1].Ns;
             const float sq = (float)sqrt((double)Ns), sqe = (float)sqrt((double)Ns + 1e-8);
             pre_bj = __builtin_amdgcn_readfirstlane(root_scan(d, t, lane, rc1.z, Pbase + rc.y, Sbase + rc.y, edges,
-                                                              (int)rc.z, (int)rc.w, (int)rc1.w, sq, sqe, pre_tag, scanned));
+                                                              (int)rc.z, (int)rc.w, (int)rc1.w, sq, sqe, pre_tag, scanned,
+                                                              gathered));
             pre_tag = __builtin_amdgcn_readfirstlane(pre_tag);
             pre = pre_bj != -1;
         }
@@ -725,7 +731,10 @@ __device__ __forceinline__ void select_game(const EngDev& d, int e, int lane, co
                 Edge ev[4];
 #pragma unroll
                 for (int t = 0; t < 4; t++)
-                    if (j0 + t < V && sv[t]) ev[t] = edges[sv[t] - 1];
+                    if (j0 + t < V && sv[t]) {
+                        ev[t] = edges[sv[t] - 1];
+                        ngl++;
+                    }
                 if (j0 + 256 < V) {
                     p4 = *reinterpret_cast<const float4*>(P + j0 + 256);
                     s4 = *reinterpret_cast<const ushort4*>(S + j0 + 256);
@@ -786,6 +795,7 @@ __device__ __forceinline__ void select_game(const EngDev& d, int e, int lane, co
         }
         s = canonical(s, np);  // MCTS.py:150
     }
+    gathered += (uint64_t)xlane_sum(ngl);
     if (lane == 0) {
         d.leaf_flag[e] = (uint8_t)(leaf ? (t < d.E ? 1 : 2) : 0);  // which net predicts it (dual trees)
         d.path_len[e] = (uint8_t)depth;
@@ -793,9 +803,10 @@ __device__ __forceinline__ void select_game(const EngDev& d, int e, int lane, co
         d.res_v[e] = res.v;
         d.res_t[e] = res.t;
         ctr_arr[e] = rs.ctr;
-        d.gstats[(long)e * 8 + 1] += scanned;
-        d.gstats[(long)e * 8 + 2] += (uint64_t)depth;
-        d.gstats[(long)e * 8 + 7] += 1;
+        d.gstats[(long)e * GST + 1] += scanned;
+        d.gstats[(long)e * GST + 2] += (uint64_t)depth;
+        d.gstats[(long)e * GST + 7] += 1;
+        d.gstats[(long)e * GST + 8] += gathered;
     }
 }
 
@@ -844,7 +855,7 @@ __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int l
         float4 q[PW_GMAX];
         float qt[PW_TMAX];
         float v, mx = 0.f, lse = 0.f;
-        const int pidx = (int)d.gstats[(long)e * 8 + 0];
+        const int pidx = (int)d.gstats[(long)e * GST + 0];
         // record_predictions samples games without changing the path: the production prior
         // below is what gets recorded (after masking, i.e. exactly what np.sum / P see)
         const bool rec = d.rec_pred && (e % d.rec_stride) == 0 && pidx < d.max_exp;
@@ -1029,7 +1040,7 @@ __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int l
             if (lane == 0) {
                 d.node_count[g * d.T + t] = nid + 1;
                 d.arena_top[t] = off + (uint32_t)VP;
-                uint64_t* gs = d.gstats + (long)e * 8;
+                uint64_t* gs = d.gstats + (long)e * GST;
                 gs[0] += 1;
                 gs[3] += (uint64_t)V;
                 if (nid + 1 > gs[4]) gs[4] = nid + 1;
@@ -1084,7 +1095,7 @@ __device__ __forceinline__ void expand_backup_game(const EngDev& d, int e, int l
         }
         if (lane == 0) {
             d.edge_count[g * d.T + t] = ne1;
-            uint64_t* gs = d.gstats + (long)e * 8;
+            uint64_t* gs = d.gstats + (long)e * GST;
             if (ne1 > gs[5]) gs[5] = ne1;
             // a new edge at level 0 (the move's root): into the root's visited list (root_scan)
             if (is_new && eid < (uint32_t)d.ECAP && eid < 65535u) {
@@ -1372,7 +1383,7 @@ __global__ __launch_bounds__(256) void k_move_end(EngDev d, int move) {
     info[0] = temp;
     info[1] = player;
     info[2] = action;
-    info[3] = (int32_t)d.gstats[(long)e * 8 + 0];
+    info[3] = (int32_t)d.gstats[(long)e * GST + 0];
     info[4] = (int32_t)root_ns;
     info[5] = nvis;
     info[6] = st;
@@ -1741,7 +1752,7 @@ constexpr int YK_FPARTS_MAX = 4;
     A(d.final_tot, 2 * E);
     A(d.seat, E);
     A(d.idle, E);
-    A(d.gstats, E * 8);
+    A(d.gstats, E * GST);
     A(d.err, 1);
     A(eng->done_count, 1);
     A(eng->mcts_env, E);
@@ -1972,7 +1983,7 @@ int yk_engine_kernel_times(yk_engine_t* eng, double* ms, int64_t* launches) {
 int yk_engine_stats(yk_engine_t* eng, int64_t* out) {
     if (!eng || !out) return YK_ERR_ARG;
     EngDev& d = eng->d;
-    std::vector<uint64_t> gs((size_t)d.E * 8);
+    std::vector<uint64_t> gs((size_t)d.E * GST);
     std::vector<int32_t> nm(d.E);
     uint32_t err = 0;
     YK_HIP(hipDeviceSynchronize());
@@ -1981,7 +1992,7 @@ int yk_engine_stats(yk_engine_t* eng, int64_t* out) {
     YK_HIP(hipMemcpy(&err, d.err, sizeof(uint32_t), hipMemcpyDeviceToHost));
     for (int i = 0; i < 16; i++) out[i] = 0;
     for (int e = 0; e < d.E; e++) {
-        const uint64_t* g = &gs[(size_t)e * 8];
+        const uint64_t* g = &gs[(size_t)e * GST];
         out[0] += (int64_t)g[0];
         out[1] += (int64_t)g[1];
         out[2] = std::max<int64_t>(out[2], nm[e]);
@@ -1999,6 +2010,18 @@ int yk_engine_stats(yk_engine_t* eng, int64_t* out) {
     out[13] = d.VCAP;
     out[14] = eng->ngroups;
     out[15] = d.fparts;
+    return YK_OK;
+}
+
+int yk_engine_counters(yk_engine_t* eng, int64_t* out, int n) {
+    if (!eng || !out || n < 0) return YK_ERR_ARG;
+    EngDev& d = eng->d;
+    std::vector<uint64_t> gs((size_t)d.E * GST);
+    YK_HIP(hipDeviceSynchronize());
+    YK_HIP(hipMemcpy(gs.data(), d.gstats, sizeof(uint64_t) * gs.size(), hipMemcpyDeviceToHost));
+    int64_t c[1] = {0};
+    for (int e = 0; e < d.E; e++) c[0] += (int64_t)gs[(size_t)e * GST + 8];
+    for (int i = 0; i < n; i++) out[i] = i < 1 ? c[i] : 0;
     return YK_OK;
 }
 
@@ -2056,9 +2079,9 @@ int yk_engine_predictions(yk_engine_t* eng, float* pi, float* v, yk_state_t* lea
     if (v) YK_HIP(hipMemcpy(v, d.rec_v, sizeof(float) * R * X, hipMemcpyDeviceToHost));
     if (leaves) YK_HIP(hipMemcpy(leaves, d.rec_leaf, sizeof(yk_state_t) * R * X, hipMemcpyDeviceToHost));
     if (count) {
-        std::vector<uint64_t> gs((size_t)d.E * 8);
+        std::vector<uint64_t> gs((size_t)d.E * GST);
         YK_HIP(hipMemcpy(gs.data(), d.gstats, sizeof(uint64_t) * gs.size(), hipMemcpyDeviceToHost));
-        for (size_t r = 0; r < R; r++) count[r] = (int32_t)gs[r * d.rec_stride * 8];  // > max_expansions: truncated
+        for (size_t r = 0; r < R; r++) count[r] = (int32_t)gs[r * d.rec_stride * GST];  // > max_expansions: truncated
     }
     return YK_OK;
 }

@@ -213,11 +213,11 @@ __device__ __forceinline__ void layernorm(float (&x)[VPL], const float* g, const
 // v_cvt_pk_f16_f32) for even VPL: the same operations per element as silu / layernorm /
 // put_planes, except that each lane's partial sums pair its values ((x0 + x2) + (x1 + x3)).
 // The trunk's LayerNorm phases are VALU-bound and on the forward's critical path.
-#ifdef XP_CONTRACT
+// The library builds with -ffp-contract=off (the search's f32 arithmetic rounds after every
+// operation, as numpy does); the forward's LayerNorm row passes - VALU-bound and on every layer's
+// critical path - contract their multiply-adds into v_pk_fma_f32 (one rounding instead of two: no
+// less accurate than torch's own LayerNorm kernels, which fuse them too).  Scoped per function.
 #define YK_ROW_CONTRACT _Pragma("clang fp contract(fast)")
-#else
-#define YK_ROW_CONTRACT
-#endif
 typedef float f2v __attribute__((ext_vector_type(2)));
 typedef _Float16 h2v __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f2v ld2(const float* p) { return *reinterpret_cast<const f2v*>(p); }
@@ -555,9 +555,6 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
         if (!amask) return;
     }
     const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-#ifdef XP_PRIO
-    if (NW == 8 && wave >= 4) __builtin_amdgcn_s_setprio(1);
-#endif
     // owns columns of the H-wide layers: every wave when NACT == NW (hidden >= 128), as a
     // compile-time true - a branch around the weight ring would make the wait counters merge at its
     // join, and the resulting vmcnt(0) drains the ring's in-flight refills of the next layer

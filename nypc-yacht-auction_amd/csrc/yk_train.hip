@@ -6,14 +6,13 @@
 // (NNet.py:143-148) -> backward -> [caller all-reduces the gradient buffer for DDP] ->
 // clip_grad_norm_(5.0) (NNet.py:152-153) -> AdamW (NNet.py:109-110).
 //
-// The dense layers are plain GEMMs and go to rocBLAS (f32).  Everything between them is
+// The dense layers are plain GEMMs on a hand-written f32 MFMA kernel (k_sgemm:
+// v_mfma_f32_16x16x4_f32, exact f32 products and f32 accumulation).  Everything between them is
 // hand-written and fused per row: bias + SiLU + LayerNorm + dropout + residual forward, the
 // matching backward (LayerNorm input gradient from the saved statistics), the loss and its
 // gradients, column reductions for bias / LayerNorm parameter gradients, the global gradient
 // norm and the AdamW update.  Parameters, gradients and the Adam moments are single flat
 // buffers in torch state_dict order, so the gradient buffer is one RCCL all-reduce.
-#include <rocblas/rocblas.h>
-
 #include <cmath>
 #include <vector>
 
@@ -26,6 +25,7 @@ using namespace yk;
 namespace {
 
 constexpr int TPB = 256;
+typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
 __device__ __forceinline__ float silu_f(float x) { return x * sigm(x); }
@@ -453,7 +453,6 @@ __global__ void k_adamw(float* p, float* g, float* m, float* v, long n, const do
 struct yk_trainer {
     int H = 0, NB = 0, Bmax = 0;
     yk_train_config_t cfg{};
-    rocblas_handle blas = nullptr;
     float *P = nullptr, *G = nullptr, *M = nullptr, *V = nullptr;
     long nparams = 0;
     std::vector<long> off;  // tensor offsets, state_dict order
@@ -506,14 +505,78 @@ int talloc(yk_trainer* t, T** p, size_t count) {
     return YK_OK;
 }
 
-// row-major C[M][N] = op(A)[M][K] . op(B)[K][N] (+ beta C) on rocBLAS's column-major API
-int gemm_rm(yk_trainer* t, bool ta, bool tb, int M, int N, int K, const float* A, int lda, const float* B, int ldb,
+// row-major C[M][N] = op(A)[M][K] . op(B)[K][N] (+ beta C), op = transpose when ta / tb (A stored
+// [K][M], B stored [N][K]).  64 x 64 output tiles per 256-thread workgroup, each wave a 32 x 32
+// quarter as 2 x 2 blocks of v_mfma_f32_16x16x4_f32 (f32 operands: exact products, f32
+// accumulation, the reference's CPU arithmetic up to summation order); K staged through LDS 16
+// deep, the global reads coalesced along whichever dimension is contiguous in memory.
+constexpr int GT = 64, GK = 16;
+__global__ __launch_bounds__(256) void k_sgemm(int ta, int tb, int M, int N, int K, const float* __restrict__ A, int lda,
+                                               const float* __restrict__ B, int ldb, float* __restrict__ C, int ldc,
+                                               float beta) {
+    __shared__ float As[GK][GT + 4];  // [k][m]
+    __shared__ float Bs[GK][GT + 4];  // [k][n]
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int m0 = blockIdx.y * GT, n0 = blockIdx.x * GT;
+    const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
+    floatx4 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+#pragma unroll
+        for (int j = 0; j < 2; j++) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int k0 = 0; k0 < K; k0 += GK) {
+        float av[4], bv[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int e = tid + 256 * i;
+            const int am = ta ? (e & 63) : (e >> 4), ak = ta ? (e >> 6) : (e & 15);
+            const int gm = m0 + am, gk = k0 + ak;
+            av[i] = (gm < M && gk < K) ? (ta ? A[(long)gk * lda + gm] : A[(long)gm * lda + gk]) : 0.f;
+            const int bn = tb ? (e >> 4) : (e & 63), bk = tb ? (e & 15) : (e >> 6);
+            const int gn = n0 + bn, gkb = k0 + bk;
+            bv[i] = (gn < N && gkb < K) ? (tb ? B[(long)gn * ldb + gkb] : B[(long)gkb * ldb + gn]) : 0.f;
+        }
+        __syncthreads();  // the previous chunk's reads are done
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int e = tid + 256 * i;
+            As[ta ? (e >> 6) : (e & 15)][ta ? (e & 63) : (e >> 4)] = av[i];
+            Bs[tb ? (e & 15) : (e >> 6)][tb ? (e >> 4) : (e & 63)] = bv[i];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int kk = 0; kk < GK; kk += 4) {
+            const int k = kk + (lane >> 4);
+            float a[2], b[2];
+#pragma unroll
+            for (int i = 0; i < 2; i++) a[i] = As[k][wm + 16 * i + (lane & 15)];
+#pragma unroll
+            for (int j = 0; j < 2; j++) b[j] = Bs[k][wn + 16 * j + (lane & 15)];
+#pragma unroll
+            for (int i = 0; i < 2; i++)
+#pragma unroll
+                for (int j = 0; j < 2; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[j], acc[i][j], 0, 0, 0);
+        }
+    }
+    // block (i, j): lane l holds rows 4 (l >> 4) + r, column l & 15
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+#pragma unroll
+        for (int j = 0; j < 2; j++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int gm = m0 + wm + 16 * i + 4 * (lane >> 4) + r, gn = n0 + wn + 16 * j + (lane & 15);
+                if (gm < M && gn < N) {
+                    float* c = C + (long)gm * ldc + gn;
+                    *c = beta != 0.f ? acc[i][j][r] + beta * *c : acc[i][j][r];
+                }
+            }
+}
+int gemm_rm(hipStream_t s, bool ta, bool tb, int M, int N, int K, const float* A, int lda, const float* B, int ldb,
             float* C, int ldc, float beta) {
-    const float one = 1.0f;
-    const rocblas_status st =
-        rocblas_sgemm(t->blas, tb ? rocblas_operation_transpose : rocblas_operation_none,
-                      ta ? rocblas_operation_transpose : rocblas_operation_none, N, M, K, &one, B, ldb, A, lda, &beta, C, ldc);
-    return st == rocblas_status_success ? YK_OK : YK_ERR_HIP;
+    hipLaunchKernelGGL(k_sgemm, dim3((unsigned)((N + GT - 1) / GT), (unsigned)((M + GT - 1) / GT)), dim3(256), 0, s,
+                       ta ? 1 : 0, tb ? 1 : 0, M, N, K, A, lda, B, ldb, C, ldc, beta);
+    return hipGetLastError() == hipSuccess ? YK_OK : YK_ERR_HIP;
 }
 
 template <int VPL>
@@ -531,17 +594,17 @@ int step_impl(yk_trainer* t, const yk_state_t* states, const int32_t* targets, c
                        t->vt, B);
     YK_LAUNCHED();
     // ---- forward
-    if ((rc = gemm_rm(t, false, true, B, H, FEAT, t->X, FEAT, Pt(T_WIN), FEAT, t->Z0, H, 0.f))) return rc;
+    if ((rc = gemm_rm(s, false, true, B, H, FEAT, t->X, FEAT, Pt(T_WIN), FEAT, t->Z0, H, 0.f))) return rc;
     hipLaunchKernelGGL(k_inp_fwd<VPL>, rows, wave4, 0, s, t->Z0, Pt(T_BIN), Pt(T_GIN), Pt(T_BEIN), t->mu0, t->rs0,
                        t->mask0, t->Hs[0], B, p, seed, step, t->row_base);
     YK_LAUNCHED();
     for (int b = 0; b < NB; b++) {
-        if ((rc = gemm_rm(t, false, true, B, H, H, t->Hs[b], H, Pt(t_blk(b, 0)), H, t->U1[b], H, 0.f))) return rc;
+        if ((rc = gemm_rm(s, false, true, B, H, H, t->Hs[b], H, Pt(t_blk(b, 0)), H, t->U1[b], H, 0.f))) return rc;
         hipLaunchKernelGGL(k_blk_fwd<VPL>, rows, wave4, 0, s, t->U1[b], Pt(t_blk(b, 1)), Pt(t_blk(b, 2)), Pt(t_blk(b, 3)),
                            t->mu1[b], t->rs1[b], t->mask1[b], t->R1[b], (const float*)nullptr, B, p, seed, step, 1 + b,
                            t->row_base);
         YK_LAUNCHED();
-        if ((rc = gemm_rm(t, false, true, B, H, H, t->R1[b], H, Pt(t_blk(b, 4)), H, t->U2[b], H, 0.f))) return rc;
+        if ((rc = gemm_rm(s, false, true, B, H, H, t->R1[b], H, Pt(t_blk(b, 4)), H, t->U2[b], H, 0.f))) return rc;
         hipLaunchKernelGGL(k_blk_fwd<VPL>, rows, wave4, 0, s, t->U2[b], Pt(t_blk(b, 5)), Pt(t_blk(b, 6)), Pt(t_blk(b, 7)),
                            t->mu2[b], t->rs2[b], (uint8_t*)nullptr, t->Hs[b + 1], t->Hs[b], B, p, seed, step, -1,
                            t->row_base);
@@ -551,17 +614,17 @@ int step_impl(yk_trainer* t, const yk_state_t* states, const int32_t* targets, c
     hipLaunchKernelGGL(k_heads_fwd<VPL>, rows, wave4, 0, s, Hh, Pt(t_head(NB, 0)), Pt(t_head(NB, 1)), Pt(t_head(NB, 4)),
                        Pt(t_head(NB, 5)), t->Api, t->Av, t->mup, t->rsp, t->muv, t->rsv, B);
     YK_LAUNCHED();
-    if ((rc = gemm_rm(t, false, true, B, A, H, t->Api, H, Pt(t_head(NB, 2)), H, t->logits, A, 0.f))) return rc;
-    if ((rc = gemm_rm(t, false, true, B, 128, H, t->Av, H, Pt(t_head(NB, 6)), H, t->Zv1, 128, 0.f))) return rc;
+    if ((rc = gemm_rm(s, false, true, B, A, H, t->Api, H, Pt(t_head(NB, 2)), H, t->logits, A, 0.f))) return rc;
+    if ((rc = gemm_rm(s, false, true, B, 128, H, t->Av, H, Pt(t_head(NB, 6)), H, t->Zv1, 128, 0.f))) return rc;
     hipLaunchKernelGGL(k_loss, dim3(B), dim3(LOSS_T), 0, s, t->logits, Pt(t_head(NB, 3)), t->Zv1, Pt(t_head(NB, 7)),
                        Pt(t_head(NB, 8)), Pt(t_head(NB, 9)), t->tgt, t->vt, t->dlogits, t->dZv1, t->dzv2, t->v2prod,
                        t->vout, t->lrow, B, A, t->cfg.vloss_weight);
     YK_LAUNCHED();
     // ---- backward: heads (bias / LayerNorm gradients are column sums, taken at the end)
-    if ((rc = gemm_rm(t, true, false, A, H, B, t->dlogits, A, t->Api, H, Gt(t_head(NB, 2)), H, 0.f))) return rc;
-    if ((rc = gemm_rm(t, true, false, 128, H, B, t->dZv1, 128, t->Av, H, Gt(t_head(NB, 6)), H, 0.f))) return rc;
-    if ((rc = gemm_rm(t, false, false, B, H, A, t->dlogits, A, Pt(t_head(NB, 2)), H, t->dA, H, 0.f))) return rc;
-    if ((rc = gemm_rm(t, false, false, B, H, 128, t->dZv1, 128, Pt(t_head(NB, 6)), H, t->dAv, H, 0.f))) return rc;
+    if ((rc = gemm_rm(s, true, false, A, H, B, t->dlogits, A, t->Api, H, Gt(t_head(NB, 2)), H, 0.f))) return rc;
+    if ((rc = gemm_rm(s, true, false, 128, H, B, t->dZv1, 128, t->Av, H, Gt(t_head(NB, 6)), H, 0.f))) return rc;
+    if ((rc = gemm_rm(s, false, false, B, H, A, t->dlogits, A, Pt(t_head(NB, 2)), H, t->dA, H, 0.f))) return rc;
+    if ((rc = gemm_rm(s, false, false, B, H, 128, t->dZv1, 128, Pt(t_head(NB, 6)), H, t->dAv, H, 0.f))) return rc;
     hipLaunchKernelGGL(k_heads_bwd<VPL>, rows, wave4, 0, s, Hh, Pt(t_head(NB, 0)), Pt(t_head(NB, 1)), Pt(t_head(NB, 4)),
                        Pt(t_head(NB, 5)), t->mup, t->rsp, t->muv, t->rsv, t->dA, t->dAv, t->dH, t->rgp, t->rbp, t->rgv,
                        t->rbv, B);
@@ -571,20 +634,20 @@ int step_impl(yk_trainer* t, const yk_state_t* states, const int32_t* targets, c
         hipLaunchKernelGGL(k_blk_bwd<VPL>, rows, wave4, 0, s, t->dH, (const uint8_t*)nullptr, 0.f, t->U2[b],
                            Pt(t_blk(b, 6)), t->mu2[b], t->rs2[b], t->dU2[b], t->rg2[b], t->rb2[b], B);
         YK_LAUNCHED();
-            if ((rc = gemm_rm(t, true, false, H, H, B, t->dU2[b], H, t->R1[b], H, Gt(t_blk(b, 4)), H, 0.f))) return rc;
-        if ((rc = gemm_rm(t, false, false, B, H, H, t->dU2[b], H, Pt(t_blk(b, 4)), H, t->dT, H, 0.f))) return rc;  // dR1
+            if ((rc = gemm_rm(s, true, false, H, H, B, t->dU2[b], H, t->R1[b], H, Gt(t_blk(b, 4)), H, 0.f))) return rc;
+        if ((rc = gemm_rm(s, false, false, B, H, H, t->dU2[b], H, Pt(t_blk(b, 4)), H, t->dT, H, 0.f))) return rc;  // dR1
         hipLaunchKernelGGL(k_blk_bwd<VPL>, rows, wave4, 0, s, t->dT, t->mask1[b], p, t->U1[b], Pt(t_blk(b, 2)), t->mu1[b],
                            t->rs1[b], t->dU1[b], t->rg1[b], t->rb1[b], B);
         YK_LAUNCHED();
-            if ((rc = gemm_rm(t, true, false, H, H, B, t->dU1[b], H, t->Hs[b], H, Gt(t_blk(b, 0)), H, 0.f))) return rc;
+            if ((rc = gemm_rm(s, true, false, H, H, B, t->dU1[b], H, t->Hs[b], H, Gt(t_blk(b, 0)), H, 0.f))) return rc;
         // dH_b = dH_{b+1} (residual) + dU1 . W1
-        if ((rc = gemm_rm(t, false, false, B, H, H, t->dU1[b], H, Pt(t_blk(b, 0)), H, t->dH, H, 1.f))) return rc;
+        if ((rc = gemm_rm(s, false, false, B, H, H, t->dU1[b], H, Pt(t_blk(b, 0)), H, t->dH, H, 1.f))) return rc;
     }
     // ---- input layer
     hipLaunchKernelGGL(k_inp_bwd<VPL>, rows, wave4, 0, s, t->dH, t->mask0, p, t->Z0, Pt(T_GIN), Pt(T_BEIN), t->mu0,
                        t->rs0, t->dZ0, t->rg0, t->rb0, B);
     YK_LAUNCHED();
-    if ((rc = gemm_rm(t, true, false, H, FEAT, B, t->dZ0, H, t->X, FEAT, Gt(T_WIN), FEAT, 0.f))) return rc;
+    if ((rc = gemm_rm(s, true, false, H, FEAT, B, t->dZ0, H, t->X, FEAT, Gt(T_WIN), FEAT, 0.f))) return rc;
     // ---- every bias / LayerNorm gradient: one launch of column sums
     hipLaunchKernelGGL(k_colsums, dim3(t->ntiles), dim3(256), 0, s, t->jobs, t->tiles, B);
     YK_LAUNCHED();
@@ -708,7 +771,6 @@ int yk_trainer_create(yk_trainer_t** out, int H, int NB, const float* const* par
         (void)hipMemcpy(t->tiles, tiles.data(), sizeof(int2) * tiles.size(), hipMemcpyHostToDevice);
     }
 #undef TA
-    if (rc == YK_OK && !cfg->amp && rocblas_create_handle(&t->blas) != rocblas_status_success) rc = YK_ERR_HIP;
     if (rc != YK_OK) {
         yk_trainer_destroy(t);
         return rc;
@@ -741,7 +803,6 @@ int yk_trainer_create(yk_trainer_t** out, int H, int NB, const float* const* par
 
 int yk_trainer_destroy(yk_trainer_t* t) {
     if (!t) return YK_OK;
-    if (t->blas) rocblas_destroy_handle(t->blas);
     yk::amp_destroy(t->amp);
     for (void* p : t->allocs) (void)hipFree(p);
     delete t;
@@ -761,7 +822,6 @@ static int backward_impl(yk_trainer_t* t, const yk_state_t* states, const int32_
     if (t->amp)
         return yk::amp_backward(t->amp, states, targets, values, batch_idx, batch, t->cfg.dropout, t->cfg.seed, t->step,
                                 t->row_base, t->cfg.vloss_weight, t->lrow, t->lsum, fuse_norm, s);
-    if (rocblas_set_stream(t->blas, s) != rocblas_status_success) return YK_ERR_HIP;
     switch (t->H) {
         case 64: return step_impl<1>(t, states, targets, values, batch_idx, batch, s);
         case 128: return step_impl<2>(t, states, targets, values, batch_idx, batch, s);

@@ -80,7 +80,7 @@ struct AmpDev {
     const float4 *win_f, *w1f, *w2f, *w1t, *w2t, *wpif, *wpit, *wv1f, *wv1t;
     _Float16 *xT, *hT, *r1T, *apiT, *avT, *api_rm, *av_rm;
     float *z0, *u1, *u2, *hF, *stats;
-    float *logits, *zv1, *lse;
+    float *logits, *zv1;
     float2* mlq;
     uint8_t* masks;                       // [1 + NB][Bmax][H / 4] the step's dropout keep bits (k_amp_masks)
     _Float16 *dz1_rm, *dz1T, *dlT, *dz0T, *du1T, *du2T;
@@ -1366,19 +1366,23 @@ __global__ __launch_bounds__(256) void k_amp_update(const UpdJob* __restrict__ j
         *sc_next = n;
     }
     const float inv = 1.0f / s0.scale;
-    if (!isfinite(total)) {  // step skipped: parameters and their fp16 copies unchanged; the gradient
-        // buffer is left unscaled as torch's unscale_ leaves p.grad (not clipped: its coefficient is nan)
+    if (!isfinite(total)) {  // step skipped: parameters and their fp16 copies unchanged.  The gradient
+        // buffer ends as p.grad does in torch: unscale_ (x 1/scale), then clip_grad_norm_'s multiply by
+        // its clamped coefficient max_norm / (total_norm + 1e-6) - 0 for an infinite norm (finite entries
+        // -> +-0, infinite ones -> nan), nan for a nan norm
+        float cf = max_norm / ((float)sqrt(total) + 1e-6f);
+        cf = cf > 1.0f ? 1.0f : cf;
         const UpdItem it = items[blockIdx.x];
         const UpdJob jb = jobs[it.job];
         const int t = threadIdx.x;
         if (!jb.dstN) {
             for (int i = 0; i < 4; i++)
-                if (4 * t + i < it.k0) jb.Gm[(long)it.n0 + 4 * t + i] *= inv;
+                if (4 * t + i < it.k0) jb.Gm[(long)it.n0 + 4 * t + i] = (jb.Gm[(long)it.n0 + 4 * t + i] * inv) * cf;
         } else {
             const int n = it.n0 + (t >> 3);
             for (int i = 0; i < 4; i++) {
                 const int k = it.k0 + (t & 7) * 4 + i;
-                if (n < jb.N && k < jb.K) jb.Gm[(long)n * jb.K + k] *= inv;
+                if (n < jb.N && k < jb.K) jb.Gm[(long)n * jb.K + k] = (jb.Gm[(long)n * jb.K + k] * inv) * cf;
             }
         }
         return;
@@ -1580,7 +1584,6 @@ int amp_create(AmpTrain** out, int H, int NB, int Bmax, float* P, float* G, cons
     AA(d.stats, (size_t)(2 + 2 * NB) * 2 * Bm);
     AA(d.logits, Bm * LDL);
     AA(d.zv1, Bm * VH);
-    AA(d.lse, Bm);
     AA(d.mlq, (size_t)HQ * Bm);
     AA(d.masks, (size_t)(1 + NB) * Bm * (H / 4));
     AA(d.dz1_rm, Bm * VH);

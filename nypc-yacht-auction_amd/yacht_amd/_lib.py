@@ -85,6 +85,7 @@ SIGNATURES = {
     "yk_arena_results": [P, P, P, P, P, P, P],
     "yk_engine_set_opponent_net": [P, P],
     "yk_engine_stats": [P, P],
+    "yk_engine_counters": [P, P, I],
     "yk_engine_profile": [P, I],
     "yk_engine_kernel_times": [P, P, P],
     "yk_engine_records": [P, P, P, P, P, P, P, P, P, P],
@@ -99,6 +100,7 @@ SIGNATURES = {
 _RESTYPE = {"yk_version": C.c_char_p, "yk_rng_draw64": C.c_uint64, "yk_engine_record_bytes": C.c_int64,
             "yk_trainer_step_count": C.c_int64}
 
+_NEWER = {"yk_engine_counters"}  # added in round 5 (tools/ab_bench.sh baselines may predate them)
 _lib = None
 
 
@@ -117,6 +119,8 @@ def lib():
                               "(or __graft_entry__.build()); there is no CPU fallback")
         lib_ = C.CDLL(LIB_PATH)
         for name, args in SIGNATURES.items():
+            if os.environ.get("YK_LIB_PATH") and name in _NEWER and not hasattr(lib_, name):
+                continue  # an older diagnostic baseline (A/B): entry points added since are absent
             fn = getattr(lib_, name)
             fn.argtypes = args
             fn.restype = _RESTYPE.get(name, C.c_int)

@@ -101,11 +101,17 @@ class SelfPlayEngine:
     STAT_NAMES = ("expansions", "scanned", "moves", "errors", "max_nodes", "max_edges", "max_arena", "vnew",
                   "path_edges", "sims", "node_cap", "edge_cap", "arena_cap", "visit_cap", "groups",
                   "forward_parts")
+    COUNTER_NAMES = ("scan_edges",)  # yk_engine_counters
 
     def stats(self) -> dict:
         out = np.zeros(16, dtype=np.int64)
         call("yk_engine_stats", self.handle, out.ctypes.data)
-        return {k: int(out[i]) for i, k in enumerate(self.STAT_NAMES)}
+        st = {k: int(out[i]) for i, k in enumerate(self.STAT_NAMES)}
+        more = np.zeros(len(self.COUNTER_NAMES), dtype=np.int64)
+        if hasattr(lib(), "yk_engine_counters"):  # (absent only from older diagnostic baselines)
+            call("yk_engine_counters", self.handle, more.ctypes.data, len(more))
+        st.update({k: int(more[i]) for i, k in enumerate(self.COUNTER_NAMES)})
+        return st
 
     def records(self) -> dict:
         E, M = self.n_envs, self.max_moves

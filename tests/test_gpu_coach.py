@@ -158,6 +158,12 @@ def _coach_worker(rank, world, port, ckdir, out):
     ws.nnet.load_state_dict(coach.pnet.nnet.state_dict())
     ws.train([shard], verbose=False)
     out[f"ps{rank}"] = {k: v.numpy().copy() for k, v in ws.nnet.state_dict().items()}
+    # the same split in the default mode under args.cuda (autocast + GradScaler): row-offset
+    # backward, the all-reduce, the unfused apply with the GradScaler state
+    wa = NNetWrapper(game, dotdict(args, ddp_batch="split", amp=True))
+    wa.nnet.load_state_dict(coach.pnet.nnet.state_dict())
+    wa.train([shard], verbose=False)
+    out[f"pa{rank}"] = ({k: v.numpy().copy() for k, v in wa.nnet.state_dict().items()}, wa._trainer().amp_state())
     # DDP weak scaling: every rank its own batch_size rows (a global minibatch of 2 x batch_size)
     wk = NNetWrapper(game, dotdict(args, ddp_batch="per_rank"))
     wk.nnet.load_state_dict(coach.pnet.nnet.state_dict())
@@ -215,6 +221,22 @@ def test_coach_iteration_two_ranks_sharing_gpu0(Y, tmp_path):
     # 2 lr on a summation-order change; everything else agrees to f32 rounding
     assert np.linalg.norm(a - b) / np.linalg.norm(b) < 1e-4
     assert (np.abs(a - b) > 1e-5).mean() < 1e-3
+    # AMP split: both ranks bit-identical with the same GradScaler state; against the single-process
+    # AMP train, each rank's half-batch gradient is rounded to fp16 before the f32 all-reduce, so a
+    # step GradScaler skips in one run (a half batch's fp16 gradient overflowing at 65536) may be
+    # taken in the other: at most one step apart, and the parameters' updates close
+    pa0, pa1 = out["pa0"], out["pa1"]
+    assert all(np.array_equal(pa0[0][k], pa1[0][k]) for k in pa0[0]) and pa0[1] == pa1[1]
+    wam = NNetWrapper(game, dotdict(args, amp=True))
+    wam.nnet.load_state_dict(net0.nnet.state_dict())
+    wam.train([single], verbose=False)
+    st1 = wam._trainer().amp_state()
+    assert wam._trainer().amp and abs(pa0[1]["steps"] - st1["steps"]) <= 1 and st1["steps"] > 0
+    a = np.concatenate([pa0[0][k].reshape(-1) for k in pa0[0]]).astype(np.float64)
+    b = np.concatenate([wam.nnet.state_dict()[k].numpy().reshape(-1) for k in pa0[0]]).astype(np.float64)
+    p_init = np.concatenate([net0.nnet.state_dict()[k].numpy().reshape(-1) for k in pa0[0]]).astype(np.float64)
+    tol = 0.02 if pa0[1]["steps"] == st1["steps"] else 0.3
+    assert np.linalg.norm(a - b) / np.linalg.norm(b - p_init) < tol
     # per_rank: the single-process train at batch 2 x batch_size, in half the steps
     pr0, pr1 = out["pr0"], out["pr1"]
     assert all(np.array_equal(pr0[0][k], pr1[0][k]) for k in pr0[0])

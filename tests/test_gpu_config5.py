@@ -12,10 +12,13 @@ dropout 0.3, numItersForTrainExamplesHistory 5, arenaCompare 10.  Checked:
   (replay.host_examples) of that iteration's record image, trimmed to the maxlenOfQueue deque's
   newest 200,000 examples (Coach.py:86-90), and the second iteration trains on both entries
   (Coach.py:99-111);
-* iteration 1's first 3 amp steps (its starting weights, its first epoch's permutation of the
-  pooled examples) against torch autocast('cuda') + GradScaler('cuda') on the same minibatches,
-  within test_amp_steps_vs_torch_autocast_gradscaler's tolerance - with dropout 0 for that
-  comparison, since torch draws its dropout masks from its own generator;
+* the trainer Coach.learn itself ran: its first 3 amp steps (dropout 0.3) are recorded as they
+  happen (minibatch indices, losses, parameters, GradScaler state), a standalone Trainer given the
+  same examples, indices, seed and dropout reproduces them bit for bit, and those recorded steps
+  are held against torch autocast('cuda') + GradScaler('cuda') on the same minibatches WITH THE
+  SAME DROPOUT MASKS (helpers.dropout_keep_np restates the trainer's Philox keep bits; torch's
+  nn.Dropout modules replaced by those fixed masks x 1/(1-p)), within
+  test_amp_steps_vs_torch_autocast_gradscaler's tolerance;
 * each iteration's gate tally equals a fresh, unsharded GatingArena run on the same two nets and
   env ids (Coach.py:117-139)."""
 import os
@@ -24,7 +27,7 @@ import numpy as np
 import pytest
 
 from oracle import oracle as O
-from helpers import check_recorded_priors
+from helpers import check_recorded_priors, dropout_keep_np
 
 pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
@@ -138,6 +141,24 @@ def test_config5_two_coach_iterations(tmp_path, monkeypatch):
                               n={k: v.detach().clone() for k, v in self.nnet.nnet.state_dict().items()}))
             return tally
 
+    # the Coach's own trainer: its first 3 steps as they happen
+    from yacht_amd import train as TM
+    rec_steps = dict(trainer=None, idx=[], losses=[], amp=[])
+    real_step = TM.Trainer.step
+
+    def recording_step(self, states, targets, values, idx=None, batch=None, stream=None):
+        out = real_step(self, states, targets, values, idx=idx, batch=batch, stream=stream)
+        if rec_steps["trainer"] is None:
+            rec_steps.update(trainer=id(self), arrays=(states, targets, values))
+        if rec_steps["trainer"] == id(self) and len(rec_steps["idx"]) < 3:
+            rec_steps["idx"].append(idx.clone())
+            rec_steps["losses"].append(self.losses())
+            rec_steps["amp"].append(self.amp_state())
+            if len(rec_steps["idx"]) == 3:
+                rec_steps["params"] = self.params().clone()
+        return out
+    monkeypatch.setattr(TM.Trainer, "step", recording_step)
+
     sizes = []
     train = nn.train
 
@@ -172,43 +193,51 @@ def test_config5_two_coach_iterations(tmp_path, monkeypatch):
     for k in range(2):
         _same_as_host(c.trainExamplesHistory[k], plays[k]["img"])
 
-    # ---- iteration 1's first 3 amp steps against torch autocast + GradScaler, same minibatches
-    shard = c.trainExamplesHistory[0]
-    g = torch.Generator(device="cuda")
-    g.manual_seed(int(args.seed))  # NNetWrapper.train's first epoch at step count 0
-    perm = torch.randperm(len(shard), generator=g, device="cuda").to(torch.int32)
-    B = args.batch_size
-    idx = perm[:3 * B]
-    S = shard.states[idx.long()].contiguous()
-    X = K.featurize(S)
-    tg = shard.targets[idx.long()].contiguous()
-    vv = shard.values[idx.long()].contiguous()
-    torch.backends.cuda.matmul.allow_tf32 = False
-    p_amp, l_amp, g_amp, scale_amp = _torch_train_steps(sd0, 256, 6, X, tg, vv, B, 3, True)
-    p_f32, l_f32, g_f32, _ = _torch_train_steps(sd0, 256, 6, X, tg, vv, B, 3, False)
-    ours = Trainer(sd0, 256, 6, lr=2e-3, weight_decay=1e-4, max_batch=B, vloss_weight=1.5, dropout=0.0, amp=True)
-    ours_l, g1 = [], None
+    # ---- the Coach's first 3 amp steps: a standalone twin reproduces them bit for bit, and they
+    # are held against torch autocast + GradScaler on the same minibatches and dropout masks
+    assert len(rec_steps["idx"]) == 3 and all(len(i) == args.batch_size for i in rec_steps["idx"])
+    S_all, T_all, V_all = rec_steps["arrays"]
+    B, P_DROP = args.batch_size, float(args.dropout)
+    twin = Trainer(sd0, 256, 6, lr=2e-3, weight_decay=1e-4, max_batch=B, vloss_weight=1.5, dropout=P_DROP,
+                   seed=int(args.seed), amp=True)
     for k in range(3):
-        ours.backward(S, tg, vv, idx=torch.arange(k * B, (k + 1) * B, dtype=torch.int32, device="cuda"))
-        if k == 0:
-            sc = ours.amp_state()["scale"]
-            g1 = {n: v.numpy() / sc for n, v in ours.gradients().items()}
-        ours.apply()
-        ce, se, _ = ours.losses()
-        ours_l.append((ce / B, se / B))
+        twin.step(S_all, T_all, V_all, idx=rec_steps["idx"][k])
+        assert np.array_equal(twin.losses()[:2], rec_steps["losses"][k][:2]), k
+        assert twin.amp_state() == rec_steps["amp"][k], k
+    assert torch.equal(twin.params().view(torch.int32), rec_steps["params"].view(torch.int32))
+    params = {k: v.numpy() for k, v in twin.state_dict().items()}  # = the Coach's, bit for bit (above)
+    twin.close()
+    idx = torch.cat(rec_steps["idx"]).long()
+    S = S_all[idx].contiguous()
+    X = K.featurize(S)
+    tg = T_all[idx].contiguous()
+    vv = V_all[idx].contiguous()
+    # the trainer's keep masks of dropout step k (a fresh trainer: steps 0, 1, 2; rows = the
+    # minibatch rows), layer 0 = inp, 1 + b = block b
+    masks = [[torch.tensor(dropout_keep_np(int(args.seed), L, k, B, 256, P_DROP), device="cuda") for L in range(7)]
+             for k in range(3)]
+    torch.backends.cuda.matmul.allow_tf32 = False
+    p_amp, l_amp, g_amp, scale_amp = _torch_train_steps(sd0, 256, 6, X, tg, vv, B, 3, True, masks=masks, p=P_DROP)
+    p_f32, l_f32, g_f32, _ = _torch_train_steps(sd0, 256, 6, X, tg, vv, B, 3, False, masks=masks, p=P_DROP)
+    # step-1 gradients of the Coach's trainer = a backward at dropout step 0 on minibatch 0
+    gtr = Trainer(sd0, 256, 6, lr=2e-3, weight_decay=1e-4, max_batch=B, vloss_weight=1.5, dropout=P_DROP,
+                  seed=int(args.seed), amp=True)
+    gtr.backward(S_all, T_all, V_all, idx=rec_steps["idx"][0])
+    sc = gtr.amp_state()["scale"]
+    g1 = {n: v.numpy() / sc for n, v in gtr.gradients().items()}
+    gtr.close()
+    ours_l = [(l[0] / B, l[1] / B) for l in rec_steps["losses"]]
     tol = lambda gap, ref: 1.5 * gap + 1e-4 * abs(ref) + 1e-7
     for k in range(3):
         for j in range(2):
             assert abs(ours_l[k][j] - l_amp[k][j]) <= tol(abs(l_f32[k][j] - l_amp[k][j]), l_amp[k][j]), (k, j)
     for name in g_amp:
         assert _relnorm(g1[name], g_amp[name]) <= 1.5 * _relnorm(g_f32[name], g_amp[name]) + 2e-3, name
-    params = ours.state_dict()
     for name in p_amp:
         p0 = sd0[name].numpy()
-        d_ours = _relnorm(params[name].numpy() - p0, p_amp[name] - p0)
+        d_ours = _relnorm(params[name] - p0, p_amp[name] - p0)
         assert d_ours <= 1.5 * _relnorm(p_f32[name] - p0, p_amp[name] - p0) + 2e-2, name
-    assert ours.amp_state()["scale"] == scale_amp
-    ours.close()
+    assert rec_steps["amp"][2]["scale"] == scale_amp
 
     # ---- the gates: a fresh unsharded GatingArena on the same nets and env ids, same tally
     for gt in gates:

@@ -37,7 +37,7 @@ ARGS = dict(numIters=1, numEps=6, tempThreshold=15, updateThreshold=0.55, maxlen
             batch_size=64, vloss_weight=1.5, cuda=True, hidden=64, nblocks=1, dropout=0.0, seed=3)
 
 
-def _worker(port, out):
+def _worker(_index, port, out):  # (start_processes passes the process index first)
     import sys
     here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     for p in (here, os.path.join(here, "nypc-yacht-auction_amd")):

@@ -193,6 +193,13 @@ def _net_prior_sampled_games_vs_oracle(E, N, n, sims, seed, base, stride, diverg
         print(f"the same oracle with every Linear summed in reverse order (f32 vs f32): {frac_ff:.3f} of the "
               f"games diverge; {summary(first_ff)}")
         st["divergence"] = (frac, first, frac_ff, first_ff)
+        # the gate: the engine diverges from an independent f32 run no more often than two f32
+        # summation orders diverge from each other, plus 3 standard errors of that floor's estimate
+        # over the sampled games (round 3's prior, 2x torch fp32's error, diverged in 17 % of them
+        # against a 6 % floor)
+        n_games = len(pick)
+        se = np.sqrt(max(frac_ff, 1.0 / n_games) * (1.0 - frac_ff) / n_games)
+        assert frac <= frac_ff + 3.0 * se, (frac, frac_ff, se)
     eng.close()
     return st
 

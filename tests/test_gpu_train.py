@@ -143,7 +143,11 @@ def test_dropout_masks_are_deterministic_and_active(T, golden):
     assert not np.allclose(res[0], res[2]) and not np.allclose(res[0], res[3])
 
 
-def test_nnetwrapper_train_and_checkpoint(T, tmp_path):
+@pytest.mark.parametrize("amp", [False, True])
+def test_nnetwrapper_train_and_checkpoint(T, tmp_path, amp):
+    """NNetWrapper.train + save/load_checkpoint (NNet.py:118-213) in both modes: the float32 step
+    and the default under args.cuda, autocast + GradScaler (the AMP path through the
+    wrapper and its checkpoint round trip).  AMP counts the steps GradScaler did not skip."""
     K, N, TR = T
     from yacht_amd.coach import Coach
     from yacht_amd.game import YachtGame
@@ -155,17 +159,20 @@ def test_nnetwrapper_train_and_checkpoint(T, tmp_path):
     args = dotdict(lr=2e-3, weight_decay=1e-4, epochs=2, batch_size=64, vloss_weight=1.5, cuda=True, hidden=64,
                    nblocks=1, dropout=0.3)
     # args.cuda selects the reference's GPU arithmetic (autocast + GradScaler, NNet.py:113-116),
-    # args.amp False the float32 step; this test counts optimiser steps, which a GradScaler skip
-    # would not, so it runs the float32 mode
+    # args.amp False the float32 step
     assert NNetWrapper(game, args).uses_amp() and not NNetWrapper(game, dotdict(args, cuda=False)).uses_amp()
-    args = dotdict(args, amp=False)
+    args = dotdict(args, amp=amp)
     w = NNetWrapper(game, args)
-    assert not w._trainer().amp
+    assert w._trainer().amp == amp
     pi0, _ = w.predict(examples[0][0])
     w.train(examples, verbose=False)
     pi1, v1 = w.predict(examples[0][0])
     assert not np.allclose(pi0, pi1)
     steps = -(-len(examples) // 64) * 2
+    if amp:  # a GradScaler skip leaves AdamW's count alone (torch's scaler.step)
+        st = w._trainer().amp_state()
+        assert 1 <= st["steps"] <= steps and st["steps"] == w._trainer().step_count
+        steps = st["steps"]
     assert w._trainer().step_count == steps
     w.save_checkpoint(str(tmp_path), "best.pth.tar")
     ck = torch.load(os.path.join(tmp_path, "best.pth.tar"), map_location="cpu", weights_only=True)
@@ -288,19 +295,40 @@ def test_dropout_rows_split_over_calls_equal_the_whole_batch(T, golden, amp, B):
     assert not np.allclose(g_wrong, half.grads().cpu().numpy())  # the offset selects other masks
 
 
-def _torch_train_steps(sd0, H, NB, X, tg, vv, B, steps, amp, vw=1.5):
+class _FixedDropout(torch.nn.Module):
+    """nn.Dropout with given keep masks: x * keep * 1/(1-p), as torch's dropout kernel scales."""
+
+    def __init__(self, p):
+        super().__init__()
+        self.scale, self.keep = 1.0 / (1.0 - p), None
+
+    def forward(self, x):
+        return x * (self.keep.to(x.dtype) * self.scale)
+
+
+def _torch_train_steps(sd0, H, NB, X, tg, vv, B, steps, amp, vw=1.5, masks=None, p=0.0):
     """The reference's train() inner loop (NNet.py:132-165) on the GPU: autocast('cuda') +
-    GradScaler('cuda') (amp) or float32, AdamW(2e-3, 1e-4), clip 5.0; dropout 0."""
+    GradScaler('cuda') (amp) or float32, AdamW(2e-3, 1e-4), clip 5.0; dropout 0, or - masks[k][L]
+    given - the nn.Dropout layers (L = 0: inp, 1 + b: block b) applying those keep masks at step k."""
     import torch.nn.functional as F
     from yacht_amd.nnet import YachtNNet
     model = YachtNNet(hidden=H, nblocks=NB, dropout=0.0).cuda().float()
     model.load_state_dict(sd0)
+    drops = None
+    if masks is not None:
+        drops = [_FixedDropout(p) for _ in range(1 + NB)]
+        model.inp[3] = drops[0]
+        for b, blk in enumerate(model.blocks):
+            blk.dropout = drops[1 + b]
     model.train()
     opt = torch.optim.AdamW(model.parameters(), lr=2e-3, weight_decay=1e-4)
     scaler = torch.amp.GradScaler("cuda") if amp else None
     losses, grads1 = [], None
     for k in range(steps):
         sl = slice(k * B, (k + 1) * B)
+        if drops is not None:
+            for L, d in enumerate(drops):
+                d.keep = masks[k][L]
         opt.zero_grad(set_to_none=True)
         with torch.autocast("cuda", enabled=amp):
             out_pi, out_v = model(X[sl])
@@ -387,9 +415,11 @@ def test_amp_steps_vs_torch_autocast_gradscaler(T, golden, H, NB, B):
     assert st["scale"] == scale_amp and tr.step_count == st["steps"]
 
 
-def test_amp_skipped_step_leaves_unscaled_gradients(T, golden):
-    """A step GradScaler skips (the scaled fp16 gradients overflow) leaves the parameters alone and
-    the gradient buffer unscaled, as torch's unscale_ leaves p.grad."""
+def test_amp_skipped_step_gradients_as_torch_leaves_them(T, golden):
+    """A step GradScaler skips (the scaled fp16 gradients overflow) leaves the parameters alone, and
+    the gradient buffer as torch leaves p.grad: unscale_, then clip_grad_norm_'s
+    multiply by min(1, 5 / (norm + 1e-6)) - 0 for an infinite norm, so finite entries become 0
+    and infinite ones nan; all nan for a nan norm."""
     K, N, TR = T
     H, NB, B = 64, 1, 32
     W = golden("states.npz")["states"][:B]
@@ -406,8 +436,14 @@ def test_amp_skipped_step_leaves_unscaled_gradients(T, golden):
     st = tr.amp_state()
     assert st["found_inf"] and st["steps"] == 0 and st["scale"] == 2.0 ** 39
     assert np.array_equal(tr.params().cpu().numpy(), p0)
-    want = g_scaled * np.float32(2.0 ** -40)
-    np.testing.assert_array_equal(tr.grads().cpu().numpy(), want)
+    u = g_scaled * np.float32(2.0 ** -40)
+    total = float(np.sum(u.astype(np.float64) ** 2))
+    assert not np.isfinite(total)
+    with np.errstate(invalid="ignore"):
+        want = u * np.float32(0.0) if np.isinf(total) else np.full_like(u, np.nan)
+    got = tr.grads().cpu().numpy()
+    np.testing.assert_array_equal(got, want)
+    assert np.isnan(got).any() and (np.isnan(total) or (got == 0).any())
 
 
 @pytest.mark.parametrize("H,NB,B,scale", [(256, 6, 512, None), (64, 1, 32, 2.0 ** 40)])
@@ -444,3 +480,39 @@ def test_amp_fused_norm_step_equals_backward_then_apply(T, golden, H, NB, B, sca
         np.testing.assert_allclose(fused.params().cpu().numpy(), split.params().cpu().numpy(), rtol=1e-6, atol=1e-9)
     if scale:
         assert fused.amp_state()["steps"] < 3
+
+
+@pytest.mark.parametrize("H,NB,B", [(64, 2, 64), (256, 6, 512)])
+def test_amp_update_made_masks_equal_k_amp_masks(T, golden, H, NB, B):
+    """Every AMP step after the first reads dropout keep bits that the previous step's k_amp_update
+    made ahead (row offset 0).  Trainer A: step() then backward() at dropout step 1 (the update-made
+    bits).  Trainer B: A's parameters and step count 1 through yk_trainer_set, so its backward makes
+    the bits with k_amp_masks.  Same gradients bit for bit, and both differ from dropout step 0's
+    masks."""
+    K, N, TR = T
+    W = golden("states.npz")["states"]
+    W = np.concatenate([W] * (2 * B // len(W) + 1))[:2 * B]
+    rng = np.random.RandomState(12)
+    S = K.states_to_device(W)
+    tg = torch.tensor(rng.randint(0, 3226, 2 * B), dtype=torch.int32, device="cuda")
+    vv = torch.tensor(rng.rand(2 * B) * 2 - 1, dtype=torch.float32, device="cuda")
+    i0 = torch.arange(0, B, dtype=torch.int32, device="cuda")
+    i1 = torch.arange(B, 2 * B, dtype=torch.int32, device="cuda")
+    kw = dict(max_batch=B, dropout=0.3, seed=13, amp=True, init_scale=256.0)  # (no skipped step)
+    a = TR.Trainer(_sd(H, NB), H, NB, **kw)
+    a.step(S, tg, vv, idx=i0)
+    assert a.amp_state()["steps"] == 1
+    a.backward(S, tg, vv, idx=i1)
+    ga = a.grads().clone()
+    b = TR.Trainer(_sd(H, NB), H, NB, **kw)
+    b.load_params(a.state_dict())
+    m, v = a.moments()
+    b.set_moments(m, v, 1)
+    b.backward(S, tg, vv, idx=i1)
+    assert torch.equal(ga.view(torch.int32), b.grads().view(torch.int32))
+    c = TR.Trainer(_sd(H, NB), H, NB, **kw)  # the same parameters at dropout step 0: other masks
+    c.load_params(a.state_dict())
+    c.backward(S, tg, vv, idx=i1)
+    assert not torch.equal(ga, c.grads())
+    for t in (a, b, c):
+        t.close()

@@ -46,7 +46,8 @@ if os.path.exists(summ):
         avg = next((x["avg_us"] for n, x in stats.items() if n == kname), None)
         short = "k_forward<256, 2>" if kind == "forward" else "k_expand_backup"
         if "hbm_bytes_per_launch" in v:
-            out = {"kernel": short, "config": cfg, "command": cmd, "launches": v["launches"],
+            out = {"kernel": short, "config": cfg, "kernel_src_sha16": s.get("kernel_src_sha16"), "command": cmd,
+                   "launches": v["launches"],
                    "FETCH_SIZE_KiB_mean": v["FETCH_SIZE_KiB_mean"], "WRITE_SIZE_KiB_mean": v["WRITE_SIZE_KiB_mean"],
                    "correction": "FETCH_SIZE x2 on gfx950 (MI355X_MICROARCH.md, HBM); WRITE_SIZE as read",
                    "hbm_bytes_per_launch": v["hbm_bytes_per_launch"], "kernel_trace_avg_us": avg}
@@ -54,7 +55,7 @@ if os.path.exists(summ):
             json.dump(out, open(p, "w"), indent=1)
             print("wrote", os.path.relpath(p, REPO))
         if kind == "forward" and "mfma_busy_frac" in v:
-            out = {"kernel": short, "config": cfg,
+            out = {"kernel": short, "config": cfg, "kernel_src_sha16": s.get("kernel_src_sha16"),
                    "command": f"tools/profile_bench.sh {tag}: rocprofv3 --kernel-include-regex k_forward --pmc "
                               "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE -- python3 "
                               "bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-arena --no-coach --no-shape "

@@ -115,7 +115,7 @@ ENGINE = [
     (r"^        if \(V == 0\) \{  // no valid action: MCTS.py:141-147.*\n", "before", "        SEL_ACC(0, t_lv);\n        SEL_T0(t_sc);\n"),
     (r"^        const int bj = bj_out;\n", "after", "        SEL_ACC(1, t_sc);\n        SEL_ADD(4, 1);\n        SEL_ADD(5, V);\n        SEL_T0(t_st);\n"),
     (r"^        s = canonical\(s, np\);  // MCTS.py:150\n", "after", "        SEL_ACC(2, t_st);\n"),
-    (r"^        d\.gstats\[\(long\)e \* 8 \+ 7\] \+= 1;\n    \}\n\}\n", "before_last_brace", "    SEL_ACC(3, t_all);\n"),
+    (r"^        d\.gstats\[\(long\)e \* GST \+ 8\] \+= gathered;\n    \}\n\}\n", "before_last_brace", "    SEL_ACC(3, t_all);\n"),
     (r"^    if \(d\.done\[e\]\) return;\n    expand_backup_game\(d, e, lane\);\n", "replace",
      "    if (d.done[e]) return;\n" + XSPAN_BEGIN + "    expand_backup_game(d, e, lane);\n" + XSPAN_MID),
     (r"^        select_game\(d, e, lane, env_ids, ctr_arr\);\n    \}\n\}\n\n__device__ __forceinline__ void expand_backup_game",

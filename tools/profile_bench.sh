@@ -8,6 +8,8 @@ export TMPDIR=/tmp
 tag=${1:-r01}
 out=gpurun_out/prof_$tag
 mkdir -p $out
+# the kernel sources measured (bench.py matches its roofline inputs to them)
+python3 -c "import bench; print(bench.kernel_sources_sha16())" > $out/kernel_src_sha16.txt
 args="--steps 1 --warmup 1 --no-cpu-baseline --no-arena --no-coach --no-shape --no-f16 --no-train"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/trace -o bench --output-format csv -- python3 bench.py $args > $out/bench_trace.json
 for c in FETCH_SIZE WRITE_SIZE; do

@@ -10,6 +10,9 @@ from collections import defaultdict
 
 d = sys.argv[1]
 out = {}
+_sha = os.path.join(d, "kernel_src_sha16.txt")
+if os.path.exists(_sha):
+    out["kernel_src_sha16"] = open(_sha).read().strip()
 st = glob.glob(os.path.join(d, "trace", "**", "*kernel_stats.csv"), recursive=True)
 if st:
     rows = list(csv.DictReader(open(st[0])))

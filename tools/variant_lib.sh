@@ -20,9 +20,12 @@ case " $* " in
 esac
 for f in yk_env yk_net yk_engine yk_train yk_train_amp yk_replay; do
   [ -f $src/$f.hip ] || continue
-  /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -fPIC -std=c++17 -ffp-contract=off -w "$@" \
+  fc=off; [ $f = yk_train_amp ] && fc=fast  # (as the Makefile)
+  /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -fPIC -std=c++17 -ffp-contract=$fc -w "$@" \
      -Iinclude -I$src -c $src/$f.hip -o $out/$f.o &
 done
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $out/libyacht_hip.so $out/yk_*.o -L/opt/rocm/lib -lrocblas -Wl,-rpath,/opt/rocm/lib
+libs=""  # (baselines staged from before round 5 still call rocBLAS in the f32 trainer)
+grep -q rocblas $src/yk_train.hip && libs="-L/opt/rocm/lib -lrocblas -Wl,-rpath,/opt/rocm/lib"
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $out/libyacht_hip.so $out/yk_*.o $libs
 echo "built $out/libyacht_hip.so"
