@@ -85,14 +85,15 @@ def cpu_baseline(state_dict, sims, seconds_target=15.0, threads=None):
 
 
 def kernel_sources_sha16():
-    """The kernels' identity: sha256 over the sources libyacht_hip.so is built from (csrc, the
-    C-ABI header, the Makefile), 16 hex digits.  tools/profile_bench.sh records it with every
-    rocprofv3 summary, so the bench line cites counters of the tree it runs, or says they are stale."""
+    """The search / predict kernels' identity: sha256 over the sources k_forward and
+    k_expand_backup are built from (every csrc file but the trainers' and the replay buffer's,
+    the C-ABI header, the Makefile), 16 hex digits.  tools/profile_bench.sh records it with every
+    rocprofv3 summary, so the bench line cites counters of the kernels it runs, or says they are stale."""
     import hashlib
     h = hashlib.sha256()
     pkg = os.path.join(REPO, "nypc-yacht-auction_amd")
     files = sorted(os.path.join(pkg, "csrc", f) for f in os.listdir(os.path.join(pkg, "csrc"))
-                   if f.endswith((".hip", ".h")))
+                   if f.endswith((".hip", ".h")) and not f.startswith(("yk_train", "yk_replay")))
     for f in files + [os.path.join(REPO, "include", "yacht_hip.h"), os.path.join(pkg, "Makefile")]:
         h.update(os.path.basename(f).encode() + b"\0")
         with open(f, "rb") as fh:
@@ -189,7 +190,7 @@ def train_leg(model_sd, eng, steps=40, batch=512, seed=0):
         g = torch.Generator(device="cuda")
         g.manual_seed(seed)
         perm = torch.randperm(n, generator=g, device="cuda").to(torch.int32)
-        for i in range(3):  # warm-up (rocBLAS kernel selection)
+        for i in range(3):  # warm-up
             tr.step(S, T, V, idx=perm[i * batch:(i + 1) * batch])
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -205,7 +206,7 @@ def train_leg(model_sd, eng, steps=40, batch=512, seed=0):
         key = "amp" if amp else "f32"
         out[key] = {"config": f"minibatch {batch} of {n} self-play examples, YachtNNet hidden {H} x {NB}, " +
                               ("autocast('cuda') + GradScaler arithmetic on hand-written fp16 MFMA kernels (6 launches)"
-                               if amp else "f32 (rocBLAS GEMMs + fused HIP row kernels)") +
+                               if amp else "f32 (hand-written f32 MFMA GEMMs + fused HIP row kernels)") +
                               ", AdamW + clip 5.0, dropout 0.3",
                     "ms_per_step": 1000.0 * dt, "examples_per_s": batch / dt, "achieved_tflops": flop / dt / 1e12,
                     "last_loss": ce / batch + 1.5 * se / batch}
@@ -372,7 +373,7 @@ def coach_leg(model, image, n_envs, max_moves, sims, world, train_steps=60, aren
     few = (shard.states[sub.to("cuda")], shard.targets[sub.to("cuda")], shard.values[sub.to("cuda")])
     from yacht_amd.replay import ExampleShard
     warm = ExampleShard(*(x[:3 * bs] for x in few))
-    new.train(warm, verbose=False)  # warm-up: 3 steps (rocBLAS kernel selection)
+    new.train(warm, verbose=False)  # warm-up: 3 steps
     timed = ExampleShard(*(x[3 * bs:] for x in few))
     D.barrier()
     torch.cuda.synchronize()

@@ -13,6 +13,7 @@
 // gradients, column reductions for bias / LayerNorm parameter gradients, the global gradient
 // norm and the AdamW update.  Parameters, gradients and the Adam moments are single flat
 // buffers in torch state_dict order, so the gradient buffer is one RCCL all-reduce.
+#include <algorithm>
 #include <cmath>
 #include <vector>
 
@@ -476,6 +477,7 @@ struct yk_trainer {
     int2* tiles = nullptr;
     int ntiles = 0;
     double* acc = nullptr;  // [0] ce sum, [1] mse sum (unused), [2] grad sq norm
+    float* gws = nullptr;   // k_sgemm's split-K partial tiles
     double* sqpart = nullptr;  // k_sqnorm partials
     float2* lrow = nullptr;    // per-row (ce, squared value error) of the last batch
     float* lsum = nullptr;     // their column sums (k_colsums)
@@ -508,74 +510,129 @@ int talloc(yk_trainer* t, T** p, size_t count) {
 // row-major C[M][N] = op(A)[M][K] . op(B)[K][N] (+ beta C), op = transpose when ta / tb (A stored
 // [K][M], B stored [N][K]).  64 x 64 output tiles per 256-thread workgroup, each wave a 32 x 32
 // quarter as 2 x 2 blocks of v_mfma_f32_16x16x4_f32 (f32 operands: exact products, f32
-// accumulation, the reference's CPU arithmetic up to summation order); K staged through LDS 16
-// deep, the global reads coalesced along whichever dimension is contiguous in memory.
-constexpr int GT = 64, GK = 16;
-__global__ __launch_bounds__(256) void k_sgemm(int ta, int tb, int M, int N, int K, const float* __restrict__ A, int lda,
-                                               const float* __restrict__ B, int ldb, float* __restrict__ C, int ldc,
-                                               float beta) {
-    __shared__ float As[GK][GT + 4];  // [k][m]
-    __shared__ float Bs[GK][GT + 4];  // [k][n]
+// accumulation, the reference's CPU arithmetic up to summation order), or 32 x 32 tiles (a 16 x 16
+// block per wave) for shapes with few tiles.  K goes through LDS 32 deep,
+// the next chunk's global reads issued before the current chunk's MFMAs (coalesced along whichever
+// dimension is contiguous in memory); LDS rows padded by 16 floats, so a wave's 64 fragment reads
+// hit 64 distinct banks (64-wide tiles).  Few output tiles over a long K (dA = dlogits W_pi: K = 3226 over 32
+// tiles) split K over blockIdx.z into partial tiles that k_sgemm_reduce sums in split order (the
+// result does not depend on scheduling: ranks stay bit-identical).
+constexpr int GK = 32;
+template <int TM>  // output tile TM x TM: 64 (each wave a 32 x 32 quarter, 2 x 2 MFMA blocks) or 32 (16 x 16)
+__global__ __launch_bounds__(256) void k_sgemm(int ta, int tb, int M, int N, int K, int kc, const float* __restrict__ A,
+                                               int lda, const float* __restrict__ B, int ldb, float* __restrict__ C,
+                                               int ldc, float beta, float* __restrict__ part) {
+    constexpr int LDA = TM + 16, BL = TM / 32, EPT = TM * GK / 256;  // LDS row; blocks per wave side; elements per thread
+    __shared__ float As[GK][LDA];  // [k][m]
+    __shared__ float Bs[GK][LDA];  // [k][n]
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int m0 = blockIdx.y * GT, n0 = blockIdx.x * GT;
-    const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
-    floatx4 acc[2][2];
+    const int m0 = blockIdx.y * TM, n0 = blockIdx.x * TM;
+    const int kb = blockIdx.z * kc, ke = min(K, kb + kc);
+    const int wm = (wave >> 1) * (TM / 2), wn = (wave & 1) * (TM / 2);
+    floatx4 acc[BL][BL];
 #pragma unroll
-    for (int i = 0; i < 2; i++)
+    for (int i = 0; i < BL; i++)
 #pragma unroll
-        for (int j = 0; j < 2; j++) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-    for (int k0 = 0; k0 < K; k0 += GK) {
-        float av[4], bv[4];
+        for (int j = 0; j < BL; j++) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    // element e = tid + 256 i of a TM x GK tile: (row, k) with the memory-contiguous index fastest
+    auto a_rc = [&](int e, int& r, int& k) {
+        if (ta) { r = e % TM; k = e / TM; } else { k = e % GK; r = e / GK; }
+    };
+    auto b_rc = [&](int e, int& c, int& k) {
+        if (tb) { k = e % GK; c = e / GK; } else { c = e % TM; k = e / TM; }
+    };
+    float av[EPT], bv[EPT];
+    auto load = [&](int k0) {
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
+        for (int i = 0; i < EPT; i++) {
             const int e = tid + 256 * i;
-            const int am = ta ? (e & 63) : (e >> 4), ak = ta ? (e >> 6) : (e & 15);
-            const int gm = m0 + am, gk = k0 + ak;
-            av[i] = (gm < M && gk < K) ? (ta ? A[(long)gk * lda + gm] : A[(long)gm * lda + gk]) : 0.f;
-            const int bn = tb ? (e >> 4) : (e & 63), bk = tb ? (e & 15) : (e >> 6);
-            const int gn = n0 + bn, gkb = k0 + bk;
-            bv[i] = (gn < N && gkb < K) ? (tb ? B[(long)gn * ldb + gkb] : B[(long)gkb * ldb + gn]) : 0.f;
+            int r, k, c, kk;
+            a_rc(e, r, k);
+            b_rc(e, c, kk);
+            const int gm = m0 + r, gk = k0 + k, gn = n0 + c, gkb = k0 + kk;
+            av[i] = (gm < M && gk < ke) ? (ta ? A[(long)gk * lda + gm] : A[(long)gm * lda + gk]) : 0.f;
+            bv[i] = (gn < N && gkb < ke) ? (tb ? B[(long)gn * ldb + gkb] : B[(long)gkb * ldb + gn]) : 0.f;
         }
-        __syncthreads();  // the previous chunk's reads are done
+    };
+    load(kb);
+    for (int k0 = kb; k0 < ke; k0 += GK) {
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
+        for (int i = 0; i < EPT; i++) {
             const int e = tid + 256 * i;
-            As[ta ? (e >> 6) : (e & 15)][ta ? (e & 63) : (e >> 4)] = av[i];
-            Bs[tb ? (e & 15) : (e >> 6)][tb ? (e >> 4) : (e & 63)] = bv[i];
+            int r, k, c, kk;
+            a_rc(e, r, k);
+            b_rc(e, c, kk);
+            As[k][r] = av[i];
+            Bs[kk][c] = bv[i];
         }
         __syncthreads();
+        if (k0 + GK < ke) load(k0 + GK);  // the next chunk's reads fly under this chunk's MFMAs
 #pragma unroll
-        for (int kk = 0; kk < GK; kk += 4) {
-            const int k = kk + (lane >> 4);
-            float a[2], b[2];
+        for (int ks = 0; ks < GK; ks += 4) {
+            const int k = ks + (lane >> 4);
+            float a[BL], b[BL];
 #pragma unroll
-            for (int i = 0; i < 2; i++) a[i] = As[k][wm + 16 * i + (lane & 15)];
+            for (int i = 0; i < BL; i++) a[i] = As[k][wm + 16 * i + (lane & 15)];
 #pragma unroll
-            for (int j = 0; j < 2; j++) b[j] = Bs[k][wn + 16 * j + (lane & 15)];
+            for (int j = 0; j < BL; j++) b[j] = Bs[k][wn + 16 * j + (lane & 15)];
 #pragma unroll
-            for (int i = 0; i < 2; i++)
+            for (int i = 0; i < BL; i++)
 #pragma unroll
-                for (int j = 0; j < 2; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[j], acc[i][j], 0, 0, 0);
+                for (int j = 0; j < BL; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[j], acc[i][j], 0, 0, 0);
         }
+        __syncthreads();  // every wave is done reading the chunk before the next one is stored
     }
     // block (i, j): lane l holds rows 4 (l >> 4) + r, column l & 15
 #pragma unroll
-    for (int i = 0; i < 2; i++)
+    for (int i = 0; i < BL; i++)
 #pragma unroll
-        for (int j = 0; j < 2; j++)
+        for (int j = 0; j < BL; j++)
 #pragma unroll
             for (int r = 0; r < 4; r++) {
                 const int gm = m0 + wm + 16 * i + 4 * (lane >> 4) + r, gn = n0 + wn + 16 * j + (lane & 15);
                 if (gm < M && gn < N) {
-                    float* c = C + (long)gm * ldc + gn;
-                    *c = beta != 0.f ? acc[i][j][r] + beta * *c : acc[i][j][r];
+                    if (part) {
+                        part[((long)blockIdx.z * M + gm) * N + gn] = acc[i][j][r];
+                    } else {
+                        float* c = C + (long)gm * ldc + gn;
+                        *c = beta != 0.f ? acc[i][j][r] + beta * *c : acc[i][j][r];
+                    }
                 }
             }
 }
-int gemm_rm(hipStream_t s, bool ta, bool tb, int M, int N, int K, const float* A, int lda, const float* B, int ldb,
-            float* C, int ldc, float beta) {
-    hipLaunchKernelGGL(k_sgemm, dim3((unsigned)((N + GT - 1) / GT), (unsigned)((M + GT - 1) / GT)), dim3(256), 0, s,
-                       ta ? 1 : 0, tb ? 1 : 0, M, N, K, A, lda, B, ldb, C, ldc, beta);
+// C = sum over the splits in order (+ beta C)
+__global__ void k_sgemm_reduce(int M, int N, int S, const float* __restrict__ part, float* __restrict__ C, int ldc,
+                               float beta) {
+    const long i = (long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (long)M * N) return;
+    float s = part[i];
+    for (int z = 1; z < S; z++) s += part[(long)z * M * N + i];
+    float* c = C + (i / N) * ldc + i % N;
+    *c = beta != 0.f ? s + beta * *c : s;
+}
+constexpr long GEMM_WS = 1L << 20;  // split-K workspace (floats): splits x M x N, <= 256 32 x 32 tiles' worth
+// tile size and K split for the shape: 64 x 64 tiles when there are >= 128 of them, else 32 x 32;
+// K split (a partial pass + k_sgemm_reduce) only for long K over few tiles (dA: K = 3226)
+int gemm_rm(hipStream_t s, float* ws, bool ta, bool tb, int M, int N, int K, const float* A, int lda, const float* B,
+            int ldb, float* C, int ldc, float beta) {
+    const int t64 = ((M + 63) / 64) * ((N + 63) / 64);
+    const int TM = t64 >= 128 ? 64 : 32;
+    const int tiles = ((M + TM - 1) / TM) * ((N + TM - 1) / TM);
+    int S = K >= 1024 ? std::max(1, std::min(256 / tiles, K / 512)) : 1;
+    while (S > 1 && (long)S * M * N > GEMM_WS) S--;
+    const int kc = ((K + S - 1) / S + GK - 1) / GK * GK;
+    S = (K + kc - 1) / kc;
+    const dim3 grid((unsigned)((N + TM - 1) / TM), (unsigned)((M + TM - 1) / TM), (unsigned)S);
+    float* part = S > 1 ? ws : nullptr;
+    if (TM == 64)
+        hipLaunchKernelGGL(k_sgemm<64>, grid, dim3(256), 0, s, ta ? 1 : 0, tb ? 1 : 0, M, N, K, kc, A, lda, B, ldb, C,
+                           ldc, beta, part);
+    else
+        hipLaunchKernelGGL(k_sgemm<32>, grid, dim3(256), 0, s, ta ? 1 : 0, tb ? 1 : 0, M, N, K, kc, A, lda, B, ldb, C,
+                           ldc, beta, part);
+    if (S > 1)
+        hipLaunchKernelGGL(k_sgemm_reduce, dim3((unsigned)(((long)M * N + 255) / 256)), dim3(256), 0, s, M, N, S, ws, C,
+                           ldc, beta);
     return hipGetLastError() == hipSuccess ? YK_OK : YK_ERR_HIP;
 }
 
@@ -594,17 +651,17 @@ int step_impl(yk_trainer* t, const yk_state_t* states, const int32_t* targets, c
                        t->vt, B);
     YK_LAUNCHED();
     // ---- forward
-    if ((rc = gemm_rm(s, false, true, B, H, FEAT, t->X, FEAT, Pt(T_WIN), FEAT, t->Z0, H, 0.f))) return rc;
+    if ((rc = gemm_rm(s, t->gws, false, true, B, H, FEAT, t->X, FEAT, Pt(T_WIN), FEAT, t->Z0, H, 0.f))) return rc;
     hipLaunchKernelGGL(k_inp_fwd<VPL>, rows, wave4, 0, s, t->Z0, Pt(T_BIN), Pt(T_GIN), Pt(T_BEIN), t->mu0, t->rs0,
                        t->mask0, t->Hs[0], B, p, seed, step, t->row_base);
     YK_LAUNCHED();
     for (int b = 0; b < NB; b++) {
-        if ((rc = gemm_rm(s, false, true, B, H, H, t->Hs[b], H, Pt(t_blk(b, 0)), H, t->U1[b], H, 0.f))) return rc;
+        if ((rc = gemm_rm(s, t->gws, false, true, B, H, H, t->Hs[b], H, Pt(t_blk(b, 0)), H, t->U1[b], H, 0.f))) return rc;
         hipLaunchKernelGGL(k_blk_fwd<VPL>, rows, wave4, 0, s, t->U1[b], Pt(t_blk(b, 1)), Pt(t_blk(b, 2)), Pt(t_blk(b, 3)),
                            t->mu1[b], t->rs1[b], t->mask1[b], t->R1[b], (const float*)nullptr, B, p, seed, step, 1 + b,
                            t->row_base);
         YK_LAUNCHED();
-        if ((rc = gemm_rm(s, false, true, B, H, H, t->R1[b], H, Pt(t_blk(b, 4)), H, t->U2[b], H, 0.f))) return rc;
+        if ((rc = gemm_rm(s, t->gws, false, true, B, H, H, t->R1[b], H, Pt(t_blk(b, 4)), H, t->U2[b], H, 0.f))) return rc;
         hipLaunchKernelGGL(k_blk_fwd<VPL>, rows, wave4, 0, s, t->U2[b], Pt(t_blk(b, 5)), Pt(t_blk(b, 6)), Pt(t_blk(b, 7)),
                            t->mu2[b], t->rs2[b], (uint8_t*)nullptr, t->Hs[b + 1], t->Hs[b], B, p, seed, step, -1,
                            t->row_base);
@@ -614,17 +671,17 @@ int step_impl(yk_trainer* t, const yk_state_t* states, const int32_t* targets, c
     hipLaunchKernelGGL(k_heads_fwd<VPL>, rows, wave4, 0, s, Hh, Pt(t_head(NB, 0)), Pt(t_head(NB, 1)), Pt(t_head(NB, 4)),
                        Pt(t_head(NB, 5)), t->Api, t->Av, t->mup, t->rsp, t->muv, t->rsv, B);
     YK_LAUNCHED();
-    if ((rc = gemm_rm(s, false, true, B, A, H, t->Api, H, Pt(t_head(NB, 2)), H, t->logits, A, 0.f))) return rc;
-    if ((rc = gemm_rm(s, false, true, B, 128, H, t->Av, H, Pt(t_head(NB, 6)), H, t->Zv1, 128, 0.f))) return rc;
+    if ((rc = gemm_rm(s, t->gws, false, true, B, A, H, t->Api, H, Pt(t_head(NB, 2)), H, t->logits, A, 0.f))) return rc;
+    if ((rc = gemm_rm(s, t->gws, false, true, B, 128, H, t->Av, H, Pt(t_head(NB, 6)), H, t->Zv1, 128, 0.f))) return rc;
     hipLaunchKernelGGL(k_loss, dim3(B), dim3(LOSS_T), 0, s, t->logits, Pt(t_head(NB, 3)), t->Zv1, Pt(t_head(NB, 7)),
                        Pt(t_head(NB, 8)), Pt(t_head(NB, 9)), t->tgt, t->vt, t->dlogits, t->dZv1, t->dzv2, t->v2prod,
                        t->vout, t->lrow, B, A, t->cfg.vloss_weight);
     YK_LAUNCHED();
     // ---- backward: heads (bias / LayerNorm gradients are column sums, taken at the end)
-    if ((rc = gemm_rm(s, true, false, A, H, B, t->dlogits, A, t->Api, H, Gt(t_head(NB, 2)), H, 0.f))) return rc;
-    if ((rc = gemm_rm(s, true, false, 128, H, B, t->dZv1, 128, t->Av, H, Gt(t_head(NB, 6)), H, 0.f))) return rc;
-    if ((rc = gemm_rm(s, false, false, B, H, A, t->dlogits, A, Pt(t_head(NB, 2)), H, t->dA, H, 0.f))) return rc;
-    if ((rc = gemm_rm(s, false, false, B, H, 128, t->dZv1, 128, Pt(t_head(NB, 6)), H, t->dAv, H, 0.f))) return rc;
+    if ((rc = gemm_rm(s, t->gws, true, false, A, H, B, t->dlogits, A, t->Api, H, Gt(t_head(NB, 2)), H, 0.f))) return rc;
+    if ((rc = gemm_rm(s, t->gws, true, false, 128, H, B, t->dZv1, 128, t->Av, H, Gt(t_head(NB, 6)), H, 0.f))) return rc;
+    if ((rc = gemm_rm(s, t->gws, false, false, B, H, A, t->dlogits, A, Pt(t_head(NB, 2)), H, t->dA, H, 0.f))) return rc;
+    if ((rc = gemm_rm(s, t->gws, false, false, B, H, 128, t->dZv1, 128, Pt(t_head(NB, 6)), H, t->dAv, H, 0.f))) return rc;
     hipLaunchKernelGGL(k_heads_bwd<VPL>, rows, wave4, 0, s, Hh, Pt(t_head(NB, 0)), Pt(t_head(NB, 1)), Pt(t_head(NB, 4)),
                        Pt(t_head(NB, 5)), t->mup, t->rsp, t->muv, t->rsv, t->dA, t->dAv, t->dH, t->rgp, t->rbp, t->rgv,
                        t->rbv, B);
@@ -634,20 +691,20 @@ int step_impl(yk_trainer* t, const yk_state_t* states, const int32_t* targets, c
         hipLaunchKernelGGL(k_blk_bwd<VPL>, rows, wave4, 0, s, t->dH, (const uint8_t*)nullptr, 0.f, t->U2[b],
                            Pt(t_blk(b, 6)), t->mu2[b], t->rs2[b], t->dU2[b], t->rg2[b], t->rb2[b], B);
         YK_LAUNCHED();
-            if ((rc = gemm_rm(s, true, false, H, H, B, t->dU2[b], H, t->R1[b], H, Gt(t_blk(b, 4)), H, 0.f))) return rc;
-        if ((rc = gemm_rm(s, false, false, B, H, H, t->dU2[b], H, Pt(t_blk(b, 4)), H, t->dT, H, 0.f))) return rc;  // dR1
+            if ((rc = gemm_rm(s, t->gws, true, false, H, H, B, t->dU2[b], H, t->R1[b], H, Gt(t_blk(b, 4)), H, 0.f))) return rc;
+        if ((rc = gemm_rm(s, t->gws, false, false, B, H, H, t->dU2[b], H, Pt(t_blk(b, 4)), H, t->dT, H, 0.f))) return rc;  // dR1
         hipLaunchKernelGGL(k_blk_bwd<VPL>, rows, wave4, 0, s, t->dT, t->mask1[b], p, t->U1[b], Pt(t_blk(b, 2)), t->mu1[b],
                            t->rs1[b], t->dU1[b], t->rg1[b], t->rb1[b], B);
         YK_LAUNCHED();
-            if ((rc = gemm_rm(s, true, false, H, H, B, t->dU1[b], H, t->Hs[b], H, Gt(t_blk(b, 0)), H, 0.f))) return rc;
+            if ((rc = gemm_rm(s, t->gws, true, false, H, H, B, t->dU1[b], H, t->Hs[b], H, Gt(t_blk(b, 0)), H, 0.f))) return rc;
         // dH_b = dH_{b+1} (residual) + dU1 . W1
-        if ((rc = gemm_rm(s, false, false, B, H, H, t->dU1[b], H, Pt(t_blk(b, 0)), H, t->dH, H, 1.f))) return rc;
+        if ((rc = gemm_rm(s, t->gws, false, false, B, H, H, t->dU1[b], H, Pt(t_blk(b, 0)), H, t->dH, H, 1.f))) return rc;
     }
     // ---- input layer
     hipLaunchKernelGGL(k_inp_bwd<VPL>, rows, wave4, 0, s, t->dH, t->mask0, p, t->Z0, Pt(T_GIN), Pt(T_BEIN), t->mu0,
                        t->rs0, t->dZ0, t->rg0, t->rb0, B);
     YK_LAUNCHED();
-    if ((rc = gemm_rm(s, true, false, H, FEAT, B, t->dZ0, H, t->X, FEAT, Gt(T_WIN), FEAT, 0.f))) return rc;
+    if ((rc = gemm_rm(s, t->gws, true, false, H, FEAT, B, t->dZ0, H, t->X, FEAT, Gt(T_WIN), FEAT, 0.f))) return rc;
     // ---- every bias / LayerNorm gradient: one launch of column sums
     hipLaunchKernelGGL(k_colsums, dim3(t->ntiles), dim3(256), 0, s, t->jobs, t->tiles, B);
     YK_LAUNCHED();
@@ -690,6 +747,7 @@ int yk_trainer_create(yk_trainer_t** out, int H, int NB, const float* const* par
     TA(t->M, o);
     TA(t->V, o);
     TA(t->X, Bm * FEAT);
+    if (!cfg->amp) TA(t->gws, GEMM_WS);
     TA(t->tgt, Bm);
     TA(t->vt, Bm);
     TA(t->vout, Bm);
