@@ -1497,6 +1497,7 @@ struct yk_engine {
     double kms[8] = {0};
     int64_t klaunch[8] = {0};
     bool root_scan = true;  // the incremental root scan (k_root_sort + root_scan); YK_ROOT_SCAN=0: full scans
+    bool split_descent = false;  // YK_SPLIT_DESCENT=1: the descent as its own k_select launch (same trees)
 };
 
 namespace {
@@ -1614,9 +1615,14 @@ int run_sims(yk_engine* eng, int G, const hipStream_t* st, int sims, const uint3
             // the move's first expansion ends without the next descent: the root's P order is built
             // in between (k_root_sort; root_scan uses it for the move's remaining simulations)
             const bool sort_root = k == 0 && sims > 1 && eng->root_scan;
-            hipLaunchKernelGGL(k_expand_backup, game_grid(d), bb, 0, st[g], d, k + 1 < sims && !sort_root ? 1 : 0,
+            const bool fuse = k + 1 < sims && !sort_root;  // the next descent in the expand's tail
+            hipLaunchKernelGGL(k_expand_backup, game_grid(d), bb, 0, st[g], d, fuse && !eng->split_descent ? 1 : 0,
                                env_ids, ctr);
             YK_LAUNCHED();
+            if (fuse && eng->split_descent) {
+                hipLaunchKernelGGL(k_select, game_grid(d), bb, 0, st[g], d, env_ids, ctr);
+                YK_LAUNCHED();
+            }
             if (sort_root) {
                 if (timed) prof_mark(eng, g, KC_SCAN, st[g]);
                 hipLaunchKernelGGL(k_root_sort, dim3((unsigned)(d.e_hi - d.e_lo)), bb, 0, st[g], d);
@@ -1772,6 +1778,11 @@ constexpr int YK_FPARTS_MAX = 4;
         eng->root_scan = !(ev && ev[0] == '0');
         const char* ek = getenv("YK_ROOT_K");  // a shorter kept order (>= 1): the tests' fallback cases
         d.ro_k = ek ? std::max(1, std::min(RO_K, atoi(ek))) : RO_K;
+        // YK_SPLIT_DESCENT=1 (measurement): k_expand_backup stops after the backup and each next
+        // descent is its own k_select launch, so rocprofv3 times and counts the expansion + backup
+        // and the descent apart (the same work: the trees are identical)
+        const char* es = getenv("YK_SPLIT_DESCENT");
+        eng->split_descent = es && es[0] == '1';
     }
     if (rc == YK_OK && G > 1) {
         if (hipEventCreateWithFlags(&eng->ev_fork, hipEventDisableTiming) != hipSuccess) rc = YK_ERR_HIP;

@@ -511,20 +511,36 @@ int talloc(yk_trainer* t, T** p, size_t count) {
 // [K][M], B stored [N][K]).  64 x 64 output tiles per 256-thread workgroup, each wave a 32 x 32
 // quarter as 2 x 2 blocks of v_mfma_f32_16x16x4_f32 (f32 operands: exact products, f32
 // accumulation, the reference's CPU arithmetic up to summation order), or 32 x 32 tiles (a 16 x 16
-// block per wave) for shapes with few tiles.  K goes through LDS 32 deep,
+// block per wave) for shapes with few tiles.  K goes through LDS 64 (128 for 32 x 32 tiles) deep,
 // the next chunk's global reads issued before the current chunk's MFMAs (coalesced along whichever
 // dimension is contiguous in memory); LDS rows padded by 16 floats, so a wave's 64 fragment reads
 // hit 64 distinct banks (64-wide tiles).  Few output tiles over a long K (dA = dlogits W_pi: K = 3226 over 32
 // tiles) split K over blockIdx.z into partial tiles that k_sgemm_reduce sums in split order (the
 // result does not depend on scheduling: ranks stay bit-identical).
-constexpr int GK = 32;
 template <int TM>  // output tile TM x TM: 64 (each wave a 32 x 32 quarter, 2 x 2 MFMA blocks) or 32 (16 x 16)
-__global__ __launch_bounds__(256) void k_sgemm(int ta, int tb, int M, int N, int K, int kc, const float* __restrict__ A,
-                                               int lda, const float* __restrict__ B, int ldb, float* __restrict__ C,
-                                               int ldc, float beta, float* __restrict__ part) {
-    constexpr int LDA = TM + 16, BL = TM / 32, EPT = TM * GK / 256;  // LDS row; blocks per wave side; elements per thread
-    __shared__ float As[GK][LDA];  // [k][m]
-    __shared__ float Bs[GK][LDA];  // [k][n]
+constexpr int gk_of() { return TM == 64 ? 64 : 128; }  // K per LDS chunk (16 elements per thread either way)
+// An operand tile in LDS keeps its memory order, so the staging stores are as contiguous as the
+// global reads: [k][row] (stride TM + 16) when the row index is contiguous in memory (a transposed
+// operand), else [row][k] (stride GK + 4).  Either way a wave's fragment read - rows l & 15, k
+// (l >> 4) - and its staging store hit 64 distinct banks.
+template <int TM, bool T>
+struct OpTile {
+    static constexpr int GK = gk_of<TM>(), LD = T ? TM + 16 : GK + 4, SZ = T ? GK * LD : TM * LD;
+    __device__ static __forceinline__ int at(int r, int k) { return T ? k * LD + r : r * LD + k; }
+    // element e of the tile (e = tid + 256 i): (row, k) with the memory-contiguous index fastest
+    __device__ static __forceinline__ void rc(int e, int& r, int& k) {
+        if (T) { r = e % TM; k = e / TM; } else { k = e % GK; r = e / GK; }
+    }
+};
+template <int TM, bool TA, bool TB>
+__global__ __launch_bounds__(256) void k_sgemm(int M, int N, int K, int kc, const float* __restrict__ A, int lda,
+                                               const float* __restrict__ B, int ldb, float* __restrict__ C, int ldc,
+                                               float beta, float* __restrict__ part) {
+    using OA = OpTile<TM, TA>;
+    using OB = OpTile<TM, !TB>;  // B[k][n] is "transposed" (n contiguous) when stored [K][N], i.e. !tb
+    constexpr int GK = gk_of<TM>(), BL = TM / 32, EPT = TM * GK / 256;  // blocks per wave side; elements per thread
+    __shared__ float As[OA::SZ];
+    __shared__ float Bs[OB::SZ];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int m0 = blockIdx.y * TM, n0 = blockIdx.x * TM;
     const int kb = blockIdx.z * kc, ke = min(K, kb + kc);
@@ -534,24 +550,17 @@ __global__ __launch_bounds__(256) void k_sgemm(int ta, int tb, int M, int N, int
     for (int i = 0; i < BL; i++)
 #pragma unroll
         for (int j = 0; j < BL; j++) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-    // element e = tid + 256 i of a TM x GK tile: (row, k) with the memory-contiguous index fastest
-    auto a_rc = [&](int e, int& r, int& k) {
-        if (ta) { r = e % TM; k = e / TM; } else { k = e % GK; r = e / GK; }
-    };
-    auto b_rc = [&](int e, int& c, int& k) {
-        if (tb) { k = e % GK; c = e / GK; } else { c = e % TM; k = e / TM; }
-    };
     float av[EPT], bv[EPT];
     auto load = [&](int k0) {
 #pragma unroll
         for (int i = 0; i < EPT; i++) {
             const int e = tid + 256 * i;
             int r, k, c, kk;
-            a_rc(e, r, k);
-            b_rc(e, c, kk);
+            OA::rc(e, r, k);
+            OB::rc(e, c, kk);
             const int gm = m0 + r, gk = k0 + k, gn = n0 + c, gkb = k0 + kk;
-            av[i] = (gm < M && gk < ke) ? (ta ? A[(long)gk * lda + gm] : A[(long)gm * lda + gk]) : 0.f;
-            bv[i] = (gn < N && gkb < ke) ? (tb ? B[(long)gn * ldb + gkb] : B[(long)gkb * ldb + gn]) : 0.f;
+            av[i] = (gm < M && gk < ke) ? (TA ? A[(long)gk * lda + gm] : A[(long)gm * lda + gk]) : 0.f;
+            bv[i] = (gn < N && gkb < ke) ? (TB ? B[(long)gn * ldb + gkb] : B[(long)gkb * ldb + gn]) : 0.f;
         }
     };
     load(kb);
@@ -560,10 +569,10 @@ __global__ __launch_bounds__(256) void k_sgemm(int ta, int tb, int M, int N, int
         for (int i = 0; i < EPT; i++) {
             const int e = tid + 256 * i;
             int r, k, c, kk;
-            a_rc(e, r, k);
-            b_rc(e, c, kk);
-            As[k][r] = av[i];
-            Bs[kk][c] = bv[i];
+            OA::rc(e, r, k);
+            OB::rc(e, c, kk);
+            As[OA::at(r, k)] = av[i];
+            Bs[OB::at(c, kk)] = bv[i];
         }
         __syncthreads();
         if (k0 + GK < ke) load(k0 + GK);  // the next chunk's reads fly under this chunk's MFMAs
@@ -572,9 +581,9 @@ __global__ __launch_bounds__(256) void k_sgemm(int ta, int tb, int M, int N, int
             const int k = ks + (lane >> 4);
             float a[BL], b[BL];
 #pragma unroll
-            for (int i = 0; i < BL; i++) a[i] = As[k][wm + 16 * i + (lane & 15)];
+            for (int i = 0; i < BL; i++) a[i] = As[OA::at(wm + 16 * i + (lane & 15), k)];
 #pragma unroll
-            for (int j = 0; j < BL; j++) b[j] = Bs[k][wn + 16 * j + (lane & 15)];
+            for (int j = 0; j < BL; j++) b[j] = Bs[OB::at(wn + 16 * j + (lane & 15), k)];
 #pragma unroll
             for (int i = 0; i < BL; i++)
 #pragma unroll
@@ -610,7 +619,7 @@ __global__ void k_sgemm_reduce(int M, int N, int S, const float* __restrict__ pa
     float* c = C + (i / N) * ldc + i % N;
     *c = beta != 0.f ? s + beta * *c : s;
 }
-constexpr long GEMM_WS = 1L << 20;  // split-K workspace (floats): splits x M x N, <= 256 32 x 32 tiles' worth
+constexpr long GEMM_WS = 1L << 21;  // split-K workspace (floats): splits x M x N, <= 512 32 x 32 tiles' worth
 // tile size and K split for the shape: 64 x 64 tiles when there are >= 128 of them, else 32 x 32;
 // K split (a partial pass + k_sgemm_reduce) only for long K over few tiles (dA: K = 3226)
 int gemm_rm(hipStream_t s, float* ws, bool ta, bool tb, int M, int N, int K, const float* A, int lda, const float* B,
@@ -618,18 +627,23 @@ int gemm_rm(hipStream_t s, float* ws, bool ta, bool tb, int M, int N, int K, con
     const int t64 = ((M + 63) / 64) * ((N + 63) / 64);
     const int TM = t64 >= 128 ? 64 : 32;
     const int tiles = ((M + TM - 1) / TM) * ((N + TM - 1) / TM);
-    int S = K >= 1024 ? std::max(1, std::min(256 / tiles, K / 512)) : 1;
+    int S = K >= 1024 ? std::max(1, std::min(512 / tiles, K / 256)) : 1;
     while (S > 1 && (long)S * M * N > GEMM_WS) S--;
-    const int kc = ((K + S - 1) / S + GK - 1) / GK * GK;
+    const int GKS = TM == 64 ? gk_of<64>() : gk_of<32>();
+    const int kc = ((K + S - 1) / S + GKS - 1) / GKS * GKS;
     S = (K + kc - 1) / kc;
     const dim3 grid((unsigned)((N + TM - 1) / TM), (unsigned)((M + TM - 1) / TM), (unsigned)S);
     float* part = S > 1 ? ws : nullptr;
-    if (TM == 64)
-        hipLaunchKernelGGL(k_sgemm<64>, grid, dim3(256), 0, s, ta ? 1 : 0, tb ? 1 : 0, M, N, K, kc, A, lda, B, ldb, C,
-                           ldc, beta, part);
-    else
-        hipLaunchKernelGGL(k_sgemm<32>, grid, dim3(256), 0, s, ta ? 1 : 0, tb ? 1 : 0, M, N, K, kc, A, lda, B, ldb, C,
-                           ldc, beta, part);
+#define YK_SGEMM(T, A_, B_) \
+    hipLaunchKernelGGL((k_sgemm<T, A_, B_>), grid, dim3(256), 0, s, M, N, K, kc, A, lda, B, ldb, C, ldc, beta, part)
+    if (TM == 64) {
+        if (ta) { if (tb) YK_SGEMM(64, true, true); else YK_SGEMM(64, true, false); }
+        else { if (tb) YK_SGEMM(64, false, true); else YK_SGEMM(64, false, false); }
+    } else {
+        if (ta) { if (tb) YK_SGEMM(32, true, true); else YK_SGEMM(32, true, false); }
+        else { if (tb) YK_SGEMM(32, false, true); else YK_SGEMM(32, false, false); }
+    }
+#undef YK_SGEMM
     if (S > 1)
         hipLaunchKernelGGL(k_sgemm_reduce, dim3((unsigned)(((long)M * N + 255) / 256)), dim3(256), 0, s, M, N, S, ws, C,
                            ldc, beta);

@@ -384,3 +384,27 @@ def test_incremental_root_scan_equals_full_scan(Y, prior, sims, keep, monkeypatc
     assert s1["scanned"] < s0["scanned"]  # the root's entries are no longer all read every simulation
     for k in ("states", "info", "ctr", "values", "final", "n_moves", "visits_off", "visits"):
         assert np.array_equal(r1[k], r0[k]), k
+
+
+def test_split_descent_launch_gives_identical_trees(Y, monkeypatch):
+    """YK_SPLIT_DESCENT=1 (the measurement knob of tools/expand_split.sh) runs each next descent as
+    its own k_select launch instead of k_expand_backup's tail: the same work, so the same records,
+    stream counters and counters (expansions, UCB entries scanned, edges gathered)."""
+    _, E, N = Y
+    n, sims, seed, base = 160, 25, 808, 4200
+    net = N.YkNet(spec.closed_form_weights(256, 6), 256, 6)
+    out = []
+    for mode in ("0", "1"):
+        monkeypatch.setenv("YK_SPLIT_DESCENT", mode)
+        eng = E.SelfPlayEngine(n, sims, 1.5, 15, net=net, max_moves=48)
+        eng.run(seed, base)
+        st = eng.stats()
+        assert st["errors"] == 0
+        out.append((eng.records(), st))
+        eng.close()
+    (r0, s0), (r1, s1) = out
+    for k in ("expansions", "scanned", "scan_edges", "path_edges", "vnew"):
+        assert s1[k] == s0[k], k
+    assert s0["scan_edges"] > 0
+    for k in ("states", "info", "ctr", "values", "final", "n_moves", "visits_off", "visits"):
+        assert np.array_equal(r1[k], r0[k]), k
