@@ -1,10 +1,11 @@
-// yk_fwd.h - the batched YachtNNet forward of one 16-row tile (forward_tile), shared by the predict
-// kernels (yk_net.hip: k_forward, one workgroup of 8 waves per tile) and the engine's per-tile
-// simulation loop (yk_engine.hip: k_sims_tile, 16 waves - the same code with one column tile per
-// wave).  Device code only; see yk_net.hip for the design notes.
+// yk_fwd.h - the batched YachtNNet forward of one 16-row tile (forward_tile) behind k_forward
+// (yk_net.hip: one workgroup of 8 waves per tile), which the predict entry points and the engine's
+// simulations launch.  Device code only; see yk_net.hip for the design notes.
 #pragma once
 #include "yk_common.h"
 #include "yk_net.h"
+
+#include <type_traits>
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
@@ -597,7 +598,13 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
     }
     W2 w0[2][NT];
     W2 ring[RW][NT];
+    // DUAL (the fp16 mode, one plane: a layer's slices take half the registers): a second ring, so
+    // fc1 and fc2 each have their own - fc1's refills fetch the next block's fc1 and stream through
+    // the row passes of fc1 and fc2, where a one-layer ring is full and the CU's stream stands idle
+    constexpr bool DUAL = PL == 1 && NW == 8 && RW == KS;
+    W2 ring2[DUAL ? RW : 1][NT];
     const float* w_first = net.NB > 0 ? net.w1 : net.w_in;  // (a valid address either way: see below)
+    const float* w_second = net.NB > 0 ? net.w2 : net.w_in;
     if (gw) {
 #pragma unroll
         for (int ks = 0; ks < 2; ks++)
@@ -611,6 +618,12 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
         for (int ks = 0; ks < RW; ks++)
 #pragma unroll
             for (int t = 0; t < NT; t++) ring[ks][t] = ld_w2<PL>(w_first, KS, nt0 + t, ks, lane);
+        if constexpr (DUAL) {
+#pragma unroll
+            for (int ks = 0; ks < RW; ks++)
+#pragma unroll
+                for (int t = 0; t < NT; t++) ring2[ks][t] = ld_w2<PL>(w_second, KS, nt0 + t, ks, lane);
+        }
     }
     __builtin_amdgcn_sched_barrier(0);  // the first layer streams in under the featurize / input phase
     // featurize (state_to_vec, NNet.py:65-86) straight into the input layer's planes, K = 64
@@ -715,13 +728,21 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
     lds_barrier();
 
     // ResidualBlock x NB: h = LN1(SiLU(fc1 x)); h = LN2(SiLU(fc2 h)); x + h  YachtNNet.py:17-21
-    for (int b = 0; b < net.NB; b++) {
+    // The last block is peeled (LAST: its refills stop) so that no branch joins streams of different
+    // lengths inside the loop: at such a join the wait counters merge and the next GEMM's first wait
+    // would drain the refills in flight.
+    auto block = [&](int b, auto last_tag) __attribute__((always_inline)) {
+        constexpr bool LAST = decltype(last_tag)::value;
         const long wo = (long)b * H * H;
         const float* after = net.w1 + wo + (long)H * H;  // the stream after fc2: the next block's fc1
         float4 vb[PB];
 #pragma unroll
         for (int k = 0; k < PB; k++) vb[k] = reinterpret_cast<const float4*>(net.vblk + (long)b * NVB)[min(tid + NTH * k, NB4 - 1)];
-        if (gw) mma_ring<PL, H, NT, RW>(P, SA, ring, acc, net.w1 + wo, net.w2 + wo, nt0);
+        if constexpr (DUAL) {  // fc1 refills with the next block's fc1 (ring), fc2 with its fc2 (ring2)
+            if (gw) mma_ring<PL, H, NT, RW, !LAST>(P, SA, ring, acc, net.w1 + wo, after, nt0);
+        } else {
+            if (gw) mma_ring<PL, H, NT, RW>(P, SA, ring, acc, net.w1 + wo, net.w2 + wo, nt0);
+        }
 #pragma unroll
         for (int k = 0; k < PB; k++)  // the previous block's readers passed a barrier; unconditional
             reinterpret_cast<float4*>(VB)[tid + NTH * k] = vb[k];  // (no branch join after the ring)
@@ -750,8 +771,8 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
         }
         lds_barrier();
         if (gw) {
-            if (b + 1 < net.NB) mma_ring<PL, H, NT, RW>(P, SA, ring, acc, net.w2 + wo, after, nt0);
-            else mma_ring<PL, H, NT, RW, false>(P, SA, ring, acc, net.w2 + wo, nullptr, nt0);
+            if constexpr (DUAL) mma_ring<PL, H, NT, RW, !LAST>(P, SA, ring2, acc, net.w2 + wo, net.w2 + wo + (long)H * H, nt0);
+            else mma_ring<PL, H, NT, RW, !LAST>(P, SA, ring, acc, net.w2 + wo, after, nt0);
         }
         if (gw) store_acc<NT>(T, LD, nt0, acc, nullptr);
         lds_barrier();  // T complete; every wave is done reading h's planes
@@ -771,7 +792,7 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
                     x[rr][i] = x[rr][i] + ld2(X + r * LD + c0 + 2 * i);
                     *reinterpret_cast<f2v*>(X + r * LD + c0 + 2 * i) = x[rr][i];
                 }
-                if (b + 1 < net.NB) put_planes2<PL, VPL / 2>(P, SA, r, c0, x[rr]);  // the next fc1's input
+                if constexpr (!LAST) put_planes2<PL, VPL / 2>(P, SA, r, c0, x[rr]);  // the next fc1's input
             }
         } else {
 #pragma unroll
@@ -786,11 +807,13 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
                     x[i] += X[r * LD + c0 + i];
                     X[r * LD + c0 + i] = x[i];
                 }
-                if (b + 1 < net.NB) put_planes<PL, VPL>(P, SA, r, c0, x);  // the next fc1's input
+                if constexpr (!LAST) put_planes<PL, VPL>(P, SA, r, c0, x);  // the next fc1's input
             }
         }
         lds_barrier();
-    }
+    };
+    for (int b = 0; b + 1 < net.NB; b++) block(b, std::false_type{});
+    if (net.NB > 0) block(net.NB - 1, std::true_type{});
 
     // heads: pi_head = LN -> SiLU -> Linear; v_head = LN -> SiLU -> Linear -> SiLU -> Linear -> tanh.
     // One ring streams v_head.2 (one 16-column tile per wave, first) and then the policy head;

@@ -37,7 +37,8 @@ k = {a: round(b["avg_ms"] * 1000, 2) for a, b in d.get("kernel_ms", {}).items()}
 c = d.get("capacity_use", {})
 print(f"{n:8s} r{r} {d['value'] / 1e6:7.3f}M exp/s  fwd {k.get('forward')}  exp {k.get('expand_backup_select')}  "
       f"sel {k.get('select')}  rs {k.get('root_sort_select')}  mb {k.get('move_begin')}  me {k.get('move_end')}  arena {c.get('max_arena')}/"
-      f"{c.get('arena_cap')}", flush=True)
+      f"{c.get('arena_cap')}" + (f"  f16 {d['predict_f16']['expansions_per_s'] / 1e6:.3f}M fwd16 "
+      f"{round(d['predict_f16'].get('kernel_avg_ms', {}).get('forward', 0) * 1000, 2)}" if 'predict_f16' in d else ""), flush=True)
 EOF
   done
 done
