@@ -156,15 +156,15 @@ FWD = [
     (r"^    const int c0 = lane \* VPL;\n", "after", "    TSTAMP(0);\n"),
     (r"^        if \(w\) atomicOr\(&UM\[lane\], w\);\n    \}\n", "after", "    TSTAMP(1);\n"),
     (r"^    lds_barrier\(\);\n\n    // ResidualBlock x NB", "before_line2", "    TSTAMP(2);\n"),
-    (r"^        if \(gw\) mma_ring<PL, H, NT, RW>\(P, SA, ring, acc, net.w1 \+ wo, net.w2 \+ wo, nt0\);\n", "around",
+    (r"^        if constexpr \(DUAL\) \{  // fc1 refills.*\n.*\n        \} else \{\n.*\n        \}\n", "around",
      ("        if (b == 2) LSTAMP(0);\n", "        if (b == 2) { LSTAMP(1); TSTAMP(16); }\n")),
     (r"^        lds_barrier\(\);  // T complete; every wave is done reading x's planes\n", "around",
      ("        if (b == 2) LSTAMP(2);\n", "        if (b == 2) { LSTAMP(3); TSTAMP(17); }\n")),
-    (r"^        lds_barrier\(\);\n        if \(gw\) \{\n            if \(b \+ 1 < net.NB\)", "around_line1",
+    (r"^        lds_barrier\(\);\n        if \(gw\) \{\n            if constexpr \(DUAL\) mma_ring", "around_line1",
      ("        if (b == 2) LSTAMP(4);\n", "        if (b == 2) { LSTAMP(5); TSTAMP(18); }\n")),
-    (r"^            else mma_ring<PL, H, NT, RW, false>.*\n        \}\n", "after", "        if (b == 2) { LSTAMP(6); TSTAMP(19); }\n"),
+    (r"^            else mma_ring<PL, H, NT, RW, !LAST>.*\n        \}\n", "after", "        if (b == 2) { LSTAMP(6); TSTAMP(19); }\n"),
     (r"^        lds_barrier\(\);  // T complete; every wave is done reading h's planes\n", "after", "        if (b == 2) TSTAMP(21);\n"),
-    (r"^        lds_barrier\(\);\n    \}\n\n    // heads: pi_head", "after_line1", "        if (b < 6) TSTAMP(3 + b);\n"),
+    (r"^        lds_barrier\(\);\n    \};\n    for \(int b = 0; b \+ 1 < net.NB", "after_line1", "        if (b < 6) TSTAMP(3 + b);\n"),
     (r"^    lds_barrier\(\);\n    // The policy head over all real tiles", "after_line1", "    TSTAMP(9);\n"),
     (r"^        for \(int t = 0; t < PC; t\+\+\) tcur\[t\] = tnxt\[t\];\n", "after",
      "        if (c == 1 || c == 3) TSTAMP(10 + (c >> 1));\n        if (c == 5) TSTAMP(12);\n"),
