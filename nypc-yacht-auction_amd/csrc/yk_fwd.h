@@ -177,6 +177,16 @@ __device__ __forceinline__ void mma_ring(const _Float16* A, int sa, W2 (&ring)[R
     for (int t = 0; t < NT; t++) acc[t] = combine<PL>(c[t]);
 }
 
+// slices S0 .. S1-1 of the ring's first fill (the prologue issues the fill in parts)
+template <int PL, int KS, int NT, int RW, int S0, int S1>
+__device__ __forceinline__ void ring_fill_part(W2 (&ring)[RW][NT], const float* __restrict__ W, int nt0) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int ks = S0; ks < S1; ks++)
+#pragma unroll
+        for (int t = 0; t < NT; t++) ring[ks][t] = ld_w2<PL>(W, KS, nt0 + t, ks, lane);
+}
+
 // D[16 x 16] tile t of the wave: lane holds rows 4(l>>4)+j, column 16(nt0 + t) + (l&15).
 // bias == nullptr: raw accumulators (the row pass adds the bias).
 template <int NT>
@@ -566,7 +576,8 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
     // loads in the order they are needed: the static vectors first (their LDS writes must not
     // wait behind the weight stream: vmcnt retires in order), then each wave's two state rows by
     // scalar loads (wave-uniform addresses: SMEM, lgkmcnt), then the weight stream - the input
-    // layer and the trunk ring's first RW slices of fc1 - and only then the features
+    // layer and the first part of fc1's ring fill (the rest between the phases below) - and only
+    // then the features
     float4 vsv[PER];
 #pragma unroll
     for (int k = 0; k < PER; k++) vsv[k] = reinterpret_cast<const float4*>(net.vstat)[min(tid + NTH * k, NV4 - 1)];
@@ -612,19 +623,15 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
             for (int t = 0; t < NT; t++) w0[ks][t] = ld_w2<PL>(net.w_in, 2, nt0 + t, ks, lane);
     }
     __builtin_amdgcn_sched_barrier(0);  // the input layer's slices ahead of the ring's (in-order vmcnt)
-    if (gw) {  // unconditional (no NB > 0 branch): a join here would make every later wait count the
-               // ring as absent and over-wait (the slices are unused when NB = 0)
-#pragma unroll
-        for (int ks = 0; ks < RW; ks++)
-#pragma unroll
-            for (int t = 0; t < NT; t++) ring[ks][t] = ld_w2<PL>(w_first, KS, nt0 + t, ks, lane);
-        if constexpr (DUAL) {
-#pragma unroll
-            for (int ks = 0; ks < RW; ks++)
-#pragma unroll
-                for (int t = 0; t < NT; t++) ring2[ks][t] = ld_w2<PL>(w_second, KS, nt0 + t, ks, lane);
-        }
-    }
+    // The ring's first fill in four parts, one between each of the prologue's phases: a wave issuing
+    // its 32 loads at once stalls ~4.5K cycles on the CU's vector-memory path (which every wave's
+    // loads share), where issued in parts its featurize / tile-mask / input-layer work runs while the
+    // other waves' loads move; each part still lands long before the fc1 GEMM reads it.
+    constexpr int RQ = RW / 4 > 0 ? RW / 4 : 1;
+    constexpr int RQ2 = 2 * RQ < RW ? 2 * RQ : RW, RQ3 = 3 * RQ < RW ? 3 * RQ : RW;
+    // (unconditional - no NB > 0 branch: a join there would make every later wait count the ring as
+    // absent and over-wait; the slices are unused when NB = 0)
+    if (gw) ring_fill_part<PL, KS, NT, RW, 0, RQ>(ring, w_first, nt0);
     __builtin_amdgcn_sched_barrier(0);  // the first layer streams in under the featurize / input phase
     // featurize (state_to_vec, NNet.py:65-86) straight into the input layer's planes, K = 64
     uint32_t vdk[FPT];
@@ -641,6 +648,8 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
         if (lane == 0) VD[rr] = vdr;
         vdk[k] = vdr;
     }
+    if (gw) ring_fill_part<PL, KS, NT, RW, RQ, RQ2>(ring, w_first, nt0);  // part 2 of the first fill
+    __builtin_amdgcn_sched_barrier(0);
     if (tid < TMW) UM[tid] = 0u;
     lds_barrier();
     if (lane < TMW) {  // this wave's rows' tile masks, and into the union (read after the input barrier)
@@ -654,6 +663,8 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
         if (w) atomicOr(&UM[lane], w);
     }
 
+    if (gw) ring_fill_part<PL, KS, NT, RW, RQ2, RQ3>(ring, w_first, nt0);  // part 3
+    __builtin_amdgcn_sched_barrier(0);
     floatx4 acc[NT];
     // inp: Linear -> LayerNorm -> SiLU (-> Dropout, identity in eval)  YachtNNet.py:30-35
     if (gw) {
@@ -673,24 +684,36 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
         store_acc<NT>(T, LD, nt0, acc, nullptr);
     }
     lds_barrier();  // T complete; every wave is done reading the feature planes
-    if (wave == 0) {  // the union as an ascending list, and each tile's rows (read after the trunk)
-        int base = 0;
-#pragma unroll
-        for (int b = 0; b < (PI_TILES + 63) / 64; b++) {
-            const int t = lane + 64 * b;
-            if (t < PI_TILES) {
-                uint32_t rb = 0;
-#pragma unroll
-                for (int r = 0; r < ROWS; r++) rb |= ((RM[r][t >> 5] >> (t & 31)) & 1u) << r;
-                TRB[t] = (uint16_t)rb;
-            }
-            const bool need = t < PI_TILES && ((UM[t >> 5] >> (t & 31)) & 1u);
-            const uint64_t bal = __ballot(need);
-            if (need) TL[base + __popcll(bal & ((1ull << lane) - 1))] = (uint8_t)t;
-            base += __popcll(bal);
-        }
-        if (lane == 0) TC = base;
+    if (gw) {  // part 4 (and the fp16 mode's second ring)
+        ring_fill_part<PL, KS, NT, RW, RQ3, RW>(ring, w_first, nt0);
+        if constexpr (DUAL) ring_fill_part<PL, KS, NT, RW, 0, RW>(ring2, w_second, nt0);
     }
+    __builtin_amdgcn_sched_barrier(0);
+    // the union as an ascending list, and each tile's rows (read by the policy head): chunk c (tiles
+    // 64 c .. 64 c + 63) built by wave c of 0-3, its list offset the union's bits below the chunk.  Built
+    // in block 0, where waves 0-3 wait for the younger waves' fc2 weights, not here on the input
+    // layer's path (one wave building all four chunks there held every wave ~3K cycles).
+    auto build_tiles = [&](int c) __attribute__((always_inline)) {
+        static_assert((PI_TILES + 63) / 64 == 4, "four 64-tile chunks");
+        const int t = lane + 64 * c;
+        if (t < PI_TILES) {
+            uint32_t rb = 0;
+#pragma unroll
+            for (int r = 0; r < ROWS; r++) rb |= ((RM[r][t >> 5] >> (t & 31)) & 1u) << r;
+            TRB[t] = (uint16_t)rb;
+        }
+        int base = 0, tot = 0;
+#pragma unroll
+        for (int j = 0; j < TMW; j++) {
+            const int pc = __popc(UM[j]);
+            base += j < 2 * c ? pc : 0;
+            tot += pc;
+        }
+        const bool need = t < PI_TILES && ((UM[t >> 5] >> (t & 31)) & 1u);
+        const uint64_t bal = __ballot(need);
+        if (need) TL[base + __popcll(bal & ((1ull << lane) - 1))] = (uint8_t)t;
+        if (c == 0 && lane == 0) TC = tot;
+    };
     if constexpr (VPL % 2 == 0) {
         f2v x[RPWN][VPL / 2];
 #pragma unroll
@@ -775,6 +798,7 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
             else mma_ring<PL, H, NT, RW, !LAST>(P, SA, ring, acc, net.w2 + wo, after, nt0);
         }
         if (gw) store_acc<NT>(T, LD, nt0, acc, nullptr);
+        if (b == 0 && wave < 4) build_tiles(wave);  // (waves 0-3: the tile list, above)
         lds_barrier();  // T complete; every wave is done reading h's planes
         if constexpr (VPL % 2 == 0) {
             f2v x[RPWN][VPL / 2];
@@ -814,6 +838,7 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
     };
     for (int b = 0; b + 1 < net.NB; b++) block(b, std::false_type{});
     if (net.NB > 0) block(net.NB - 1, std::true_type{});
+    else if (wave < 4) build_tiles(wave);  // (no block: read after the heads' LayerNorm barrier)
 
     // heads: pi_head = LN -> SiLU -> Linear; v_head = LN -> SiLU -> Linear -> SiLU -> Linear -> tanh.
     // One ring streams v_head.2 (one 16-column tile per wave, first) and then the policy head;

@@ -133,18 +133,38 @@ ENGINE = [
 FWD_GLOBALS = r'''
 // ---- diagnostic hooks (tools/diag_sources.py) ----
 #ifdef YK_TIMING
-__device__ unsigned long long g_tstamp[4096 * 32];
+constexpr int TS_STRIDE = 48;  // stamp slots per workgroup
+__device__ unsigned long long g_tstamp[4096 * TS_STRIDE];
 __device__ unsigned long long g_wstamp[4096 * 16 * 8];  // [workgroup][wave][event] of block 2
 #define TSTAMP(i) \
-    if (threadIdx.x == 0) g_tstamp[blockIdx.x * 32 + (i)] = __builtin_amdgcn_s_memtime()
+    if (threadIdx.x == 0) g_tstamp[blockIdx.x * TS_STRIDE + (i)] = __builtin_amdgcn_s_memtime()
 #define WSTAMP(i) \
-    if ((threadIdx.x & 63) == 0) g_tstamp[blockIdx.x * 32 + (i) + (threadIdx.x >> 6)] = __builtin_amdgcn_s_memtime()
+    if ((threadIdx.x & 63) == 0) g_tstamp[blockIdx.x * TS_STRIDE + (i) + (threadIdx.x >> 6)] = __builtin_amdgcn_s_memtime()
 #define LSTAMP(k) \
     if ((threadIdx.x & 63) == 0) g_wstamp[(blockIdx.x * 16 + (threadIdx.x >> 6)) * 8 + (k)] = __builtin_amdgcn_s_memtime()
+extern "C" int yk_diag_fwd_ts(void* dst, int nwg) {  // the last launch's stamps of workgroups 0 .. nwg-1
+    return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_tstamp), sizeof(unsigned long long) * TS_STRIDE * nwg) == hipSuccess ? 0 : -2;
+}
+// every launch's stamps, summed relative to each workgroup's start (slot 47: workgroups summed)
+__device__ unsigned long long g_tacc[TS_STRIDE];
+#define TACC()                                                                                      \
+    if (threadIdx.x == 0) {                                                                         \
+        const unsigned long long* ts = g_tstamp + blockIdx.x * TS_STRIDE;                           \
+        for (int i = 1; i < TS_STRIDE - 1; i++) atomicAdd(&g_tacc[i], ts[i] - ts[0]);              \
+        atomicAdd(&g_tacc[TS_STRIDE - 1], 1ull);                                                   \
+    }
+extern "C" int yk_diag_fwd_tacc(void* dst, int reset) {
+    if (reset) {
+        static const unsigned long long z[TS_STRIDE] = {};
+        return hipMemcpyToSymbol(HIP_SYMBOL(g_tacc), z, sizeof(z)) == hipSuccess ? 0 : -2;
+    }
+    return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_tacc), sizeof(unsigned long long) * TS_STRIDE) == hipSuccess ? 0 : -2;
+}
 #else
 #define TSTAMP(i)
 #define WSTAMP(i)
 #define LSTAMP(k)
+#define TACC()
 #endif
 '''
 
@@ -154,6 +174,15 @@ __device__ unsigned long long g_wstamp[4096 * 16 * 8];  // [workgroup][wave][eve
 FWD = [
     (r"^constexpr int ROWS = 16;.*\n", "after", FWD_GLOBALS),
     (r"^    const int c0 = lane \* VPL;\n", "after", "    TSTAMP(0);\n"),
+    # the prologue (slots 32-36, 38): static vectors in LDS, the weight loads issued, features
+    # written, the input barrier, the input GEMM done, its barrier passed; block 0's tile-list build (39 -> 37)
+    (r"^        reinterpret_cast<float4\*>\(VS\)\[tid \+ NTH \* k\] = vsv\[k\];.*\n", "after", "    TSTAMP(32);\n"),
+    (r"^    if \(tid < TMW\) UM\[tid\] = 0u;\n    lds_barrier\(\);\n", "around", ("    TSTAMP(33);\n", "    TSTAMP(34);\n")),
+    (r"^    __builtin_amdgcn_sched_barrier\(0\);  // the first layer streams in under the featurize / input phase\n", "after",
+     "    TSTAMP(38);\n"),
+    (r"^    lds_barrier\(\);  // T complete; every wave is done reading the feature planes\n", "around",
+     ("    TSTAMP(35);\n", "    TSTAMP(36);\n")),
+    (r"^        if \(b == 0 && wave < 4\) build_tiles\(wave\);.*\n", "around", ("        if (b == 0) TSTAMP(39);\n", "        if (b == 0) TSTAMP(37);\n")),
     (r"^        if \(w\) atomicOr\(&UM\[lane\], w\);\n    \}\n", "after", "    TSTAMP(1);\n"),
     (r"^    lds_barrier\(\);\n\n    // ResidualBlock x NB", "before_line2", "    TSTAMP(2);\n"),
     (r"^        if constexpr \(DUAL\) \{  // fc1 refills.*\n.*\n        \} else \{\n.*\n        \}\n", "around",
@@ -170,7 +199,7 @@ FWD = [
      "        if (c == 1 || c == 3) TSTAMP(10 + (c >> 1));\n        if (c == 5) TSTAMP(12);\n"),
     (r"^#undef YK_PI_CHUNK\n", "after", "    TSTAMP(14);\n    WSTAMP(24);\n"),
     (r"^        for \(int j = 0; j < 4; j\+\+\) SS\[wave \* ROWS.*\n    \}\n", "after", "    TSTAMP(23);\n"),
-    (r"^            mlse\[\(long\)part \* mstride.*\n        \}\n    \}\n", "after", "    TSTAMP(15);\n"),
+    (r"^            mlse\[\(long\)part \* mstride.*\n        \}\n    \}\n", "after", "    TSTAMP(15);\n    TACC();\n"),
 ]
 
 

@@ -11,6 +11,7 @@
 #   trainab[:R[:amp|f32]] tools/train_ab.sh: head vs base train step, R rounds (default 3, amp)
 #   trainprof   rocprofv3 kernel trace of 30 AMP train steps (tools/prof_train.py) -> gpurun_out/trp_TAG/
 #   divergence  the opt-in 256-game divergence statistic (tests/test_gpu_divergence.py)
+#   fwdts       k_forward's phase stamps inside the engine (YK_TIMING build, tools/diag_fwd_prologue.py)
 #   select      per-phase stamps of the descent / expansion (YK_SEL_TIMING build, tools/diag_select.py)
 #   xspan       per-game launch spans of k_expand_backup (YK_XSPAN build, tools/diag_xspan.py)
 #   amp         per-wave stamps of the AMP train step (YK_AMP_TIMING build, tools/diag_amp.py)
@@ -35,6 +36,7 @@ for r in "$@"; do
               steps+=("trainab:600:bash tools/train_ab.sh ${rounds:-3} ${mode:-amp}") ;;
     trainprof) steps+=("trainprof:200:YK_AMP=1 rocprofv3 --kernel-trace --stats -d gpurun_out/trp_$tag -o tr --output-format csv -- python3 tools/prof_train.py") ;;
     divergence) steps+=("divergence:400:YK_DIVERGENCE_STRIDE=16 YK_DIVERGENCE_TAG=$tag python -u -m pytest tests/test_gpu_divergence.py -x -q -s --timeout 380 --timeout-method thread") ;;
+    fwdts) steps+=("fwdts:200:YK_LIB_PATH=tools/_variants/fwdts/libyacht_hip.so timeout -k 5 180 python -u tools/diag_fwd_prologue.py") ;;
     select) steps+=("select:200:YK_LIB_PATH=tools/_variants/sel/libyacht_hip.so timeout -k 5 180 python -u tools/diag_select.py") ;;
     xspan) steps+=("xspan:200:YK_LIB_PATH=tools/_variants/xspan/libyacht_hip.so timeout -k 5 180 python -u tools/diag_xspan.py") ;;
     amp) steps+=("amp_ts:120:YK_LIB_PATH=tools/_variants/amp/libyacht_hip.so python -u tools/diag_amp.py") ;;

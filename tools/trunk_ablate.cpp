@@ -28,32 +28,32 @@ int main(int argc, char** argv) {
 #ifdef YK_TIMING
     {  // mean s_memtime ticks per phase of wave 0, over the workgroups of the last launch
         const int nb = (n + 15) / 16;
-        std::vector<unsigned long long> t((size_t)nb * 32);
+        std::vector<unsigned long long> t((size_t)nb * TS_STRIDE);
         hipMemcpyFromSymbol(t.data(), HIP_SYMBOL(g_tstamp), sizeof(unsigned long long) * t.size());
         const char* names[16] = {"start", "featurize", "input", "blk0", "blk1", "blk2", "blk3", "blk4", "blk5",
                                  "headLN", "pi01", "pi23", "pi45", "-", "pitail", "end"};
         unsigned long long tmin = ~0ull, tmax = 0;
-        for (int b = 0; b < nb; b++) { tmin = std::min(tmin, t[b * 32]); tmax = std::max(tmax, t[b * 32 + 15]); }
+        for (int b = 0; b < nb; b++) { tmin = std::min(tmin, t[b * TS_STRIDE]); tmax = std::max(tmax, t[b * TS_STRIDE + 15]); }
         printf("launch span %llu ticks; per-WG mean phase ticks:\n", tmax - tmin);
         int prev = 0;
         for (int i = 1; i < 16; i++) {
             if (i == 13) continue;
-            double s = 0; for (int b = 0; b < nb; b++) s += (double)(t[b * 32 + i] - t[b * 32 + prev]);
+            double s = 0; for (int b = 0; b < nb; b++) s += (double)(t[b * TS_STRIDE + i] - t[b * TS_STRIDE + prev]);
             printf("  %-9s %9.0f\n", names[i], s / nb);
             prev = i;
         }
-        double s = 0, mx = 0; for (int b = 0; b < nb; b++) { double d = (double)(t[b * 32 + 15] - t[b * 32]); s += d; mx = std::max(mx, d); }
+        double s = 0, mx = 0; for (int b = 0; b < nb; b++) { double d = (double)(t[b * TS_STRIDE + 15] - t[b * TS_STRIDE]); s += d; mx = std::max(mx, d); }
         printf("  total     %9.0f (max %9.0f)\n", s / nb, mx);
         // block 2 detail (16 fc1 GEMM, 17 LN1 vec+store+barrier, 18 LN1 pass, 19 fc2 GEMM,
         // 20 barrier, 21 store+barrier) and the end phase (22 tail barrier, 23 v store+barrier)
         const int det[][2] = {{4, 16}, {16, 13}, {13, 22}, {22, 17}, {18, 19}, {19, 20}, {20, 5}, {23, 15}};
         const char* dn[] = {"b2.fc1", "b2.ep1st", "b2.ep1bar", "b2.ep1app", "b2.fc2", "b2.ep2", "b2.rest", "vfinal"};
         for (int w = 0; w < 8; w++) {  // per-wave end of the policy head, relative to the heads LN stamp
-            double a = 0; for (int b = 0; b < nb; b++) a += (double)(t[b * 32 + 24 + w] - t[b * 32 + 9]);
+            double a = 0; for (int b = 0; b < nb; b++) a += (double)(t[b * TS_STRIDE + 24 + w] - t[b * TS_STRIDE + 9]);
             printf("  pi.w%d    %9.0f\n", w, a / nb);
         }
         for (int k = 0; k < 8; k++) {
-            double a = 0; for (int b = 0; b < nb; b++) a += (double)(t[b * 32 + det[k][1]] - t[b * 32 + det[k][0]]);
+            double a = 0; for (int b = 0; b < nb; b++) a += (double)(t[b * TS_STRIDE + det[k][1]] - t[b * TS_STRIDE + det[k][0]]);
             printf("  %-9s %9.0f\n", dn[k], a / nb);
         }
         // block 2, per wave (tools/diag_sources.py LSTAMP): fc1 GEMM, accumulator store, first barrier,
