@@ -137,7 +137,9 @@ __device__ __forceinline__ void put_planes(_Float16* planes, int sa, int r, int 
 // weight slices taken from the ring; slice ks lives in slot ks % RW.  After use, the slot is
 // refilled with slice ks + RW of this layer (cur) or, past its end, of the next layer (nxt,
 // same shape).
-template <int PL, int K, int NT, int RW, bool NEXT = true>
+// DEF > 0: the last DEF slots' next-layer refills are left to the caller (ring_fill_part during the
+// row pass that follows, where the CU's vector-memory path is otherwise idle).
+template <int PL, int K, int NT, int RW, bool NEXT = true, int DEF = 0>
 __device__ __forceinline__ void mma_ring(const _Float16* A, int sa, W2 (&ring)[RW][NT], floatx4 (&acc)[NT],
                                          const float* __restrict__ cur, const float* __restrict__ nxt, int nt0) {
     constexpr int KS = K / 32;
@@ -164,7 +166,7 @@ __device__ __forceinline__ void mma_ring(const _Float16* A, int sa, W2 (&ring)[R
             for (int t = 0; t < NT; t++) c[t].c = mfma16(als, w[t].l, c[t].c);
         }
         const int g = ks + RW;
-        if (g < KS || NEXT) {
+        if (g < KS || (NEXT && ks < KS - DEF)) {
 #pragma unroll
             for (int t = 0; t < NT; t++)
                 w[t] = g < KS ? ld_w2<PL>(cur, KS, nt0 + t, g, lane) : ld_w2<PL>(nxt, KS, nt0 + t, g - KS, lane);
@@ -613,6 +615,13 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
     // fc1 and fc2 each have their own - fc1's refills fetch the next block's fc1 and stream through
     // the row passes of fc1 and fc2, where a one-layer ring is full and the CU's stream stands idle
     constexpr bool DUAL = PL == 1 && NW == 8 && RW == KS;
+    // DEF: each trunk GEMM's last DEF ring slots are refilled during the row pass that follows instead
+    // of right after their MFMAs (mma_ring).  A wave's refills stall it while the CU's vector-memory
+    // path is busy with every wave's loads, and that path is otherwise idle during the row passes;
+    // the slices refilled late are the ones the next GEMM reads last.  Measured at 4096 x 100
+    // (profiles/r05l_defer_ab.log): f32-equivalent forward 74.8 -> 72.4 us at 2 (1: 73.5, 3: 72.6),
+    // the fp16 mode 52.4 -> 49.5 us at 4 (6: 50.6, 8: 53.0).
+    constexpr int DEF = (RW == KS && VPL % 2 == 0) ? (PL == 2 ? 2 : 4) : 0;
     W2 ring2[DUAL ? RW : 1][NT];
     const float* w_first = net.NB > 0 ? net.w1 : net.w_in;  // (a valid address either way: see below)
     const float* w_second = net.NB > 0 ? net.w2 : net.w_in;
@@ -758,14 +767,21 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
         constexpr bool LAST = decltype(last_tag)::value;
         const long wo = (long)b * H * H;
         const float* after = net.w1 + wo + (long)H * H;  // the stream after fc2: the next block's fc1
+        // where each GEMM's ring refills from (DUAL: fc1 -> the next block's fc1, fc2 -> its fc2)
+        constexpr bool N1 = DUAL ? !LAST : true, N2 = !LAST;
+        const float* nxt1 = DUAL ? after : net.w2 + wo;
+        const float* nxt2 = DUAL ? net.w2 + wo + (long)H * H : after;
+        // the GEMMs' deferred refills (DEF slots), issued in two parts inside the row pass that follows
+        auto refill = [&](auto& rg, const float* nx, auto part) __attribute__((always_inline)) {
+            constexpr int P0 = decltype(part)::value ? KS - DEF / 2 : KS - DEF;
+            constexpr int P1 = decltype(part)::value ? KS : KS - DEF / 2;
+            if (gw) ring_fill_part<PL, KS, NT, RW, P0, P1>(rg, nx, nt0);
+            __builtin_amdgcn_sched_barrier(0);
+        };
         float4 vb[PB];
 #pragma unroll
         for (int k = 0; k < PB; k++) vb[k] = reinterpret_cast<const float4*>(net.vblk + (long)b * NVB)[min(tid + NTH * k, NB4 - 1)];
-        if constexpr (DUAL) {  // fc1 refills with the next block's fc1 (ring), fc2 with its fc2 (ring2)
-            if (gw) mma_ring<PL, H, NT, RW, !LAST>(P, SA, ring, acc, net.w1 + wo, after, nt0);
-        } else {
-            if (gw) mma_ring<PL, H, NT, RW>(P, SA, ring, acc, net.w1 + wo, net.w2 + wo, nt0);
-        }
+        if (gw) mma_ring<PL, H, NT, RW, N1, DEF>(P, SA, ring, acc, net.w1 + wo, nxt1, nt0);
 #pragma unroll
         for (int k = 0; k < PB; k++)  // the previous block's readers passed a barrier; unconditional
             reinterpret_cast<float4*>(VB)[tid + NTH * k] = vb[k];  // (no branch join after the ring)
@@ -778,7 +794,11 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
 #pragma unroll
                 for (int i = 0; i < VPL / 2; i++)
                     x[rr][i] = silu2(ld2(T + (wave * RPWN + rr) * LD + c0 + 2 * i) + ld2(VB + c0 + 2 * i));
-            layernorm2<VPL / 2, RPWN>(x, VB + H, VB + 2 * H, c0, H);
+            if constexpr (DEF > 0 && N1) refill(ring, nxt1, std::false_type{});
+            float mean[RPWN], rstd[RPWN];
+            ln_stats2<VPL / 2, RPWN>(x, mean, rstd, H);
+            if constexpr (DEF > 0 && N1) refill(ring, nxt1, std::true_type{});
+            ln_apply2<VPL / 2, RPWN>(x, mean, rstd, VB + H, VB + 2 * H, c0);
 #pragma unroll
             for (int rr = 0; rr < RPWN; rr++) put_planes2<PL, VPL / 2>(P, SA, wave * RPWN + rr, c0, x[rr]);  // fc2's input
         } else {
@@ -794,8 +814,8 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
         }
         lds_barrier();
         if (gw) {
-            if constexpr (DUAL) mma_ring<PL, H, NT, RW, !LAST>(P, SA, ring2, acc, net.w2 + wo, net.w2 + wo + (long)H * H, nt0);
-            else mma_ring<PL, H, NT, RW, !LAST>(P, SA, ring, acc, net.w2 + wo, after, nt0);
+            if constexpr (DUAL) mma_ring<PL, H, NT, RW, N2, DEF>(P, SA, ring2, acc, net.w2 + wo, nxt2, nt0);
+            else mma_ring<PL, H, NT, RW, N2, DEF>(P, SA, ring, acc, net.w2 + wo, nxt2, nt0);
         }
         if (gw) store_acc<NT>(T, LD, nt0, acc, nullptr);
         if (b == 0 && wave < 4) build_tiles(wave);  // (waves 0-3: the tile list, above)
@@ -807,7 +827,17 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
 #pragma unroll
                 for (int i = 0; i < VPL / 2; i++)
                     x[rr][i] = silu2(ld2(T + (wave * RPWN + rr) * LD + c0 + 2 * i) + ld2(VB + 3 * H + c0 + 2 * i));
-            layernorm2<VPL / 2, RPWN>(x, VB + 4 * H, VB + 5 * H, c0, H);
+            if constexpr (DEF > 0 && N2) {
+                if constexpr (DUAL) refill(ring2, nxt2, std::false_type{});
+                else refill(ring, nxt2, std::false_type{});
+            }
+            float mean[RPWN], rstd[RPWN];
+            ln_stats2<VPL / 2, RPWN>(x, mean, rstd, H);
+            if constexpr (DEF > 0 && N2) {
+                if constexpr (DUAL) refill(ring2, nxt2, std::true_type{});
+                else refill(ring, nxt2, std::true_type{});
+            }
+            ln_apply2<VPL / 2, RPWN>(x, mean, rstd, VB + 4 * H, VB + 5 * H, c0);
 #pragma unroll
             for (int rr = 0; rr < RPWN; rr++) {
                 const int r = wave * RPWN + rr;
