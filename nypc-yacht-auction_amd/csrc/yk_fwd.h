@@ -622,6 +622,9 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
     // (profiles/r05l_defer_ab.log): f32-equivalent forward 74.8 -> 72.4 us at 2 (1: 73.5, 3: 72.6),
     // the fp16 mode 52.4 -> 49.5 us at 4 (6: 50.6, 8: 53.0).
     constexpr int DEF = (RW == KS && VPL % 2 == 0) ? (PL == 2 ? 2 : 4) : 0;
+    // where in the row pass the two halves go: after the SiLU and after the statistics (f32-equivalent),
+    // after the statistics and after the affine map (fp16 mode; profiles/r05l_defer_pos_ab.log)
+    constexpr bool LATE = PL == 1;
     W2 ring2[DUAL ? RW : 1][NT];
     const float* w_first = net.NB > 0 ? net.w1 : net.w_in;  // (a valid address either way: see below)
     const float* w_second = net.NB > 0 ? net.w2 : net.w_in;
@@ -794,11 +797,12 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
 #pragma unroll
                 for (int i = 0; i < VPL / 2; i++)
                     x[rr][i] = silu2(ld2(T + (wave * RPWN + rr) * LD + c0 + 2 * i) + ld2(VB + c0 + 2 * i));
-            if constexpr (DEF > 0 && N1) refill(ring, nxt1, std::false_type{});
+            if constexpr (DEF > 0 && N1 && !LATE) refill(ring, nxt1, std::false_type{});
             float mean[RPWN], rstd[RPWN];
             ln_stats2<VPL / 2, RPWN>(x, mean, rstd, H);
-            if constexpr (DEF > 0 && N1) refill(ring, nxt1, std::true_type{});
+            if constexpr (DEF > 0 && N1) refill(ring, nxt1, std::integral_constant<bool, !LATE>{});
             ln_apply2<VPL / 2, RPWN>(x, mean, rstd, VB + H, VB + 2 * H, c0);
+            if constexpr (DEF > 0 && N1 && LATE) refill(ring, nxt1, std::true_type{});
 #pragma unroll
             for (int rr = 0; rr < RPWN; rr++) put_planes2<PL, VPL / 2>(P, SA, wave * RPWN + rr, c0, x[rr]);  // fc2's input
         } else {
@@ -819,6 +823,10 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
         }
         if (gw) store_acc<NT>(T, LD, nt0, acc, nullptr);
         if (b == 0 && wave < 4) build_tiles(wave);  // (waves 0-3: the tile list, above)
+        auto refill2 = [&](auto part) __attribute__((always_inline)) {
+            if constexpr (DUAL) refill(ring2, nxt2, part);
+            else refill(ring, nxt2, part);
+        };
         lds_barrier();  // T complete; every wave is done reading h's planes
         if constexpr (VPL % 2 == 0) {
             f2v x[RPWN][VPL / 2];
@@ -827,17 +835,12 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
 #pragma unroll
                 for (int i = 0; i < VPL / 2; i++)
                     x[rr][i] = silu2(ld2(T + (wave * RPWN + rr) * LD + c0 + 2 * i) + ld2(VB + 3 * H + c0 + 2 * i));
-            if constexpr (DEF > 0 && N2) {
-                if constexpr (DUAL) refill(ring2, nxt2, std::false_type{});
-                else refill(ring, nxt2, std::false_type{});
-            }
+            if constexpr (DEF > 0 && N2 && !LATE) refill2(std::false_type{});
             float mean[RPWN], rstd[RPWN];
             ln_stats2<VPL / 2, RPWN>(x, mean, rstd, H);
-            if constexpr (DEF > 0 && N2) {
-                if constexpr (DUAL) refill(ring2, nxt2, std::true_type{});
-                else refill(ring, nxt2, std::true_type{});
-            }
+            if constexpr (DEF > 0 && N2) refill2(std::integral_constant<bool, !LATE>{});
             ln_apply2<VPL / 2, RPWN>(x, mean, rstd, VB + 4 * H, VB + 5 * H, c0);
+            if constexpr (DEF > 0 && N2 && LATE) refill2(std::true_type{});
 #pragma unroll
             for (int rr = 0; rr < RPWN; rr++) {
                 const int r = wave * RPWN + rr;
