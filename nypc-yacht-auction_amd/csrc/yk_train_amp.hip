@@ -193,7 +193,9 @@ __device__ __forceinline__ void write_tl(const _Float16* A, int sa, int col0, in
 // acc[t] = A[16 x K] (fp16 plane in LDS) x W^T over this wave's NT column tiles, weights from the
 // register ring (slice ks in slot ks % RW); a consumed slot is refilled with slice ks + RW of
 // this matrix (cur) or, past its end, of the next one (nxt, same shape; none if null).
-template <int KS, int NT, int RW>
+// DEF > 0: the last DEF slots' next-matrix refills are left to the caller (ring_part during the row
+// pass that follows, where the CU's vector-memory path is otherwise idle; yk_fwd.h mma_ring)
+template <int KS, int NT, int RW, int DEF = 0>
 __device__ __forceinline__ void gemm_ring(const _Float16* A, int sa, float4 (&ring)[RW][NT], floatx4 (&acc)[NT],
                                           const float4* __restrict__ cur, const float4* __restrict__ nxt, int nt0) {
     static_assert(KS % RW == 0, "ring slots align with layers");
@@ -212,8 +214,8 @@ __device__ __forceinline__ void gemm_ring(const _Float16* A, int sa, float4 (&ri
         if (g < KS) {
 #pragma unroll
             for (int t = 0; t < NT; t++) w[t] = cur[((long)(nt0 + t) * KS + g) * 64 + lane];
-        } else {  // the next layer's slices; after the last layer `cur` again (unused): the refills stay
-                  // unconditional, so the wait counters after this loop are exact (no vmcnt(0) drains)
+        } else if (ks < KS - DEF) {  // the next layer's slices; after the last layer `cur` again (unused):
+                  // the refills stay unconditional, so the wait counters after this loop are exact (no vmcnt(0) drains)
             const float4* src = nxt ? nxt : cur;
 #pragma unroll
             for (int t = 0; t < NT; t++) w[t] = src[((long)(nt0 + t) * KS + g - KS) * 64 + lane];
@@ -221,6 +223,18 @@ __device__ __forceinline__ void gemm_ring(const _Float16* A, int sa, float4 (&ri
         __builtin_amdgcn_sched_barrier(0);
         a = an;
     }
+}
+// slots S0 .. S1-1 refilled with the same slices of the next matrix (gemm_ring's deferred refills;
+// RW == KS, so slot s holds slice s of every matrix)
+template <int KS, int NT, int RW, int S0, int S1>
+__device__ __forceinline__ void ring_part(float4 (&ring)[RW][NT], const float4* __restrict__ W, int nt0) {
+    static_assert(RW == KS || S0 == S1, "deferred refills need a one-matrix ring");
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int s = S0; s < S1; s++)
+#pragma unroll
+        for (int t = 0; t < NT; t++) ring[s][t] = W[((long)(nt0 + t) * KS + s) * 64 + lane];
+    __builtin_amdgcn_sched_barrier(0);
 }
 template <int KS, int NT, int RW>
 __device__ __forceinline__ void ring_fill(float4 (&ring)[RW][NT], const float4* __restrict__ W, int nt0) {
@@ -322,6 +336,11 @@ __global__ __launch_bounds__(TTHR) void k_amp_fwd(AmpDev d, const yk_state_t* __
     constexpr int LD = H + 4, SA = H + 8, VPL = H / 64, KS = H / 32;
     constexpr int NT = H >= 128 ? H / 128 : 1, NACT = H / (16 * NT);
     constexpr int RW = KS * NT <= 16 ? KS : 16 / NT;
+    // each trunk GEMM's last FDEF ring slots are refilled in the row pass that follows (gemm_ring): the
+    // refills stall a wave while every wave's loads share the CU's vector-memory path, which is idle
+    // during the row passes.  AMP step 122.6 -> 115.3 us with 6 in both kernels (4: 116.0, 8: 116.5;
+    // profiles/r05m_amp_defer_*trainab.log)
+    constexpr int FDEF = RW == KS ? 6 : 0;
     __shared__ __attribute__((aligned(16))) float Xs[TR * LD];
     __shared__ __attribute__((aligned(16))) float Ts[TR * LD];
     __shared__ __attribute__((aligned(16))) _Float16 Pa[TR * SA];
@@ -448,8 +467,9 @@ __global__ __launch_bounds__(TTHR) void k_amp_fwd(AmpDev d, const yk_state_t* __
             }
             const float4* cur = (half == 0 ? d.w1f : d.w2f) + b * HH8;
             const float4* nxt = half == 0 ? d.w2f + b * HH8 : (b + 1 < NB ? d.w1f + (b + 1) * HH8 : nullptr);
+            const float4* dsrc = nxt ? nxt : cur;  // the deferred refills' matrix (as gemm_ring's)
             if (gw) {
-                gemm_ring<KS, NT, RW>(Pa, SA, ring, acc, cur, nxt, nt0);
+                gemm_ring<KS, NT, RW, FDEF>(Pa, SA, ring, acc, cur, nxt, nt0);
                 store_acc<NT>(Ts, LD, nt0, acc);
             }
 #pragma unroll
@@ -457,6 +477,9 @@ __global__ __launch_bounds__(TTHR) void k_amp_fwd(AmpDev d, const yk_state_t* __
             lds_barrier();
             float* U = (half == 0 ? d.u1 : d.u2) + (long)b * d.Bmax * H;
             const int L = 1 + 2 * b + half;
+            // the GEMM's deferred refills, half before the row pass and half after it (unconditional:
+            // every row of the tile reads the next GEMM's weights)
+            if constexpr (FDEF > 0) if (gw) ring_part<KS, NT, RW, KS - FDEF, KS - FDEF / 2>(ring, dsrc, nt0);
 #pragma unroll
             for (int rr = 0; rr < TRPW; rr++) {
                 const int r = wave * TRPW + rr, row = row0 + r;
@@ -495,6 +518,7 @@ __global__ __launch_bounds__(TTHR) void k_amp_fwd(AmpDev d, const yk_state_t* __
                     Pa[r * SA + c0 + i] = (_Float16)x[i];
                 }
             }
+            if constexpr (FDEF > 0) if (gw) ring_part<KS, NT, RW, KS - FDEF / 2, KS>(ring, dsrc, nt0);
             lds_barrier();
             if (half == 0) write_tl<TRV>(Pa, SA, 0, H, d.r1T + (long)b * (H / 16) * d.RS * 512, d.RS, 0, tile, zero_rest);
             else if (b + 1 < NB)
@@ -938,6 +962,7 @@ __global__ __launch_bounds__(TTHR) void k_amp_bwd(AmpDev d, int B, float p, uint
     constexpr int LD = H + 4, SA = H + 8, VPL = H / 64, KS = H / 32;
     constexpr int NT = H >= 128 ? H / 128 : 1, NACT = H / (16 * NT);
     constexpr int RW = KS * NT <= 16 ? KS : 16 / NT;
+    constexpr int BDEF = RW == KS ? 6 : 0;  // deferred ring refills per trunk GEMM (k_amp_fwd's FDEF)
     constexpr int SV = VH + 8;
     static_assert(SV <= SA || H == 64, "dz1 rows fit the plane buffer");
     __shared__ __attribute__((aligned(16))) float Xs[TR * LD];
@@ -1025,7 +1050,13 @@ __global__ __launch_bounds__(TTHR) void k_amp_bwd(AmpDev d, int B, float p, uint
                     NB > 0 ? t_blk(NB - 1, 6) : (int)T_GIN, NB > 0 ? t_blk(NB - 1, 7) : (int)T_BEIN, row0, B, 0, drop);
     __builtin_amdgcn_sched_barrier(0);
     float4 ring[RW][NT];
-    if (gw) ring_fill<KS, NT, RW>(ring, NB > 0 ? d.w2t + (NB - 1) * HH8 : d.wpit, nt0);
+    // (the first trunk GEMM's last BDEF slots are loaded in the row pass before it, as every later
+    // GEMM's: gemm_ring's deferred refills)
+    if (gw) {
+        const float4* first = NB > 0 ? d.w2t + (NB - 1) * HH8 : d.wpit;
+        if constexpr (BDEF > 0) ring_part<KS, NT, RW, 0, KS - BDEF>(ring, first, nt0);
+        else ring_fill<KS, NT, RW>(ring, first, nt0);
+    }
     lds_barrier();
     // heads backward (YachtNNet.py:40-52): dT = dA SiLU'(T) for both heads (f32), one LayerNorm
     // backward over the shared statistics -> dh
@@ -1076,6 +1107,10 @@ __global__ __launch_bounds__(TTHR) void k_amp_bwd(AmpDev d, int B, float p, uint
         for (int half = 1; half >= 0; half--) {
             // row pass: (half 1) dL2 = dh; (half 0) dL1 = Dropout'(fp16(dR1)).  LayerNorm backward on
             // S = fp16(SiLU(U)), dU = fp16(fp16(dS) SiLU'(U)); partials: gamma, beta, bias
+            const float4* cur = (half == 1 ? d.w2t : d.w1t) + b * HH8;
+            // this step's GEMM's last BDEF slots (the previous GEMM deferred them), half before the row
+            // pass and half after it
+            if constexpr (BDEF > 0) if (gw) ring_part<KS, NT, RW, KS - BDEF, KS - BDEF / 2>(ring, cur, nt0);
 #pragma unroll
             for (int rr = 0; rr < TRPW; rr++) {
                 const int r = wave * TRPW + rr, row = row0 + r;
@@ -1105,6 +1140,7 @@ __global__ __launch_bounds__(TTHR) void k_amp_bwd(AmpDev d, int B, float p, uint
                     Pa[r * SA + c0 + i] = (_Float16)dx[i];
                 }
             }
+            if constexpr (BDEF > 0) if (gw) ring_part<KS, NT, RW, KS - BDEF / 2, KS>(ring, cur, nt0);
             lds_barrier();
             flush_gbb<H>(d, CP, tile, CV_BLK + 6 * b + (half == 0 ? 0 : 3));
             write_tl<TRV>(Pa, SA, 0, H, (half == 0 ? d.du1T : d.du2T) + b * TLH, d.RS, 0, tile, zero_rest);
@@ -1119,10 +1155,9 @@ __global__ __launch_bounds__(TTHR) void k_amp_bwd(AmpDev d, int B, float p, uint
                 row_prefetch<H>(R, d, Up, Lp, tg, tb, row0, B, h1 ? 1 + b : 0, drop);  // (next: b's fc1 dropout / inp's)
             }
             __builtin_amdgcn_sched_barrier(0);
-            const float4* cur = (half == 1 ? d.w2t : d.w1t) + b * HH8;
             const float4* nxt = half == 1 ? d.w1t + b * HH8 : (b > 0 ? d.w2t + (b - 1) * HH8 : nullptr);
             if (gw) {
-                gemm_ring<KS, NT, RW>(Pa, SA, ring, acc, cur, nxt, nt0);
+                gemm_ring<KS, NT, RW, BDEF>(Pa, SA, ring, acc, cur, nxt, nt0);
                 store_acc<NT>(Ts, LD, nt0, acc);
             }
             lds_barrier();

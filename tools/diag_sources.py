@@ -221,8 +221,8 @@ extern "C" int yk_diag_amp_ts(void* dst) {
 # passed, 3 the row pass done, 4 the next barrier passed, 5 the T-layout store done
 AMP = [
     (r"^constexpr int SQ_BLOCKS = 1024;\n", "after", AMP_GLOBALS),
-    (r"^            const float4\* nxt = half == 0 \? d.w2f.*\n            if \(gw\) \{\n"
-     r"                gemm_ring<KS, NT, RW>\(Pa, SA, ring, acc, cur, nxt, nt0\);\n"
+    (r"^            const float4\* nxt = half == 0 \? d.w2f.*\n            const float4\* dsrc.*\n            if \(gw\) \{\n"
+     r"                gemm_ring<KS, NT, RW, FDEF>\(Pa, SA, ring, acc, cur, nxt, nt0\);\n"
      r"                store_acc<NT>\(Ts, LD, nt0, acc\);\n            \}\n", "around",
      ("            AMP_STAMP(0, 0);\n", "            AMP_STAMP(0, 1);\n")),
     (r"^            lds_barrier\(\);\n            float\* U = ", "after_line1", "            AMP_STAMP(0, 2);\n"),
@@ -237,10 +237,10 @@ AMP = [
      ("            AMP_STAMP(1, 1);\n", "            AMP_STAMP(1, 2);\n")),
     (r"^            flush_gbb<H>\(d, CP, tile, CV_BLK.*\n", "after", "            AMP_STAMP(1, 3);\n"),
     (r"^            write_tl<TRV>\(Pa, SA, 0, H, \(half == 0 \? d.du1T.*\n", "after", "            AMP_STAMP(1, 4);\n"),
-    (r"^            __builtin_amdgcn_sched_barrier\(0\);\n            const float4\* cur = \(half == 1", "after_line1",
+    (r"^            __builtin_amdgcn_sched_barrier\(0\);\n            const float4\* nxt = half == 1", "after_line1",
      "            AMP_STAMP(1, 5);\n"),
     (r"^            const float4\* nxt = half == 1 \? d.w1t.*\n            if \(gw\) \{\n"
-     r"                gemm_ring<KS, NT, RW>\(Pa, SA, ring, acc, cur, nxt, nt0\);\n"
+     r"                gemm_ring<KS, NT, RW, BDEF>\(Pa, SA, ring, acc, cur, nxt, nt0\);\n"
      r"                store_acc<NT>\(Ts, LD, nt0, acc\);\n            \}\n", "after", "            AMP_STAMP(1, 6);\n"),
     (r"^            lds_barrier\(\);\n            if \(half == 0\) \{  // residual", "after_line1",
      "            AMP_STAMP(1, 7);\n"),

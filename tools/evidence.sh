@@ -8,7 +8,7 @@
 #   prof        tools/profile_bench.sh TAG: rocprofv3 kernel trace + FETCH/WRITE/MFMA passes
 #   ab[:R[:V..]] tools/ab_bench.sh R (default 3) head vs base [vs variants V = NAME=FLAGS]
 #   train       the AMP and the f32 train step times (tools/train_time.py, 512 examples)
-#   trainab[:R[:amp|f32]] tools/train_ab.sh: head vs base train step, R rounds (default 3, amp)
+#   trainab[:R[:amp|f32[:V,..]]] tools/train_ab.sh: head vs base [vs prebuilt variants V] train step
 #   trainprof   rocprofv3 kernel trace of 30 AMP train steps (tools/prof_train.py) -> gpurun_out/trp_TAG/
 #   divergence  the opt-in 256-game divergence statistic (tests/test_gpu_divergence.py)
 #   fwdts       k_forward's phase stamps inside the engine (YK_TIMING build, tools/diag_fwd_prologue.py)
@@ -32,8 +32,8 @@ for r in "$@"; do
     ab*) IFS=: read -r _ rounds rest <<< "$r"
          steps+=("ab:900:bash tools/ab_bench.sh ${rounds:-3} ${rest//,/ }") ;;
     train) steps+=("t_amp:120:YK_AMP=1 python -u tools/train_time.py 512" "t_f32:120:python -u tools/train_time.py 512") ;;
-    trainab*) IFS=: read -r _ rounds mode <<< "$r"
-              steps+=("trainab:600:bash tools/train_ab.sh ${rounds:-3} ${mode:-amp}") ;;
+    trainab*) IFS=: read -r _ rounds mode vars <<< "$r"
+              steps+=("trainab:600:bash tools/train_ab.sh ${rounds:-3} ${mode:-amp} ${vars//,/ }") ;;
     trainprof) steps+=("trainprof:200:YK_AMP=1 rocprofv3 --kernel-trace --stats -d gpurun_out/trp_$tag -o tr --output-format csv -- python3 tools/prof_train.py") ;;
     divergence) steps+=("divergence:400:YK_DIVERGENCE_STRIDE=16 YK_DIVERGENCE_TAG=$tag python -u -m pytest tests/test_gpu_divergence.py -x -q -s --timeout 380 --timeout-method thread") ;;
     fwdts) steps+=("fwdts:200:YK_LIB_PATH=tools/_variants/fwdts/libyacht_hip.so timeout -k 5 180 python -u tools/diag_fwd_prologue.py") ;;
