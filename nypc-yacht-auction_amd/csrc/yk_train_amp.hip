@@ -380,7 +380,15 @@ __global__ __launch_bounds__(TTHR) void k_amp_fwd(AmpDev d, const yk_state_t* __
 #pragma unroll
         for (int i = 0; i < VPL; i++) hg[v][i] = d.P[poff(H, d.NB, t_head(NB, v == 0 ? HP_G : v == 1 ? HP_B : v == 2 ? HV_G : HV_B)) + c0 + i];
     float4 ring[RW][NT];
-    if (gw) ring_fill<KS, NT, RW>(ring, NB > 0 ? d.w1f : d.wpif, nt0);  // (whatever NB is: no branch join)
+    // the first block's ring (whatever NB is: no branch join), in four parts between the prologue's
+    // phases when RW == KS (a wave issuing all of them at once stalls on the CU's vector-memory path
+    // while the other waves' loads move; yk_fwd.h's prologue does the same)
+    const float4* wfirst = NB > 0 ? d.w1f : d.wpif;
+    constexpr bool PARTS = RW == KS && KS % 4 == 0;
+    if (gw) {
+        if constexpr (PARTS) ring_part<KS, NT, RW, 0, KS / 4>(ring, wfirst, nt0);
+        else ring_fill<KS, NT, RW>(ring, wfirst, nt0);
+    }
 #pragma unroll
     for (int k = 0; k < 2; k++) {  // state_to_vec (NNet.py:65-86), K padded to 64 (rows past TRV: zeros)
         const int r = wave + TW * k, row = row0 + r;
@@ -395,6 +403,7 @@ __global__ __launch_bounds__(TTHR) void k_amp_fwd(AmpDev d, const yk_state_t* __
         }
         Pa[r * SA + lane] = (_Float16)x;
     }
+    if constexpr (PARTS) if (gw) ring_part<KS, NT, RW, KS / 4, KS / 2>(ring, wfirst, nt0);
     lds_barrier();
     write_tl<TRV>(Pa, SA, 0, 64, d.xT, d.RS, 0, tile, zero_rest);
     floatx4 acc[NT];
@@ -410,6 +419,7 @@ __global__ __launch_bounds__(TTHR) void k_amp_fwd(AmpDev d, const yk_state_t* __
         }
         store_acc<NT>(Ts, LD, nt0, acc);
     }
+    if constexpr (PARTS) if (gw) ring_part<KS, NT, RW, KS / 2, 3 * KS / 4>(ring, wfirst, nt0);
     lds_barrier();
     // inp.1-3: LayerNorm (f32) -> SiLU -> Dropout  YachtNNet.py:30-35
 #pragma unroll
@@ -444,6 +454,7 @@ __global__ __launch_bounds__(TTHR) void k_amp_fwd(AmpDev d, const yk_state_t* __
             Pa[r * SA + c0 + i] = (_Float16)x[i];
         }
     }
+    if constexpr (PARTS) if (gw) ring_part<KS, NT, RW, 3 * KS / 4, KS>(ring, wfirst, nt0);
     lds_barrier();
     if (NB > 0) write_tl<TRV>(Pa, SA, 0, H, d.hT, d.RS, 0, tile, zero_rest);
 

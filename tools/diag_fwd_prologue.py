@@ -1,7 +1,7 @@
 """Diagnostic: k_forward's phases inside the engine (the -DYK_TIMING library: tools/evidence.sh fwdts).
 
 Runs self-play batches at the bench shape; each workgroup of every forward launch adds its wave-0
-stamps (tools/diag_sources.py: slots 1-15 the phases, 32-39 the prologue and the tile list) relative to its start
+stamps (tools/diag_sources.py: slots 1-15 the phases, 32-40 the prologue, the tile list and the v_head.2 chunk) relative to its start
 into a device accumulator, read after the batch.  Ticks are s_memtime counts."""
 import ctypes as C
 import os
@@ -28,7 +28,7 @@ L.yk_diag_fwd_tacc.argtypes = [C.c_void_p, C.c_int]
 seq = [("vstat->LDS", 0, 32), ("weights issued (w0)", 32, 38), ("features", 38, 33), ("input barrier", 33, 34),
        ("tile masks", 34, 1), ("input GEMM", 1, 35), ("input T barrier", 35, 36),
        ("input row pass", 36, 2), ("blk0", 2, 3), ("blk1", 3, 4), ("blk2", 4, 5), ("blk3", 5, 6), ("blk4", 6, 7),
-       ("blk5", 7, 8), ("heads LN", 8, 9), ("policy head", 9, 14), ("end", 14, 15),
+       ("blk5", 7, 8), ("heads LN", 8, 9), ("v_head.2 chunk", 9, 40), ("policy chunks", 40, 14), ("end", 14, 15),
        ("(blk0: wave 0's tile-list chunk)", 39, 37)]
 eng.run(0, 0)  # warm-up
 torch.cuda.synchronize()

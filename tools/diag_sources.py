@@ -197,6 +197,7 @@ FWD = [
     (r"^    lds_barrier\(\);\n    // The policy head over all real tiles", "after_line1", "    TSTAMP(9);\n"),
     (r"^        for \(int t = 0; t < PC; t\+\+\) tcur\[t\] = tnxt\[t\];\n", "after",
      "        if (c == 1 || c == 3) TSTAMP(10 + (c >> 1));\n        if (c == 5) TSTAMP(12);\n"),
+    (r"^    float sm\[4\], ss\[4\];  // running max", "before", "    TSTAMP(40);\n"),
     (r"^#undef YK_PI_CHUNK\n", "after", "    TSTAMP(14);\n    WSTAMP(24);\n"),
     (r"^        for \(int j = 0; j < 4; j\+\+\) SS\[wave \* ROWS.*\n    \}\n", "after", "    TSTAMP(23);\n"),
     (r"^            mlse\[\(long\)part \* mstride.*\n        \}\n    \}\n", "after", "    TSTAMP(15);\n    TACC();\n"),
