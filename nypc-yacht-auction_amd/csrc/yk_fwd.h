@@ -139,9 +139,13 @@ __device__ __forceinline__ void put_planes(_Float16* planes, int sa, int r, int 
 // same shape).
 // DEF > 0: the last DEF slots' next-layer refills are left to the caller (ring_fill_part during the
 // row pass that follows, where the CU's vector-memory path is otherwise idle).
-template <int PL, int K, int NT, int RW, bool NEXT = true, int DEF = 0>
+// VH (the last trunk GEMM, RW == KS): each consumed slot's first tile is refilled with slice ks of
+// tile `vt` of nxt (v_head.2's weights, read from the ring by the head).
+template <int PL, int K, int NT, int RW, bool NEXT = true, int DEF = 0, bool VH = false>
 __device__ __forceinline__ void mma_ring(const _Float16* A, int sa, W2 (&ring)[RW][NT], floatx4 (&acc)[NT],
-                                         const float* __restrict__ cur, const float* __restrict__ nxt, int nt0) {
+                                         const float* __restrict__ cur, const float* __restrict__ nxt, int nt0,
+                                         int vt = 0) {
+    static_assert(!VH || (RW == K / 32 && !NEXT), "the v_head.2 refill replaces a one-layer ring's last refills");
     constexpr int KS = K / 32;
     const int lane = threadIdx.x & 63;
     const APtr ap = a_ptr(A, sa);
@@ -170,6 +174,8 @@ __device__ __forceinline__ void mma_ring(const _Float16* A, int sa, W2 (&ring)[R
 #pragma unroll
             for (int t = 0; t < NT; t++)
                 w[t] = g < KS ? ld_w2<PL>(cur, KS, nt0 + t, g, lane) : ld_w2<PL>(nxt, KS, nt0 + t, g - KS, lane);
+        } else if constexpr (VH) {
+            w[0] = ld_w2<PL>(nxt, KS, vt, ks, lane);
         }
         __builtin_amdgcn_sched_barrier(0);  // keep the refill here, a ring's depth ahead of its use
         ah = ahn;
@@ -622,6 +628,12 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
     // (profiles/r05l_defer_ab.log): f32-equivalent forward 74.8 -> 72.4 us at 2 (1: 73.5, 3: 72.6),
     // the fp16 mode 52.4 -> 49.5 us at 4 (6: 50.6, 8: 53.0).
     constexpr int DEF = (RW == KS && VPL % 2 == 0) ? (PL == 2 ? 2 : 4) : 0;
+    // VHP: v_head.2's weights (one 16-column tile per wave) stream into the trunk ring's slots during
+    // the last trunk GEMM, whose slots otherwise go unrefilled, so the head computes that layer from
+    // registers while its ring fetches the first policy chunk (streamed behind the heads' LayerNorm,
+    // v_head.2 took ~11.6K of a workgroup's ~158K cycles: profiles/r05n_forward_phases.txt)
+    constexpr bool VHP = RW == KS && NW == 8 && NACT == NW;  // (every wave runs the trunk GEMMs)
+    const int vwave = wave & 7;  // v_head.2's tile: 8 of them (16 waves: waves 8-15 redo 0-7, unstored)
     // where in the row pass the two halves go: after the SiLU and after the statistics (f32-equivalent),
     // after the statistics and after the affine map (fp16 mode; profiles/r05l_defer_pos_ab.log)
     constexpr bool LATE = PL == 1;
@@ -818,8 +830,11 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
         }
         lds_barrier();
         if (gw) {
-            if constexpr (DUAL) mma_ring<PL, H, NT, RW, N2, DEF>(P, SA, ring2, acc, net.w2 + wo, nxt2, nt0);
-            else mma_ring<PL, H, NT, RW, N2, DEF>(P, SA, ring, acc, net.w2 + wo, nxt2, nt0);
+            // (the last block: v_head.2's tile into the consumed slots, VHP)
+            constexpr bool V = LAST && VHP;
+            const float* n2 = V ? net.w_v1 : nxt2;
+            if constexpr (DUAL) mma_ring<PL, H, NT, RW, N2, DEF, V>(P, SA, ring2, acc, net.w2 + wo, n2, nt0, vwave);
+            else mma_ring<PL, H, NT, RW, N2, DEF, V>(P, SA, ring, acc, net.w2 + wo, n2, nt0, vwave);
         }
         if (gw) store_acc<NT>(T, LD, nt0, acc, nullptr);
         if (b == 0 && wave < 4) build_tiles(wave);  // (waves 0-3: the tile list, above)
@@ -881,10 +896,11 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
     _Float16* PV = reinterpret_cast<_Float16*>(T);
     // chunk width: 4 tiles per wave at 8 waves; 2 at 16 waves (128 VGPRs), the same bytes in flight
     constexpr int PC = NW == 16 ? 2 : PCH;
-    const int vwave = wave & 7;  // v_head.2's tile: 8 of them (16 waves: waves 8-15 redo 0-7, unstored)
     W2 pring[RD][PC];
+    if constexpr (!VHP) {
 #pragma unroll
-    for (int ks = 0; ks < RD; ks++) pring[ks][0] = ld_w2<PL>(net.w_v1, KS, vwave, ks, lane);
+        for (int ks = 0; ks < RD; ks++) pring[ks][0] = ld_w2<PL>(net.w_v1, KS, vwave, ks, lane);
+    }
     if constexpr (VPL % 2 == 0) {
         // both heads' LayerNorms see the same row: one set of statistics, two affine maps
         f2v x[RPWN][VPL / 2], y[RPWN][VPL / 2];
@@ -978,7 +994,30 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
     const float* bpi = VS + vs_bpi(H);
     int tcur[PC], tnxt[PC];
     chunk_tiles(0, tcur);
-    {
+    if constexpr (VHP) {
+        // the first policy chunk's first RD slices (every slot: a short chunk's extra ones read tile 0),
+        // then v_head.2 from the trunk ring (slice ks of tile vwave in slot ks, tile 0; same products
+        // and order as ring_chunk's)
+#pragma unroll
+        for (int ks = 0; ks < RD; ks++)
+#pragma unroll
+            for (int t = 0; t < PC; t++) pring[ks][t] = ld_w2<PL>(net.w_pi, KS, tcur[t], ks, lane);
+        __builtin_amdgcn_sched_barrier(0);
+        auto vhead = [&](auto& vr) __attribute__((always_inline)) {
+            const APtr ap = a_ptr(PV, SA);
+            Acc3 c;
+            acc_zero(c);
+#pragma unroll
+            for (int ks = 0; ks < KS; ks++) {
+                const float4 ah = ld_a(ap.h, ks);
+                const float4 al = PL == 2 ? ld_a(ap.l, ks) : ah;
+                mma3<PL>(c, ah, al, vr[ks][0]);
+            }
+            av[0] = combine<PL>(c);
+        };
+        if constexpr (DUAL) vhead(ring2);
+        else vhead(ring);
+    } else {
         int vt[PC] = {};
         vt[0] = vwave;
         static_assert(PC == 4 || PC == 2, "chunk-shape dispatch below");

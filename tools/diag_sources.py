@@ -189,9 +189,9 @@ FWD = [
      ("        if (b == 2) LSTAMP(0);\n", "        if (b == 2) { LSTAMP(1); TSTAMP(16); }\n")),
     (r"^        lds_barrier\(\);  // T complete; every wave is done reading x's planes\n", "around",
      ("        if (b == 2) LSTAMP(2);\n", "        if (b == 2) { LSTAMP(3); TSTAMP(17); }\n")),
-    (r"^        lds_barrier\(\);\n        if \(gw\) \{\n            if constexpr \(DUAL\) mma_ring", "around_line1",
+    (r"^        lds_barrier\(\);\n        if \(gw\) \{\n            // \(the last block: v_head", "around_line1",
      ("        if (b == 2) LSTAMP(4);\n", "        if (b == 2) { LSTAMP(5); TSTAMP(18); }\n")),
-    (r"^            else mma_ring<PL, H, NT, RW, N2, DEF>.*\n        \}\n", "after", "        if (b == 2) { LSTAMP(6); TSTAMP(19); }\n"),
+    (r"^            else mma_ring<PL, H, NT, RW, N2, DEF, V>.*\n        \}\n", "after", "        if (b == 2) { LSTAMP(6); TSTAMP(19); }\n"),
     (r"^        lds_barrier\(\);  // T complete; every wave is done reading h's planes\n", "after", "        if (b == 2) TSTAMP(21);\n"),
     (r"^        lds_barrier\(\);\n    \};\n    for \(int b = 0; b \+ 1 < net.NB", "after_line1", "        if (b < 6) TSTAMP(3 + b);\n"),
     (r"^    lds_barrier\(\);\n    // The policy head over all real tiles", "after_line1", "    TSTAMP(9);\n"),
