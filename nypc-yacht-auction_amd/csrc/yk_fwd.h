@@ -968,10 +968,9 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
         const uint32_t md = VD[r] & 0xF;
         return md == LM_ALL || (md != LM_NONE && net.pi_bspread + 2.f * net.pi_wmax * sqrtf(HN[r]) > FULL_SPREAD);
     };
-    bool full = false;
-#pragma unroll
-    for (int r = 0; r < ROWS; r++) full |= row_allc(r);
-    full = __builtin_amdgcn_readfirstlane(full ? 1 : 0) != 0;
+    // lane r < ROWS decides row r (one round of LDS reads for all rows, not a chain of 16)
+    const uint32_t allrows = (uint32_t)__ballot(lane < ROWS && row_allc(lane));
+    const bool full = allrows != 0u;
     const int cnt_all = full ? REAL_TILES : __builtin_amdgcn_readfirstlane(TC);
     const int lo = cnt_all * part / parts, cnt = cnt_all * (part + 1) / parts - lo;  // this part's slice
     // this wave's list entries k = 0 .. m-1 (list index lo + wave + NW k): nf full chunks in list
@@ -1039,7 +1038,7 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
     for (int j = 0; j < 4; j++) {
         sm[j] = -INFINITY;
         ss[j] = 0.f;
-        allc[j] = row_allc(4 * (lane >> 4) + j);
+        allc[j] = (allrows >> (4 * (lane >> 4) + j)) & 1u;
     }
 #define YK_PI_CHUNK(NTL, NXT) \
     pi_chunk<PL, KS, NTL, NXT, PC>(P, SA, pring, net.w_pi, tcur, tnxt, bpi, logits, row0, n, sm, ss, TRB, allc)

@@ -28,7 +28,8 @@ L.yk_diag_fwd_tacc.argtypes = [C.c_void_p, C.c_int]
 seq = [("vstat->LDS", 0, 32), ("weights issued (w0)", 32, 38), ("features", 38, 33), ("input barrier", 33, 34),
        ("tile masks", 34, 1), ("input GEMM", 1, 35), ("input T barrier", 35, 36),
        ("input row pass", 36, 2), ("blk0", 2, 3), ("blk1", 3, 4), ("blk2", 4, 5), ("blk3", 5, 6), ("blk4", 6, 7),
-       ("blk5", 7, 8), ("heads LN", 8, 9), ("v_head.2 chunk", 9, 40), ("policy chunks", 40, 14), ("end", 14, 15),
+       ("blk5", 7, 8), ("heads LN", 8, 9), ("v_head.2 chunk", 9, 40), ("  full / list reads", 9, 43), ("  chunk 0 tiles", 43, 41),
+       ("  chunk 0 ring issue", 41, 42), ("  v_head.2 MFMAs", 42, 40), ("policy chunks", 40, 14), ("end", 14, 15),
        ("(blk0: wave 0's tile-list chunk)", 39, 37)]
 eng.run(0, 0)  # warm-up
 torch.cuda.synchronize()

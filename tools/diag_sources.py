@@ -198,6 +198,9 @@ FWD = [
     (r"^        for \(int t = 0; t < PC; t\+\+\) tcur\[t\] = tnxt\[t\];\n", "after",
      "        if (c == 1 || c == 3) TSTAMP(10 + (c >> 1));\n        if (c == 5) TSTAMP(12);\n"),
     (r"^    float sm\[4\], ss\[4\];  // running max", "before", "    TSTAMP(40);\n"),
+    (r"^    chunk_tiles\(0, tcur\);\n", "around", ("    TSTAMP(43);\n", "    TSTAMP(41);\n")),
+    (r"^            for \(int t = 0; t < PC; t\+\+\) pring\[ks\]\[t\] = ld_w2<PL>\(net.w_pi, KS, tcur\[t\], ks, lane\);\n        __builtin_amdgcn_sched_barrier\(0\);\n",
+     "after", "        TSTAMP(42);\n"),
     (r"^#undef YK_PI_CHUNK\n", "after", "    TSTAMP(14);\n    WSTAMP(24);\n"),
     (r"^        for \(int j = 0; j < 4; j\+\+\) SS\[wave \* ROWS.*\n    \}\n", "after", "    TSTAMP(23);\n"),
     (r"^            mlse\[\(long\)part \* mstride.*\n        \}\n    \}\n", "after", "    TSTAMP(15);\n    TACC();\n"),
