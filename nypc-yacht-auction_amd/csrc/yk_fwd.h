@@ -980,12 +980,15 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
     const int m = cnt > wave ? (cnt - wave + NW - 1) / NW : 0;
     const int nf = m / PC, l = m % PC, nch = nf + (l ? 1 : 0);
 
-    auto chunk_tiles = [&](int c, int (&tl)[PC]) {
+    auto chunk_tiles = [&](int c, int (&tl)[PC]) {  // (the PC list reads unconditional: one LDS round trip)
         const int k0 = PC * c;
+        int v[PC];
+#pragma unroll
+        for (int t = 0; t < PC; t++) v[t] = TL[min(lo + wave + NW * (k0 + t), PI_TILES - 1)];
 #pragma unroll
         for (int t = 0; t < PC; t++) {
             const int i = lo + wave + NW * (k0 + t);
-            tl[t] = c < nch && k0 + t < m ? (full ? i : __builtin_amdgcn_readfirstlane((int)TL[i])) : 0;
+            tl[t] = c < nch && k0 + t < m ? (full ? i : __builtin_amdgcn_readfirstlane(v[t])) : 0;
         }
     };
     auto chunk_n = [&](int c) { return c < nf ? PC : c < nch ? l : 0; };
