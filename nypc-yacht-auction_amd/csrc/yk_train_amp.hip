@@ -159,15 +159,17 @@ __device__ __forceinline__ void stat_merge(float& m, float& s, float m2, float s
 // col0 + C) into the T layout at column tile offset ct0: a 32-row slice holds 32 / R tiles, lane
 // group q = lane >> 4 rows 8 q .. 8 q + 7 of it.  The batch's last tile (zero_rest) also zeroes
 // the rest of its slice (rows past the batch must not enter a weight gradient).
+// nthr > 0: only threads 0 .. nthr-1 (whole waves) take part (default: the whole workgroup)
 template <int R>
 __device__ __forceinline__ void write_tl(const _Float16* A, int sa, int col0, int C, _Float16* dst, int RS, int ct0,
-                                         int tile, bool zero_rest) {
+                                         int tile, bool zero_rest, int nthr = 0) {
     constexpr int QPT = R / 8, TPS = 32 / R;  // lane groups per tile, tiles per slice
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int nt = nthr > 0 ? nthr : (int)blockDim.x;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = nt >> 6;
     const int h = tile % TPS, rs = tile / TPS, q = lane >> 4;
     const bool mine = q / QPT == h, after = q / QPT > h;
     if constexpr (R == 8) {  // one 8-row piece per column: every thread takes half of one (4 rows, 8 bytes)
-        for (int i = threadIdx.x; i < C * 2; i += blockDim.x) {
+        for (int i = threadIdx.x; i < C * 2; i += nt) {
             const int cc = i >> 1, hf = i & 1, ct = cc >> 4, cl = cc & 15;
             half4 v;
 #pragma unroll
@@ -456,7 +458,7 @@ __global__ __launch_bounds__(TTHR) void k_amp_fwd(AmpDev d, const yk_state_t* __
     }
     if constexpr (PARTS) if (gw) ring_part<KS, NT, RW, 3 * KS / 4, KS>(ring, wfirst, nt0);
     lds_barrier();
-    if (NB > 0) write_tl<TRV>(Pa, SA, 0, H, d.hT, d.RS, 0, tile, zero_rest);
+    // (block 0's input h in the T layout: written by waves 0-3 beside its first GEMM, below)
 
     // ResidualBlock x NB: h = LN1(SiLU(fc1 x)); h = Dropout(h); h = LN2(SiLU(fc2 h)); x + h  YachtNNet.py:8-21
     for (int b = 0; b < NB; b++) {
@@ -483,6 +485,12 @@ __global__ __launch_bounds__(TTHR) void k_amp_fwd(AmpDev d, const yk_state_t* __
                 gemm_ring<KS, NT, RW, FDEF>(Pa, SA, ring, acc, cur, nxt, nt0);
                 store_acc<NT>(Ts, LD, nt0, acc);
             }
+            // this GEMM's input (h_b or r1_b) in the T layout for the weight gradients, by waves 0-3,
+            // which reach the barrier below before the younger waves (their weights arrive first);
+            // the row pass after it overwrites Pa
+            if (wave < 4)
+                write_tl<TRV>(Pa, SA, 0, H, (half == 0 ? d.hT : d.r1T) + (long)b * (H / 16) * d.RS * 512, d.RS, 0, tile,
+                              zero_rest, 256);
 #pragma unroll
             for (int k = 0; k < (3 * H + TTHR - 1) / TTHR; k++) VL[tid + TTHR * k] = vr[k];
             lds_barrier();
@@ -531,9 +539,6 @@ __global__ __launch_bounds__(TTHR) void k_amp_fwd(AmpDev d, const yk_state_t* __
             }
             if constexpr (FDEF > 0) if (gw) ring_part<KS, NT, RW, KS - FDEF / 2, KS>(ring, dsrc, nt0);
             lds_barrier();
-            if (half == 0) write_tl<TRV>(Pa, SA, 0, H, d.r1T + (long)b * (H / 16) * d.RS * 512, d.RS, 0, tile, zero_rest);
-            else if (b + 1 < NB)
-                write_tl<TRV>(Pa, SA, 0, H, d.hT + (long)(b + 1) * (H / 16) * d.RS * 512, d.RS, 0, tile, zero_rest);
         }
     }
 

@@ -32,7 +32,7 @@ L.yk_diag_amp_ts.argtypes = [C.c_void_p]
 ts = np.zeros((2, 64, 8, 16), dtype=np.uint64)
 assert L.yk_diag_amp_ts(ts.ctypes.data) == 0
 T = B // 8  # the trunk workgroups (TRV = 8 rows each)
-names = {0: ["GEMM + acc store", "barrier 1", "row pass", "barrier 2", "T-layout store"],
+names = {0: ["GEMM + acc store", "T-layout store (waves 0-3)", "barrier 1", "row pass", "barrier 2"],
          1: ["row pass", "barrier", "column partials", "T-layout store", "row prefetch", "GEMM + acc store", "barrier"]}
 for kk, kname in ((0, "k_amp_fwd"), (1, "k_amp_bwd")):
     print(f"{kname}, residual block 2 (ticks, mean over {T} tiles):")

@@ -221,18 +221,18 @@ extern "C" int yk_diag_amp_ts(void* dst) {
 #define AMP_STAMP(kk, k)
 #endif
 '''
-# k_amp_fwd, block 2, per half: 0 before the GEMM, 1 GEMM + accumulator store done, 2 the barrier
-# passed, 3 the row pass done, 4 the next barrier passed, 5 the T-layout store done
+# k_amp_fwd, block 2, per half: 0 before the GEMM, 1 GEMM + accumulator store done, 2 the T-layout
+# store of waves 0-3 done, 3 the barrier passed, 4 the row pass done, 5 the next barrier passed
 AMP = [
     (r"^constexpr int SQ_BLOCKS = 1024;\n", "after", AMP_GLOBALS),
     (r"^            const float4\* nxt = half == 0 \? d.w2f.*\n            const float4\* dsrc.*\n            if \(gw\) \{\n"
      r"                gemm_ring<KS, NT, RW, FDEF>\(Pa, SA, ring, acc, cur, nxt, nt0\);\n"
      r"                store_acc<NT>\(Ts, LD, nt0, acc\);\n            \}\n", "around",
      ("            AMP_STAMP(0, 0);\n", "            AMP_STAMP(0, 1);\n")),
-    (r"^            lds_barrier\(\);\n            float\* U = ", "after_line1", "            AMP_STAMP(0, 2);\n"),
-    (r"^            lds_barrier\(\);\n            if \(half == 0\) write_tl<TRV>\(Pa, SA", "around_line1",
-     ("            AMP_STAMP(0, 3);\n", "            AMP_STAMP(0, 4);\n")),
-    (r"^                write_tl<TRV>\(Pa, SA, 0, H, d.hT \+ \(long\)\(b \+ 1\).*\n", "after", "            AMP_STAMP(0, 5);\n"),
+    (r"^                              zero_rest, 256\);\n", "after", "            AMP_STAMP(0, 2);\n"),
+    (r"^            lds_barrier\(\);\n            float\* U = ", "after_line1", "            AMP_STAMP(0, 3);\n"),
+    (r"^            lds_barrier\(\);\n        \}\n    \}\n\n    // the heads' LayerNorms", "around_line1",
+     ("            AMP_STAMP(0, 4);\n", "            AMP_STAMP(0, 5);\n")),
     # k_amp_bwd, block 2, per half: 0 row pass start, 1 its end, 2 the barrier passed, 3 column
     # partials flushed, 4 T-layout store done, 5 next row's operands issued, 6 GEMM + store done,
     # 7 the barrier passed
