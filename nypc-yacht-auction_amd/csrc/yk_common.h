@@ -679,14 +679,24 @@ __device__ __forceinline__ float exp_acc(float x) {
     return fmaf(e, r * LN2, e);
 }
 // ------------------------------------------------------------------ features
-// c_tab.die_scale / round_feat recomputed in registers (IEEE double division, then the f32
-// rounding the host table applies - the same values bit for bit): a per-lane table index would
-// be a vector load, and in k_forward that would retire only after the weight ring's first fill
-__device__ __forceinline__ float die_scale(uint32_t d) { return (float)(((double)d - 3.5) / 3.5); }
+// c_tab.die_scale / round_feat recomputed in registers: a per-lane table index would be a vector
+// load, and in k_forward that would retire only after the weight ring's first fill.  numpy computes
+// them in float64 and rounds to float32; the correctly rounded f32 division of the same (exact)
+// operands gives the same bits for every d in 0..15 and round in 0..13 (checked on the host: a
+// float64 quotient of these operands never lies on an f32 rounding midpoint), at a third of the cost
+__device__ __forceinline__ float die_scale(uint32_t d) { return ((float)d - 3.5f) / 3.5f; }
+constexpr bool f32_feature_quotients_exact() {
+    for (int d = 0; d < 16; d++)
+        if (((float)d - 3.5f) / 3.5f != (float)(((double)d - 3.5) / 3.5)) return false;
+    for (int r = 0; r < 16; r++)
+        if ((float)r / 13.0f != (float)((double)r / 13.0)) return false;
+    return true;
+}
+static_assert(f32_feature_quotients_exact(), "f32 feature quotients == numpy's float64-then-float32");
 // state_to_vec  yacht/NNet.py:65-86 (bit-exact f32).  f(i) for i in [0, 59).
 __device__ inline float feature(const YkS& s, int i) {
     const int round = s_round(s), phase = s_phase(s);
-    if (i == 0) return (float)((double)round / 13.0);
+    if (i == 0) return (float)round / 13.0f;  // (= float32(round / 13.0), die_scale above)
     if (i == 1) return phase == 0 ? 1.0f : 0.0f;
     if (i == 2) return phase == 1 ? 1.0f : 0.0f;
     if (i < 23) {  // my / opp carry, pad -1

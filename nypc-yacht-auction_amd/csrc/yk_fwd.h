@@ -464,15 +464,10 @@ __device__ __forceinline__ uint32_t tile_word(uint32_t vd, int w) {
 }
 
 // Running softmax statistics (online form: max and sum exp(x - max)), merged over lanes and waves
-// at the end of the head.  The native __expf suffices here: its relative error |y| 2^-24 on a term
-// exp(y) is largest where the term is small, so the log-sum-exp moves by < 1e-7 (the expand's
-// final exp(x - m - lse) is the accurate exp_acc, yk_common.h); the log is the library logf
-__device__ __forceinline__ void stat_merge(float& m, float& s, float m2, float s2) {
-    const float mm = fmaxf(m, m2);
-    if (mm == -INFINITY) return;
-    s = s * __expf(m - mm) + s2 * __expf(m2 - mm);
-    m = mm;
-}
+// at the end of the head (the max of the parts first, then one rescale per part).  The native
+// __expf suffices here: its relative error |y| 2^-24 on a term exp(y) is largest where the term is
+// small, so the log-sum-exp moves by < 1e-7 (the expand's final exp(x - m - lse) is the accurate
+// exp_acc, yk_common.h); the log is the library logf
 // one chunk of policy tiles: a row's logits (+ bias) in the tiles it keeps a column in (`allc`:
 // every real column) - a set that depends on the row alone - stored and folded into its running
 // (max, sum exp): one rescale per row and chunk.  Lane (q, c) holds rows 4 q + j, column c.
@@ -556,6 +551,7 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
     __shared__ uint32_t UM[TMW];                             // the union of the rows' tile masks
     __shared__ uint32_t RM[ROWS][TMW];                       // each row's tile mask
     __shared__ uint16_t TRB[PI_TILES];                       // per tile: the rows that keep a column in it
+    __shared__ uint32_t VHC;                                 // waves whose v_head.2 columns are in X
 
     if (count) n = min(n, *count);
     if (row0 >= n) return;
@@ -573,6 +569,7 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
         }
         if (!amask) return;
     }
+    const float bv2 = net.b_v2[0];  // (v_head.4's bias, read at the end: loaded now, off that path)
     const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     // owns columns of the H-wide layers: every wave when NACT == NW (hidden >= 128), as a
     // compile-time true - a branch around the weight ring would make the wait counters merge at its
@@ -675,6 +672,7 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
     if (gw) ring_fill_part<PL, KS, NT, RW, RQ, RQ2>(ring, w_first, nt0);  // part 2 of the first fill
     __builtin_amdgcn_sched_barrier(0);
     if (tid < TMW) UM[tid] = 0u;
+    if (tid == 0) VHC = 0u;
     lds_barrier();
     if (lane < TMW) {  // this wave's rows' tile masks, and into the union (read after the input barrier)
         uint32_t w = 0;
@@ -1035,6 +1033,14 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
                 break;
         }
     }
+    // v_head.2's columns into X (the trunk output, read by the heads' LayerNorms only), counted: waves
+    // 0-3 compute the value head from them after their policy chunks, before the younger waves end
+    // theirs (a wave's LDS operations complete in order, so its count follows its stores)
+    constexpr uint32_t NVW = NW < 8 ? NW : 8;
+    if (NW == 8 || wave < 8) {
+        store_acc<1>(X, LD, vwave, av, VS + VS_BV1 * H);
+        if (lane == 0) atomicAdd(&VHC, 1u);
+    }
     float sm[4], ss[4];  // running max and sum exp of the lane's rows 4 q + j
     bool allc[4];
 #pragma unroll
@@ -1080,16 +1086,43 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
         for (int t = 0; t < PC; t++) tcur[t] = tnxt[t];
     }
 #undef YK_PI_CHUNK
-    if (NW == 8 || wave < 8) store_acc<1>(X, LD, vwave, av, VS + VS_BV1 * H);  // X (the trunk output) was read by the head LNs only
+    if (wave < 4) {  // SiLU -> Linear(128, 1) -> tanh  YachtNNet.py:49-52,69, rows 4 wave .. 4 wave + 3
+        for (int it = 0; it < (1 << 20) && *(volatile uint32_t*)&VHC < NVW; it++) __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+        for (int rr = 0; rr < ROWS / 4; rr++) {
+            const int r = wave * (ROWS / 4) + rr;
+            const int row = row0 + r;
+            const float* wv2 = VS + VS_BV1 * H + 128;
+            float s = silu(X[r * LD + 2 * lane]) * wv2[2 * lane] + silu(X[r * LD + 2 * lane + 1]) * wv2[2 * lane + 1];
+            s = wave_sum(s);
+            if (lane == 0 && part == 0 && row < n && ((amask >> r) & 1u)) vout[row] = tanhf(s + bv2);  // active rows only
+        }
+    }
     // softmax statistics of the policy logits per row: over the 16 column lanes, then the waves
     float2* SS = reinterpret_cast<float2*>(T);  // T (a_v's planes) is no longer read
-    if (mlse) {  // over the 16 column lanes
+    if (mlse) {  // over the 16 column lanes: the max first, then one rescale per lane and a sum (4 exps, not 32)
+        float mm[4], t[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) mm[j] = fmaxf(sm[j], xlane<1>(sm[j]));
+#pragma unroll
+        for (int j = 0; j < 4; j++) mm[j] = fmaxf(mm[j], xlane<2>(mm[j]));
+#pragma unroll
+        for (int j = 0; j < 4; j++) mm[j] = fmaxf(mm[j], xlane<4>(mm[j]));
+#pragma unroll
+        for (int j = 0; j < 4; j++) mm[j] = fmaxf(mm[j], xlane<8>(mm[j]));
+#pragma unroll
+        for (int j = 0; j < 4; j++) t[j] = sm[j] == -INFINITY ? 0.f : ss[j] * __expf(sm[j] - mm[j]);
+#pragma unroll
+        for (int j = 0; j < 4; j++) t[j] += xlane<1>(t[j]);
+#pragma unroll
+        for (int j = 0; j < 4; j++) t[j] += xlane<2>(t[j]);
+#pragma unroll
+        for (int j = 0; j < 4; j++) t[j] += xlane<4>(t[j]);
 #pragma unroll
         for (int j = 0; j < 4; j++) {
-            stat_merge(sm[j], ss[j], xlane<1>(sm[j]), xlane<1>(ss[j]));
-            stat_merge(sm[j], ss[j], xlane<2>(sm[j]), xlane<2>(ss[j]));
-            stat_merge(sm[j], ss[j], xlane<4>(sm[j]), xlane<4>(ss[j]));
-            stat_merge(sm[j], ss[j], xlane<8>(sm[j]), xlane<8>(ss[j]));
+            t[j] += xlane<8>(t[j]);
+            sm[j] = mm[j];
+            ss[j] = t[j];
         }
     }
     lds_barrier();  // every wave is done with v_head.2 (reads of T) and stored its av columns
@@ -1097,21 +1130,18 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
 #pragma unroll
         for (int j = 0; j < 4; j++) SS[wave * ROWS + 4 * (lane >> 4) + j] = make_float2(sm[j], ss[j]);
     }
-#pragma unroll
-    for (int rr = 0; rr < RPWN; rr++) {  // SiLU -> Linear(128, 1) -> tanh  YachtNNet.py:49-52,69
-        const int r = wave * RPWN + rr;
-        const int row = row0 + r;
-        const float* wv2 = VS + VS_BV1 * H + 128;
-        float s = silu(X[r * LD + 2 * lane]) * wv2[2 * lane] + silu(X[r * LD + 2 * lane + 1]) * wv2[2 * lane + 1];
-        s = wave_sum(s);
-        if (lane == 0 && part == 0 && row < n && ((amask >> r) & 1u)) vout[row] = tanhf(s + net.b_v2[0]);  // active rows only
-    }
     if (mlse) {
         lds_barrier();
         if (tid < ROWS && row0 + tid < n && ((amask >> tid) & 1u)) {  // (max, log sum exp(x - max)) of the row
+            float2 q[NW];
             float m = -INFINITY, sm = 0.f;
 #pragma unroll
-            for (int w = 0; w < NW; w++) stat_merge(m, sm, SS[w * ROWS + tid].x, SS[w * ROWS + tid].y);
+            for (int w = 0; w < NW; w++) {
+                q[w] = SS[w * ROWS + tid];
+                m = fmaxf(m, q[w].x);
+            }
+#pragma unroll
+            for (int w = 0; w < NW; w++) sm += q[w].x == -INFINITY ? 0.f : q[w].y * __expf(q[w].x - m);
             mlse[(long)part * mstride + row0 + tid] = make_float2(m, parts > 1 ? sm : logf(sm));
         }
     }

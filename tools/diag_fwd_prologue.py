@@ -29,7 +29,8 @@ seq = [("vstat->LDS", 0, 32), ("weights issued (w0)", 32, 38), ("features", 38, 
        ("tile masks", 34, 1), ("input GEMM", 1, 35), ("input T barrier", 35, 36),
        ("input row pass", 36, 2), ("blk0", 2, 3), ("blk1", 3, 4), ("blk2", 4, 5), ("blk3", 5, 6), ("blk4", 6, 7),
        ("blk5", 7, 8), ("heads LN", 8, 9), ("v_head.2 chunk", 9, 40), ("  full / list reads", 9, 43), ("  chunk 0 tiles", 43, 41),
-       ("  chunk 0 ring issue", 41, 42), ("  v_head.2 MFMAs", 42, 40), ("policy chunks", 40, 14), ("end", 14, 15),
+       ("  chunk 0 ring issue", 41, 42), ("  v_head.2 MFMAs", 42, 40), ("policy chunks", 40, 14), ("end", 14, 15), ("  value head (waves 0-3)", 14, 46), ("  stat merges", 46, 44),
+       ("  end barrier", 44, 45), ("  SS stores", 45, 23), ("  mlse", 23, 15),
        ("(blk0: wave 0's tile-list chunk)", 39, 37)]
 eng.run(0, 0)  # warm-up
 torch.cuda.synchronize()
@@ -44,10 +45,12 @@ for rep in range(2):
     n = float(a[S - 1])
     m = a.astype(np.float64) / n  # mean ticks of slot i after the workgroup's start
     m[0] = 0.0
-    rows.append((n, [m[b] - m[a_] for _, a_, b in seq], m[15]))
+    rows.append((n, [m[b] - m[a_] for _, a_, b in seq], m[15], [m[24 + w] - m[9] for w in range(8)]))
 print(f"k_forward phases, mean ticks over every workgroup of every launch of a batch ({E} games x {sims} sims)")
 print("  " + " ".join(f"{'batch ' + str(i):>10s}" for i in range(len(rows))) + "   phase")
 for j, (k, _, _) in enumerate(seq):
     print("  " + " ".join(f"{r[1][j]:10.0f}" for r in rows) + f"   {k}")
 print("  " + " ".join(f"{r[2]:10.0f}" for r in rows) + "   total")
 print("  " + " ".join(f"{r[0]:10.0f}" for r in rows) + "   workgroup-launches")
+for w in range(8):
+    print("  " + " ".join(f"{r[3][w]:10.0f}" for r in rows) + f"   wave {w}: end of its policy chunks after the heads' LayerNorm")

@@ -177,7 +177,7 @@ FWD = [
     # the prologue (slots 32-36, 38): static vectors in LDS, the weight loads issued, features
     # written, the input barrier, the input GEMM done, its barrier passed; block 0's tile-list build (39 -> 37)
     (r"^        reinterpret_cast<float4\*>\(VS\)\[tid \+ NTH \* k\] = vsv\[k\];.*\n", "after", "    TSTAMP(32);\n"),
-    (r"^    if \(tid < TMW\) UM\[tid\] = 0u;\n    lds_barrier\(\);\n", "around", ("    TSTAMP(33);\n", "    TSTAMP(34);\n")),
+    (r"^    if \(tid < TMW\) UM\[tid\] = 0u;\n    if \(tid == 0\) VHC = 0u;\n    lds_barrier\(\);\n", "around", ("    TSTAMP(33);\n", "    TSTAMP(34);\n")),
     (r"^    __builtin_amdgcn_sched_barrier\(0\);  // the first layer streams in under the featurize / input phase\n", "after",
      "    TSTAMP(38);\n"),
     (r"^    lds_barrier\(\);  // T complete; every wave is done reading the feature planes\n", "around",
@@ -203,6 +203,8 @@ FWD = [
      "after", "        TSTAMP(42);\n"),
     (r"^#undef YK_PI_CHUNK\n", "after", "    TSTAMP(14);\n    WSTAMP(24);\n"),
     (r"^        for \(int j = 0; j < 4; j\+\+\) SS\[wave \* ROWS.*\n    \}\n", "after", "    TSTAMP(23);\n"),
+    (r"^    lds_barrier\(\);  // every wave is done with v_head.2", "around_line1", ("    TSTAMP(44);\n", "    TSTAMP(45);\n")),
+    (r"^            if \(lane == 0 && part == 0 && row < n.*\n        \}\n    \}\n", "after", "    TSTAMP(46);\n"),
     (r"^            mlse\[\(long\)part \* mstride.*\n        \}\n    \}\n", "after", "    TSTAMP(15);\n    TACC();\n"),
 ]
 
