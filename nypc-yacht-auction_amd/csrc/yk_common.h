@@ -693,29 +693,29 @@ constexpr bool f32_feature_quotients_exact() {
     return true;
 }
 static_assert(f32_feature_quotients_exact(), "f32 feature quotients == numpy's float64-then-float32");
-// state_to_vec  yacht/NNet.py:65-86 (bit-exact f32).  f(i) for i in [0, 59).
+// state_to_vec  yacht/NNet.py:65-86 (bit-exact f32).  f(i) for i in [0, 59).  Branch-free: the lanes
+// of a wave compute different features, and divergent branches would run every region's code for
+// every lane; each region's value is computed from per-lane selects instead, with one die-value
+// quotient for the carry and roll regions
 __device__ inline float feature(const YkS& s, int i) {
     const int round = s_round(s), phase = s_phase(s);
-    if (i == 0) return (float)round / 13.0f;  // (= float32(round / 13.0), die_scale above)
-    if (i == 1) return phase == 0 ? 1.0f : 0.0f;
-    if (i == 2) return phase == 1 ? 1.0f : 0.0f;
-    if (i < 23) {  // my / opp carry, pad -1
-        const int p = (i - 3) / 10, k = (i - 3) % 10;
-        const uint64_t wa = s_pw(s, p, 0);
-        return k < wa_n(wa) ? die_scale((uint32_t)(wa >> (4 * k)) & 0xFu) : -1.0f;
-    }
-    if (i < 33) {  // rolls only when bidding (NNet.py:76-77)
-        const int r = (i - 23) / 5, k = (i - 23) % 5;
-        const bool has = (s.w[0] >> (5 + r)) & 1;
-        if (!(phase == 0 && round != 13) || !has) return -1.0f;
-        return die_scale((uint32_t)(s.w[0] >> (24 + 20 * r + 4 * k)) & 0xFu);
-    }
-    if (i < 57) {
-        const int p = (i - 33) / 12, k = (i - 33) % 12;
-        return (float)((wa_used(s_pw(s, p, 0)) >> k) & 1);
-    }
-    const int p = i - 57;
-    return (float)((double)wc_bid(s_pw(s, p, 2)) * 1e-5);
+    const bool carry = i >= 3 && i < 23, rolls = i >= 23 && i < 33, used = i >= 33 && i < 57;
+    // the player and position within the region (carry: 10 dice, rolls: 5 per roll, used: 12)
+    // (every shift below stays in 0 .. 63 for every lane, also where its value is not selected)
+    const int rel = carry ? i - 3 : rolls ? i - 23 : used ? i - 33 : i >= 57 ? i - 57 : 0;
+    const int per = carry ? 10 : rolls ? 5 : 12;
+    const int p = (i >= 57) ? (rel & 1) : rel / per, k = (i >= 57) ? 0 : rel - p * per;
+    const uint64_t wa = p ? s_pw(s, 1, 0) : s_pw(s, 0, 0);
+    // the die of a carry / roll slot, and whether the slot holds one (else -1)
+    const uint64_t src = rolls ? s.w[0] >> (24 + 20 * (p & 1)) : wa;
+    const uint32_t die = (uint32_t)(src >> (4 * k)) & 0xFu;
+    const bool has = rolls ? (phase == 0 && round != 13 && ((s.w[0] >> (5 + (p & 1))) & 1)) : k < wa_n(wa);
+    const float dv = has ? die_scale(die) : -1.0f;
+    const float uv = (float)((wa_used(wa) >> k) & 1);
+    const float bv = (float)((double)wc_bid(p ? s_pw(s, 1, 2) : s_pw(s, 0, 2)) * 1e-5);
+    const float r0 = (float)round / 13.0f;  // (= float32(round / 13.0), die_scale above)
+    return i == 0 ? r0 : i == 1 ? (phase == 0 ? 1.0f : 0.0f) : i == 2 ? (phase == 1 ? 1.0f : 0.0f)
+         : (carry || rolls) ? dv : used ? uv : bv;
 }
 
 }  // namespace yk

@@ -583,26 +583,35 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
     // scalar loads (wave-uniform addresses: SMEM, lgkmcnt), then the weight stream - the input
     // layer and the first part of fc1's ring fill (the rest between the phases below) - and only
     // then the features
+    constexpr int FPT = ROWS * 64 / NTH;  // feature rows per wave (row = wave + NW k)
+    static_assert(FPT * NW == ROWS, "one feature row per wave and k");
+    // the wave's state rows first: their scalar loads (both rows at once; the row map, when given,
+    // read before them) fly beside the static vectors' round trip below instead of after it
+    YkS fs[FPT];
+    if (!xin) {
+        int src[FPT];
+#pragma unroll
+        for (int k = 0; k < FPT; k++) {
+            const int row = row0 + wave + NW * k;
+            src[k] = row < n ? row : 0;
+        }
+        if (rows) {
+#pragma unroll
+            for (int k = 0; k < FPT; k++) src[k] = row0 + wave + NW * k < n ? rows[row0 + wave + NW * k] : 0;
+        }
+#pragma unroll
+        for (int k = 0; k < FPT; k++) {
+            const uint64_t* p = reinterpret_cast<const uint64_t*>(states + __builtin_amdgcn_readfirstlane(src[k]));
+#pragma unroll
+            for (int q = 0; q < 8; q++) fs[k].w[q] = p[q];
+        }
+    }
     float4 vsv[PER];
 #pragma unroll
     for (int k = 0; k < PER; k++) vsv[k] = reinterpret_cast<const float4*>(net.vstat)[min(tid + NTH * k, NV4 - 1)];
 #pragma unroll
     for (int k = 0; k < PER; k++)
         reinterpret_cast<float4*>(VS)[tid + NTH * k] = vsv[k];  // unconditional: the PER loads are waited for once
-    constexpr int FPT = ROWS * 64 / NTH;  // feature rows per wave (row = wave + NW k)
-    static_assert(FPT * NW == ROWS, "one feature row per wave and k");
-    YkS fs[FPT];
-    if (!xin) {
-#pragma unroll
-        for (int k = 0; k < FPT; k++) {
-            const int row = row0 + wave + NW * k;
-            int src = row < n ? (rows ? rows[row] : row) : 0;
-            src = __builtin_amdgcn_readfirstlane(src);
-            const uint64_t* p = reinterpret_cast<const uint64_t*>(states + src);
-#pragma unroll
-            for (int q = 0; q < 8; q++) fs[k].w[q] = p[q];
-        }
-    }
     // explicit features (predict on given rows) are loaded here, ahead of the weight stream: a
     // vector load issued after it would retire behind it (vmcnt is in order)
     float xv[FPT];
