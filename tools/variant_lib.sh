@@ -18,13 +18,16 @@ case " $* " in
     python3 tools/diag_sources.py $out/stage > /dev/null
     src=$out/stage/csrc ;;
 esac
+rm -f $out/*.o $out/libyacht_hip.so  # (a failed compile must not link a stale object)
+pids=()
 for f in yk_env yk_net yk_engine yk_train yk_train_amp yk_replay; do
   [ -f $src/$f.hip ] || continue
   fc=off; [ $f = yk_train_amp ] && fc=fast  # (as the Makefile)
   /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -fPIC -std=c++17 -ffp-contract=$fc -w "$@" \
      -Iinclude -I$src -c $src/$f.hip -o $out/$f.o &
+  pids+=($!)
 done
-wait
+for p in "${pids[@]}"; do wait $p || { echo "variant $name: compile failed" >&2; exit 1; }; done
 libs=""  # (baselines staged from before round 5 still call rocBLAS in the f32 trainer)
 grep -q rocblas $src/yk_train.hip && libs="-L/opt/rocm/lib -lrocblas -Wl,-rpath,/opt/rocm/lib"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $out/libyacht_hip.so $out/yk_*.o $libs
