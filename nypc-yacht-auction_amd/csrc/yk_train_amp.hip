@@ -1370,16 +1370,28 @@ struct UpdItem {
 __device__ __forceinline__ void adamw_elem(float& p, float& g, float& m, float& v, float inv, float coef,
                                            float decay, float b1, float b2, float eps, float step_size,
                                            float bc2_sqrt) {  // torch.optim.AdamW's single-tensor step
-    const float gi = (g * inv) * coef;
+    // Its multiply-adds fused explicitly, one per torch op, as the GPU build of ATen's pointwise
+    // formulas contracts them (lerp_ below weight 0.5: self + w (end - self); addcmul_: self + value
+    // (t1 t2); addcdiv_: self + value (t1 / t2)) - not left to -ffp-contract=fast, whose choice
+    // of which product to fuse moved with the surrounding code (train losses changed with the
+    // update kernel's block shape alone, profiles/r05zb_update_items_trainab.log).
+#pragma clang fp contract(off)
+    const float gi = (g * inv) * coef;  // unscale_, then clip_grad_norm_'s mul_
     g = gi;
-    float pi = p * decay;
-    const float mi = m + (gi - m) * (1.0f - b1);
-    const float vi = v * b2 + (1.0f - b2) * gi * gi;
+    const float pi = p * decay;                            // p.mul_(1 - lr wd)
+    const float mi = __builtin_fmaf(1.0f - b1, gi - m, m);  // m.lerp_(g, 1 - b1)
+    const float vi = __builtin_fmaf(1.0f - b2, gi * gi, v * b2);  // v.mul_(b2).addcmul_(g, g, 1 - b2)
     m = mi;
     v = vi;
-    const float denom = sqrtf(vi) / bc2_sqrt + eps;
-    pi -= step_size * (mi / denom);
-    p = pi;
+    const float denom = sqrtf(vi) / bc2_sqrt + eps;        // (v.sqrt() / bc2_sqrt).add_(eps)
+    p = __builtin_fmaf(-step_size, mi / denom, pi);        // p.addcdiv_(m, denom, -step_size)
+}
+// the fp16 copy of a stored float32 weight, rounded from that float32: the value is opaque to the
+// compiler, which would otherwise fold the conversion into the weight's fma as one v_fma_mixlo_f16
+// (a single rounding to fp16 - unlike k_amp_pack's and torch's autocast cast of the stored weight)
+__device__ __forceinline__ _Float16 f16_of_stored(float x) {
+    asm volatile("" : "+v"(x));
+    return (_Float16)x;
 }
 __global__ __launch_bounds__(256) void k_amp_update(const UpdJob* __restrict__ jobs, const UpdItem* __restrict__ items,
                                                     const double* __restrict__ part, double* sq_out,
@@ -1477,10 +1489,10 @@ __global__ __launch_bounds__(256) void k_amp_update(const UpdJob* __restrict__ j
         *reinterpret_cast<float4*>(jb.Gm + o) = g;
         *reinterpret_cast<float4*>(jb.Mm + o) = m;
         *reinterpret_cast<float4*>(jb.Vm + o) = v;
-        Tl[r][c] = (_Float16)p.x;
-        Tl[r][c + 1] = (_Float16)p.y;
-        Tl[r][c + 2] = (_Float16)p.z;
-        Tl[r][c + 3] = (_Float16)p.w;
+        Tl[r][c] = f16_of_stored(p.x);
+        Tl[r][c + 1] = f16_of_stored(p.y);
+        Tl[r][c + 2] = f16_of_stored(p.z);
+        Tl[r][c + 3] = f16_of_stored(p.w);
     } else {
 #pragma unroll
         for (int i = 0; i < 4; i++) {
@@ -1496,7 +1508,7 @@ __global__ __launch_bounds__(256) void k_amp_update(const UpdJob* __restrict__ j
                 jb.Vm[o] = v;
                 pv = p;
             }
-            Tl[r][c + i] = (_Float16)pv;
+            Tl[r][c + i] = f16_of_stored(pv);
         }
     }
     __syncthreads();
