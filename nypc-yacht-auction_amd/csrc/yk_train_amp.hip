@@ -57,8 +57,16 @@ constexpr int TRPW = TRV / TW;  // rows per wave in the row passes
 constexpr int LDL = 3264;       // logits row stride: 204 tiles of 16 columns
 constexpr int PT = LDL / 16;    // policy column tiles
 constexpr int PKS = LDL / 32;   // 32-deep action slices
-constexpr int HQ = 8;           // policy-head column parts per row tile (+1 part: v_head.2)
-constexpr int BQ = 6;           // head-backward action parts per row tile
+#ifndef YK_HQ
+#define YK_HQ 8
+#endif
+#ifndef YK_BQ
+#define YK_BQ 12
+#endif
+constexpr int HQ = YK_HQ;       // policy-head column parts per row tile (+1 part: v_head.2)
+constexpr int BQ = YK_BQ;       // head-backward action parts per row tile (12: 6 -> 12 took the step
+                                // 102.5 -> 99.0 us at batch 64, +-0 at 512; 16 and 24 slower at 512,
+                                // profiles/r05ze_head_parts_trainab.log)
 constexpr int VH = 128;         // v_head hidden width
 constexpr int SQ_BLOCKS = 1024;
 
