@@ -12,6 +12,10 @@ of the reference = one new MCTS.Ps entry), whole job, plus episodes/s.
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
+`python bench.py --gpus N` (N > 1) with no launcher environment starts the N ranks itself
+(spawn_ranks: one fresh process per GPU, torchrun's environment contract) and relays rank 0's
+line; under torch.distributed.run each rank runs main() directly.
+
 Prints ONE JSON line on rank 0.  Data: synthetic (games from seeded streams), random-init
 YachtNNet (kaiming-uniform per YachtNNet._init, seed 0, hidden 256, 6 blocks).
 """
@@ -44,23 +48,60 @@ GAME_MOVES = 48  # every Yacht Auction game has exactly 48 real moves (SURVEY Q1
 PREDICT_FLOP = 2 * (59 * H + 2 * NB * H * H + H * 128 + 128 + H * A)  # = 3,320,576
 
 
+def _cgroup_cpus():
+    """CPUs this process's cgroup may use: cgroup v2 cpu.max (quota / period), else v1's
+    cpu.cfs_quota_us / cpu.cfs_period_us; None when unlimited or unreadable."""
+    try:
+        with open("/proc/self/cgroup") as fh:
+            lines = [ln.strip().split(":", 2) for ln in fh if ln.strip()]
+    except OSError:
+        lines = []
+    cands = []
+    for _, ctrl, path in lines:
+        if ctrl == "":  # v2 unified hierarchy
+            cands.append(("v2", os.path.join("/sys/fs/cgroup", path.lstrip("/"))))
+            cands.append(("v2", "/sys/fs/cgroup"))
+        elif "cpu" in ctrl.split(","):
+            for root in ("/sys/fs/cgroup/cpu,cpuacct", "/sys/fs/cgroup/cpu"):
+                cands.append(("v1", os.path.join(root, path.lstrip("/"))))
+                cands.append(("v1", root))
+    for kind, d in cands:
+        try:
+            if kind == "v2":
+                with open(os.path.join(d, "cpu.max")) as fh:
+                    q, per = fh.read().split()[:2]
+                if q == "max":
+                    return None
+                return max(1, int(int(q) // int(per)))
+            with open(os.path.join(d, "cpu.cfs_quota_us")) as fh:
+                q = int(fh.read())
+            with open(os.path.join(d, "cpu.cfs_period_us")) as fh:
+                per = int(fh.read())
+            return None if q <= 0 else max(1, q // per)
+        except (OSError, ValueError):
+            continue
+    return None
+
+
 def host_cores():
-    """The host cores this process may use: OMP_NUM_THREADS when the box sets it (the GPU pool
-    gives each 1-GPU box a share of 16 of the machine's CPUs and exports OMP_NUM_THREADS=16),
-    else the CPUs in this process's affinity mask."""
-    env = os.environ.get("OMP_NUM_THREADS", "")
-    if env.isdigit() and int(env) > 0:
-        return int(env), "OMP_NUM_THREADS"
-    return len(os.sched_getaffinity(0)), "affinity mask"
+    """The host cores this process may use: the minimum of the CPUs in its affinity mask and its
+    cgroup's CPU quota (unlimited quota: the mask).  -> (cores, {affinity_cpus, cgroup_cpus,
+    omp_num_threads_env, host_cpus})."""
+    aff = len(os.sched_getaffinity(0))
+    cg = _cgroup_cpus()
+    cores = min(aff, cg) if cg else aff
+    return cores, {"affinity_cpus": aff, "cgroup_cpus": cg,
+                   "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"), "host_cpus": os.cpu_count()}
 
 
 def cpu_baseline(state_dict, sims, seconds_target=15.0, threads=None):
     """The oracle restatement (C, OpenMP over games) on every host core this process may use:
     a bounded sample of the same workload."""
     from oracle import oracle as O
-    src = "argument"
+    src = {"source": "argument"}
     if not threads:
         threads, src = host_cores()
+    os.environ["OMP_NUM_THREADS"] = str(threads)  # (the oracle's OpenMP pool reads it when it loads)
     net = O.Net(state_dict, H, NB)
     # calibrate: one game per thread, then scale the sample to ~seconds_target
     t0 = time.time()
@@ -77,7 +118,10 @@ def cpu_baseline(state_dict, sims, seconds_target=15.0, threads=None):
         exps += int(r["stats"][:, 1].sum())
         games += threads * k
     return {"value": exps / dt, "unit": "expansions/s", "cores": threads, "kind": "port",
-            "cores_source": f"{src}; the host has {os.cpu_count()} CPUs",
+            "affinity_cpus": src.get("affinity_cpus"), "cgroup_cpus": src.get("cgroup_cpus"),
+            "omp_num_threads_env": src.get("omp_num_threads_env"), "host_cpus": src.get("host_cpus"),
+            "cores_basis": "cores = min(affinity_cpus, cgroup_cpus) (cgroup_cpus null: no quota); one OpenMP "
+                           "thread per core",
             "sample": f"{games} full self-play games x {sims} sims (C restatement, oracle/yk_oracle.c, "
                       f"same net, one OpenMP thread per game), {exps} expansions in {dt:.1f}s",
             "reference_python": "the reference's own Coach/MCTS (Python, 1 core) ran 236 expansions/s in the "
@@ -413,6 +457,105 @@ def coach_leg(model, image, n_envs, max_moves, sims, world, train_steps=60, aren
             "arena_tally_prev_new_draws": [pw, nw, dr]}
 
 
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def spawn_ranks(nprocs, argv, timeout_s, script=None, out=None, err=None, poll_s=0.2):
+    """Run `nprocs` ranks of this job on one node without an external launcher: fresh child
+    interpreters (`python -u script argv`), each with torchrun's environment contract (RANK,
+    LOCAL_RANK, WORLD_SIZE, LOCAL_WORLD_SIZE, MASTER_ADDR 127.0.0.1, a free MASTER_PORT), started
+    before this process makes any GPU call (it makes none).  Rank 0's stdout lines that parse as
+    a JSON object are relayed to `out` (the bench line); everything else any rank prints goes to
+    `err` (stderr is inherited when `err` is sys.stderr).  The first child to fail (or the
+    timeout) ends the job: the other ranks' process groups are terminated (then killed) and the
+    return code is non-zero (the failing rank's code, 124 on timeout, 1 when rank 0 printed no
+    JSON line or more than one).  -> exit code."""
+    import signal
+    import subprocess
+    import threading
+    out = out or sys.stdout
+    err = err or sys.stderr
+    script = script or os.path.abspath(__file__)
+    port = _free_port()
+    procs, lines = [], []
+
+    def pump(stream, rank):
+        for raw in iter(stream.readline, b""):
+            line = raw.decode(errors="replace")
+            obj = None
+            if rank == 0 and line.lstrip().startswith("{"):
+                try:
+                    obj = json.loads(line)
+                except ValueError:
+                    obj = None
+            if isinstance(obj, dict):
+                lines.append(line.rstrip("\n"))
+            else:
+                err.write(f"[rank {rank if rank >= 0 else -1 - rank}] {line}")
+                err.flush()
+        stream.close()
+
+    pumps = []
+    for r in range(nprocs):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nprocs),
+                   LOCAL_WORLD_SIZE=str(nprocs), GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   YK_SELF_SPAWNED="1")
+        p = subprocess.Popen([sys.executable, "-u", script] + list(argv), env=env, stdout=subprocess.PIPE,
+                             stderr=None if err is sys.stderr else subprocess.PIPE, start_new_session=True)
+        procs.append(p)
+        for stream, kind in ((p.stdout, "out"), (p.stderr, "err")):
+            if stream is not None:  # (stderr: inherited unless `err` is not this process's stderr)
+                t = threading.Thread(target=pump, args=(stream, r if kind == "out" else -1 - r), daemon=True)
+                t.start()
+                pumps.append(t)
+
+    def stop_all():
+        for sig, wait in ((signal.SIGTERM, 10.0), (signal.SIGKILL, 5.0)):
+            live = [p for p in procs if p.poll() is None]
+            for p in live:
+                try:
+                    os.killpg(p.pid, sig)  # the child's own process group (start_new_session)
+                except ProcessLookupError:
+                    pass
+            t_end = time.time() + wait
+            while any(p.poll() is None for p in live) and time.time() < t_end:
+                time.sleep(0.1)
+
+    t0 = time.time()
+    rc = 0
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+        if bad:
+            r, c = bad[0]
+            err.write(f"spawn_ranks: rank {r} exited with {c}; stopping the other ranks\n")
+            stop_all()
+            rc = c if c > 0 else 128 - c  # (a signal: 128 + signal number)
+            break
+        if all(c == 0 for c in codes):
+            break
+        if time.time() - t0 > timeout_s:
+            err.write(f"spawn_ranks: timeout after {timeout_s:.0f} s; stopping every rank\n")
+            stop_all()
+            rc = 124
+            break
+        time.sleep(poll_s)
+    for t in pumps:
+        t.join(timeout=5.0)
+    if rc == 0 and len(lines) != 1:
+        err.write(f"spawn_ranks: rank 0 printed {len(lines)} JSON lines (expected one)\n")
+        rc = 1
+    if rc == 0:
+        out.write(lines[0] + "\n")
+        out.flush()
+    err.flush()
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -444,7 +587,13 @@ def main():
                     help="entries of the root's P order kept (YK_ROOT_K; 0: the engine's 512; A/B only)")
     ap.add_argument("--arena-entries", type=int, default=0,
                     help="P-arena entries per game (0: the engine's overflow-free default)")
+    ap.add_argument("--spawn-timeout", type=float, default=3000.0,
+                    help="--gpus N > 1 without a launcher's WORLD_SIZE: seconds the self-spawned ranks may take")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no launcher: this process starts the N ranks itself (before touching the GPU) and relays
+        # rank 0's line; under torchrun (WORLD_SIZE set) each rank runs the code below
+        raise SystemExit(spawn_ranks(args.gpus, sys.argv[1:], args.spawn_timeout))
     if not args.root_scan:
         os.environ["YK_ROOT_SCAN"] = "0"
     if args.root_k:

@@ -46,6 +46,7 @@ typedef struct { uint64_t w[8]; } yk_state_t;
 #define YK_ERR_NOMEM (-3)
 #define YK_ERR_CAPACITY (-4) /* a fixed-size engine pool overflowed; results invalid */
 #define YK_ERR_STATE (-5)    /* engine misuse (e.g. MCTS root round went backwards) */
+#define YK_ERR_RANGE (-6)    /* a weight outside the fp16 split's range (|w| >= 65520: its hi plane overflows) */
 
 /* per-element status of yk_step: the reference's exceptions */
 #define YK_ST_OK 0
@@ -111,7 +112,9 @@ int yk_hash_prior(const yk_state_t* in, float* pi, float* v, int n, void* stream
 typedef struct yk_net yk_net_t;
 /* params: HOST float32 arrays in YachtNNet.state_dict() order (inp.0.weight, inp.0.bias,
  * inp.1.weight, inp.1.bias, blocks.{b}.{fc1,ln1,fc2,ln2}.{weight,bias}, pi_head.0.*,
- * pi_head.2.*, v_head.0.*, v_head.2.*, v_head.4.*).  hidden in {64,128,256,512}. */
+ * pi_head.2.*, v_head.0.*, v_head.2.*, v_head.4.*).  hidden in {64,128,256,512}, nblocks 0-64.
+ * YK_ERR_RANGE when a finite weight of a Linear layer overflows the fp16 hi plane of the
+ * f32-equivalent split (|w| >= 65520): the planes would hold inf where torch holds a number. */
 int yk_net_create(yk_net_t** net, int hidden, int nblocks, const float* const* params, int nparams);
 /* pi[i*3226 + a] = exp(log_softmax(logits)), v[i] = tanh(v_head). */
 int yk_net_predict(yk_net_t* net, const yk_state_t* states, float* pi, float* v, int n, void* stream);
@@ -132,6 +135,11 @@ int yk_net_leaf_prior(yk_net_t* net, const yk_state_t* states, float* pi, float*
 int yk_net_policy_action(yk_net_t* net, const yk_state_t* states, int32_t* actions, float* probs, int n,
                          void* stream);
 int yk_net_destroy(yk_net_t* net);
+/* Device-side check flags of this net's forwards since the last call (cleared by it; synchronises
+ * the device): YK_NET_ERR_SYNC - a wave of the value head timed out waiting for v_head.2's columns
+ * (its v row is then not trustworthy).  0 when every forward completed its hand-offs. */
+#define YK_NET_ERR_SYNC 1u
+int yk_net_errors(yk_net_t* net, uint32_t* flags);
 /* Precision of every forward of this net (predict, leaf prior, the engine's expansions):
  * YK_PREDICT_F32 (default) - f32-equivalent products (fp16 hi/lo planes, three MFMAs each; within
  * 1e-5 of the reference's float32 CPU path); YK_PREDICT_F16 - fp16 weights and GEMM inputs with

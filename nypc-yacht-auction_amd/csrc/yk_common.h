@@ -514,7 +514,7 @@ __device__ __forceinline__ uint32_t xlane_u(uint32_t v) {
     else {
         // v_permlane{16,32}_swap(v, v): the first result holds the lower row / half in both
         // positions, the second the upper
-        const bool upper = (threadIdx.x & O) != 0;
+        const bool upper = (__lane_id() & O) != 0;  // the lane's position in the wave, any launch shape
         if constexpr (O == 16) {
             const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
             return upper ? r[0] : r[1];

@@ -147,7 +147,8 @@ struct EngDev {
 
 enum : uint32_t {
     ERR_NODES = 1u, ERR_EDGES = 2u, ERR_ARENA = 4u, ERR_DEPTH = 8u, ERR_STEP = 16u, ERR_ROUND = 32u,
-    ERR_VISITS = 64u, ERR_MOVES = 128u, ERR_ZERO_COUNTS = 256u, ERR_ROOT = 512u, ERR_HASH = 1024u
+    ERR_VISITS = 64u, ERR_MOVES = 128u, ERR_ZERO_COUNTS = 256u, ERR_ROOT = 512u, ERR_HASH = 1024u,
+    ERR_FWD_SYNC = 2048u  // a forward's value head timed out on its v_head.2 hand-off (the net's flag word)
 };
 
 // numpy float32 pairwise-sum plan for n = 3226 (loops_utils.h.src @TYPE@_pairwise_sum)
@@ -1562,8 +1563,15 @@ int dalloc(yk_engine* eng, T** p, size_t count) {
 }
 int check_errors(yk_engine* eng, hipStream_t s) {
     uint32_t err = 0;
+    uint32_t nerr[2] = {0u, 0u};
     YK_HIP(hipMemcpyAsync(&err, eng->d.err, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    if (eng->net) YK_HIP(hipMemcpyAsync(&nerr[0], eng->net->dev.err, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    if (eng->net2) YK_HIP(hipMemcpyAsync(&nerr[1], eng->net2->dev.err, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     YK_HIP(hipStreamSynchronize(s));
+    if ((nerr[0] | nerr[1]) && !(err & ERR_FWD_SYNC)) {  // into the engine's word, so yk_engine_stats shows it
+        err |= ERR_FWD_SYNC;
+        YK_HIP(hipMemcpy(eng->d.err, &err, sizeof(uint32_t), hipMemcpyHostToDevice));
+    }
     if (err & (ERR_NODES | ERR_EDGES | ERR_ARENA | ERR_DEPTH | ERR_VISITS | ERR_HASH)) return YK_ERR_CAPACITY;
     if (err) return YK_ERR_STATE;
     return YK_OK;

@@ -188,6 +188,7 @@ __device__ __forceinline__ void mma_ring(const _Float16* A, int sa, W2 (&ring)[R
 // slices S0 .. S1-1 of the ring's first fill (the prologue issues the fill in parts)
 template <int PL, int KS, int NT, int RW, int S0, int S1>
 __device__ __forceinline__ void ring_fill_part(W2 (&ring)[RW][NT], const float* __restrict__ W, int nt0) {
+    static_assert(0 <= S0 && S0 <= S1 && S1 <= RW, "slots within the ring");
     const int lane = threadIdx.x & 63;
 #pragma unroll
     for (int ks = S0; ks < S1; ks++)
@@ -892,8 +893,21 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
         lds_barrier();
     };
     for (int b = 0; b + 1 < net.NB; b++) block(b, std::false_type{});
-    if (net.NB > 0) block(net.NB - 1, std::true_type{});
-    else if (wave < 4) build_tiles(wave);  // (no block: read after the heads' LayerNorm barrier)
+    if (net.NB > 0) {
+        block(net.NB - 1, std::true_type{});
+    } else {
+        if (wave < 4) build_tiles(wave);  // (no block: read after the heads' LayerNorm barrier)
+        // no last fc2 GEMM streamed v_head.2's tile into the ring the heads read (VHP): load it here
+        if constexpr (VHP) {
+            if (gw) {
+#pragma unroll
+                for (int ks = 0; ks < KS; ks++) {
+                    if constexpr (DUAL) ring2[ks][0] = ld_w2<PL>(net.w_v1, KS, vwave, ks, lane);
+                    else ring[ks][0] = ld_w2<PL>(net.w_v1, KS, vwave, ks, lane);
+                }
+            }
+        }
+    }
 
     // heads: pi_head = LN -> SiLU -> Linear; v_head = LN -> SiLU -> Linear -> SiLU -> Linear -> tanh.
     // One ring streams v_head.2 (one 16-column tile per wave, first) and then the policy head;
@@ -1048,7 +1062,7 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
     constexpr uint32_t NVW = NW < 8 ? NW : 8;
     if (NW == 8 || wave < 8) {
         store_acc<1>(X, LD, vwave, av, VS + VS_BV1 * H);
-        if (lane == 0) atomicAdd(&VHC, 1u);
+        if (lane == 0) __hip_atomic_fetch_add(&VHC, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     float sm[4], ss[4];  // running max and sum exp of the lane's rows 4 q + j
     bool allc[4];
@@ -1096,7 +1110,17 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
     }
 #undef YK_PI_CHUNK
     if (wave < 4) {  // SiLU -> Linear(128, 1) -> tanh  YachtNNet.py:49-52,69, rows 4 wave .. 4 wave + 3
-        for (int it = 0; it < (1 << 20) && *(volatile uint32_t*)&VHC < NVW; it++) __builtin_amdgcn_s_sleep(1);
+        // (bounded: a wave that never sees every count flags the net's error word instead of hanging
+        // the grid; yk_net_errors / the engine's ERR_FWD_SYNC report it)
+        bool seen = false;
+        for (int it = 0; it < (1 << 20); it++) {
+            if (__hip_atomic_load(&VHC, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= NVW) {
+                seen = true;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        if (!seen && lane == 0 && net.err) atomicOr(net.err, FWD_ERR_SYNC);
 #pragma unroll
         for (int rr = 0; rr < ROWS / 4; rr++) {
             const int r = wave * (ROWS / 4) + rr;

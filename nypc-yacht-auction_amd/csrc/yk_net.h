@@ -27,7 +27,9 @@ struct NetDev {
     float pi_bspread;    // max - min of pi_head.2's bias over the 3226 actions
     float pi_wmax;       // max over actions of |pi_head.2 weight row|_2
     int planes;          // 2: f32-equivalent hi/lo products (default); 1: fp16 mode (hi planes only)
+    uint32_t* err;       // device check flags (FWD_ERR_SYNC), a word of the net's blob; read by yk_net_errors
 };
+constexpr uint32_t FWD_ERR_SYNC = 1u;  // = YK_NET_ERR_SYNC: the value head's wait for v_head.2 timed out
 // vstat offsets in units of H (b_v1 at VS_BV1*H, w_v2 right after it, b_pi at vs_bpi(H))
 enum { VS_BIN = 0, VS_GIN = 1, VS_BEIN = 2, VS_GPI = 3, VS_BEPI = 4, VS_GV = 5, VS_BEV = 6, VS_BV1 = 7 };
 constexpr int vs_bpi(int H) { return 7 * H + 256; }

@@ -191,6 +191,23 @@ int yk_net_create(yk_net_t** out, int H, int NB, const float* const* p, int npar
     const size_t o_gv = put(H), o_bev = put(H), o_wv1 = put((size_t)128 * H), o_bv1 = put(128), o_wv2 = put(128),
                  o_bv2 = put(1);
     const size_t o_vs = put(vstat_size(H)), o_vb = put((size_t)NB * 6 * H);
+    const size_t o_err = put(1);  // the forwards' check flags (a uint32 word, zeroed below)
+    // the f32-equivalent split's range: hi = fp16(w) must be finite for every finite weight of the
+    // packed (MFMA) matrices - |w| >= 65520 rounds to inf, where torch's float32 holds a number
+    {
+        const int mats[4] = {0, 6 + 8 * NB, 10 + 8 * NB, -1};
+        const size_t mlen[3] = {(size_t)H * FEAT, (size_t)ASIZE * H, (size_t)128 * H};
+        auto out_of_range = [](const float* w, size_t n) {
+            for (size_t i = 0; i < n; i++)
+                if (std::isfinite(w[i]) && std::fabs(w[i]) >= 65520.f) return true;
+            return false;
+        };
+        for (int m = 0; mats[m] >= 0; m++)
+            if (out_of_range(p[mats[m]], mlen[m])) return YK_ERR_RANGE;
+        for (int b = 0; b < NB; b++)
+            if (out_of_range(p[4 + 8 * b], (size_t)H * H) || out_of_range(p[8 + 8 * b], (size_t)H * H))
+                return YK_ERR_RANGE;
+    }
     // pi_head.2 bounds for the valid-only softmax (k_forward): bias spread, largest weight-row norm
     float pi_bmin = INFINITY, pi_bmax = -INFINITY, pi_wmax = 0.f;
     {
@@ -254,6 +271,7 @@ int yk_net_create(yk_net_t** out, int H, int NB, const float* const* p, int npar
     d.g_pi = B + o_gpi; d.be_pi = B + o_bepi; d.w_pi = B + o_wpi; d.b_pi = B + o_bpi;
     d.g_v = B + o_gv; d.be_v = B + o_bev; d.w_v1 = B + o_wv1; d.b_v1 = B + o_bv1; d.w_v2 = B + o_wv2; d.b_v2 = B + o_bv2;
     d.vstat = B + o_vs; d.vblk = B + o_vb;
+    d.err = reinterpret_cast<uint32_t*>(net->blob + o_err);
     // rounded up so the device-side bound stays an upper bound (and non-finite weights force the
     // full softmax)
     d.pi_bspread = std::isfinite(pi_bmax - pi_bmin) ? (pi_bmax - pi_bmin) * 1.001f + 1e-3f : INFINITY;
@@ -266,6 +284,14 @@ int yk_net_create(yk_net_t** out, int H, int NB, const float* const* p, int npar
 int yk_net_set_precision(yk_net_t* net, int mode) {
     if (!net || (mode != YK_PREDICT_F32 && mode != YK_PREDICT_F16)) return YK_ERR_ARG;
     net->dev.planes = mode == YK_PREDICT_F16 ? 1 : 2;
+    return YK_OK;
+}
+
+int yk_net_errors(yk_net_t* net, uint32_t* flags) {
+    if (!net || !flags) return YK_ERR_ARG;
+    YK_HIP(hipDeviceSynchronize());
+    YK_HIP(hipMemcpy(flags, net->dev.err, sizeof(uint32_t), hipMemcpyDeviceToHost));
+    if (*flags) YK_HIP(hipMemset(net->dev.err, 0, sizeof(uint32_t)));
     return YK_OK;
 }
 

@@ -734,6 +734,22 @@ int yk_trainer_create(yk_trainer_t** out, int H, int NB, const float* const* par
     if (!(H == 64 || H == 128 || H == 256 || H == 512) || NB < 0 || NB > 64) return YK_ERR_ARG;
     if (nparams != 14 + 8 * NB || cfg->max_batch <= 0) return YK_ERR_ARG;
     if (!(cfg->dropout >= 0.0f && cfg->dropout < 1.0f)) return YK_ERR_ARG;
+    if (cfg->amp) {
+        // the mixed-precision step casts the Linear weights to fp16 (autocast): a finite weight with
+        // |w| >= 65520 becomes inf there - every step's loss non-finite, every GradScaler step skipped
+        // (torch's autocast path stalls the same way, silently); refused up front instead
+        auto out_of_range = [](const float* w, long len) {
+            for (long i = 0; i < len; i++)
+                if (std::isfinite(w[i]) && std::fabs(w[i]) >= 65520.f) return true;
+            return false;
+        };
+        if (out_of_range(params[0], (long)H * FEAT) || out_of_range(params[6 + 8 * NB], (long)ASIZE * H) ||
+            out_of_range(params[10 + 8 * NB], 128L * H))
+            return YK_ERR_RANGE;
+        for (int b = 0; b < NB; b++)
+            if (out_of_range(params[4 + 8 * b], (long)H * H) || out_of_range(params[8 + 8 * b], (long)H * H))
+                return YK_ERR_RANGE;
+    }
     yk_trainer* t = new yk_trainer();
     t->H = H;
     t->NB = NB;

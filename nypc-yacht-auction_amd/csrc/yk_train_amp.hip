@@ -209,6 +209,7 @@ template <int KS, int NT, int RW, int DEF = 0>
 __device__ __forceinline__ void gemm_ring(const _Float16* A, int sa, float4 (&ring)[RW][NT], floatx4 (&acc)[NT],
                                           const float4* __restrict__ cur, const float4* __restrict__ nxt, int nt0) {
     static_assert(KS % RW == 0, "ring slots align with layers");
+    static_assert(0 <= DEF && DEF <= KS - RW + DEF && (DEF == 0 || RW == KS), "deferred refills within a one-matrix ring");
     const int lane = threadIdx.x & 63;
     const _Float16* ap = A + (lane & 15) * sa + 8 * (lane >> 4);
 #pragma unroll
@@ -239,6 +240,7 @@ __device__ __forceinline__ void gemm_ring(const _Float16* A, int sa, float4 (&ri
 template <int KS, int NT, int RW, int S0, int S1>
 __device__ __forceinline__ void ring_part(float4 (&ring)[RW][NT], const float4* __restrict__ W, int nt0) {
     static_assert(RW == KS || S0 == S1, "deferred refills need a one-matrix ring");
+    static_assert(0 <= S0 && S0 <= S1 && S1 <= RW, "slots within the ring");
     const int lane = threadIdx.x & 63;
 #pragma unroll
     for (int s = S0; s < S1; s++)
@@ -350,7 +352,8 @@ __global__ __launch_bounds__(TTHR) void k_amp_fwd(AmpDev d, const yk_state_t* __
     // refills stall a wave while every wave's loads share the CU's vector-memory path, which is idle
     // during the row passes.  AMP step 122.6 -> 115.3 us with 6 in both kernels (4: 116.0, 8: 116.5;
     // profiles/r05m_amp_defer_*trainab.log)
-    constexpr int FDEF = RW == KS ? 6 : 0;
+    // (hidden >= 256 only: at KS < 8 a GEMM has too few slices to leave 6 to the row pass)
+    constexpr int FDEF = (RW == KS && KS >= 8) ? 6 : 0;
     __shared__ __attribute__((aligned(16))) float Xs[TR * LD];
     __shared__ __attribute__((aligned(16))) float Ts[TR * LD];
     __shared__ __attribute__((aligned(16))) _Float16 Pa[TR * SA];
@@ -986,7 +989,7 @@ __global__ __launch_bounds__(TTHR) void k_amp_bwd(AmpDev d, int B, float p, uint
     constexpr int LD = H + 4, SA = H + 8, VPL = H / 64, KS = H / 32;
     constexpr int NT = H >= 128 ? H / 128 : 1, NACT = H / (16 * NT);
     constexpr int RW = KS * NT <= 16 ? KS : 16 / NT;
-    constexpr int BDEF = RW == KS ? 6 : 0;  // deferred ring refills per trunk GEMM (k_amp_fwd's FDEF)
+    constexpr int BDEF = (RW == KS && KS >= 8) ? 6 : 0;  // deferred ring refills per trunk GEMM (k_amp_fwd's FDEF)
     constexpr int SV = VH + 8;
     static_assert(SV <= SA || H == 64, "dz1 rows fit the plane buffer");
     __shared__ __attribute__((aligned(16))) float Xs[TR * LD];

@@ -16,8 +16,11 @@ PKG_ROOT = os.path.dirname(HERE)
 LIB_PATH = os.environ.get("YK_LIB_PATH") or os.path.join(HERE, "libyacht_hip.so")
 
 YK_OK, YK_ERR_ARG, YK_ERR_HIP, YK_ERR_NOMEM, YK_ERR_CAPACITY, YK_ERR_STATE = 0, -1, -2, -3, -4, -5
+YK_ERR_RANGE = -6
 _ERR_NAMES = {YK_ERR_ARG: "bad argument", YK_ERR_HIP: "HIP error", YK_ERR_NOMEM: "out of device memory",
-              YK_ERR_CAPACITY: "engine capacity exceeded", YK_ERR_STATE: "engine state error"}
+              YK_ERR_CAPACITY: "engine capacity exceeded", YK_ERR_STATE: "engine state error",
+              YK_ERR_RANGE: "a weight outside the fp16 split's range (|w| >= 65520)"}
+YK_NET_ERR_SYNC = 1  # yk_net_errors: a value-head wave timed out on the v_head.2 hand-off
 
 # per-element yk_step status -> the reference's exception (YachtGame.py:268-269, 306-307, 372, 508)
 ST_OK, ST_VALUE_BID, ST_VALUE_SCORE, ST_RUNTIME, ST_ASSERT, ST_CAPACITY = 0, 1, 2, 3, 4, 5
@@ -63,6 +66,7 @@ SIGNATURES = {
     "yk_net_policy_action": [P, P, P, P, I, P],
     "yk_net_destroy": [P],
     "yk_net_set_precision": [P, I],
+    "yk_net_errors": [P, P],
     "yk_engine_create": [C.POINTER(P), C.POINTER(YkEngineConfig), P],
     "yk_engine_destroy": [P],
     "yk_selfplay": [P, U64, U32, P],
@@ -100,7 +104,7 @@ SIGNATURES = {
 _RESTYPE = {"yk_version": C.c_char_p, "yk_rng_draw64": C.c_uint64, "yk_engine_record_bytes": C.c_int64,
             "yk_trainer_step_count": C.c_int64}
 
-_NEWER = {"yk_engine_counters"}  # added in round 5 (tools/ab_bench.sh baselines may predate them)
+_NEWER = {"yk_engine_counters", "yk_net_errors"}  # added in rounds 5-6 (A/B baselines may predate them)
 _lib = None
 
 

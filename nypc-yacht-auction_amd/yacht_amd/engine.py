@@ -45,7 +45,7 @@ class SelfPlayEngine:
 
     ERROR_BITS = {1: "node pool", 2: "edge pool", 4: "arena", 8: "search depth", 16: "transition status",
                   32: "root round went backwards", 64: "visit records", 128: "move cap", 256: "zero visit counts",
-                  512: "root not in tree", 1024: "hash index full"}
+                  512: "root not in tree", 1024: "hash index full", 2048: "forward hand-off timed out"}
 
     def run(self, seed: int, env_base: int = 0, stream=None):
         from ._lib import YkError

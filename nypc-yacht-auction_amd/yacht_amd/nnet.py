@@ -129,6 +129,13 @@ class YkNet:
              stream_ptr())
         return actions, probs
 
+    def errors(self) -> int:
+        """The device check flags of this net's forwards since the last call (yk_net_errors; synchronises
+        the device): 0, or YK_NET_ERR_SYNC when a value-head wave timed out on its v_head.2 hand-off."""
+        f = C.c_uint32()
+        call("yk_net_errors", self.handle, C.byref(f))
+        return int(f.value)
+
     def __del__(self):
         try:
             if getattr(self, "handle", None):

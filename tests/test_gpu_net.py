@@ -119,3 +119,72 @@ def test_leaf_prior_keeps_the_full_softmax_when_underflow_is_possible(mods, gold
     np.testing.assert_allclose(lp, np.where(ok, pp, 0.0).astype(np.float32), rtol=1e-6, atol=0)
     bid = ok[:, :202].any(1)
     assert bid.any() and (lp[bid].sum(1) < 1e-30).all()  # the bids underflow: uniform fallback
+
+
+def _torch_model(N, hidden, nblocks, seed):
+    torch.manual_seed(seed)
+    model = N.YachtNNet(hidden=hidden, nblocks=nblocks).eval()
+    with torch.no_grad():  # non-trivial LayerNorm affines
+        for m in model.modules():
+            if isinstance(m, torch.nn.LayerNorm):
+                m.weight.uniform_(0.5, 1.5)
+                m.bias.uniform_(-0.2, 0.2)
+    return model
+
+
+def _torch_fp32(K, model, S):
+    m = model.to("cuda").float()
+    with torch.no_grad():
+        torch.backends.cuda.matmul.allow_tf32 = False
+        logits, vr = m(K.featurize(S))
+        pr = torch.nn.functional.log_softmax(logits, dim=1).exp()
+    return pr.cpu().numpy(), vr[:, 0].cpu().numpy()
+
+
+@pytest.mark.parametrize("hidden", [256, 64])
+def test_predict_no_residual_blocks(mods, golden, hidden):
+    """nblocks = 0 (YachtNNet with an empty ModuleList: inp -> heads): the value head's v_head.2
+    weights come from their own load, not from a last trunk GEMM's ring (there is none)."""
+    K, N = mods
+    model = _torch_model(N, hidden, 0, 7)
+    net = N.YkNet(model.state_dict(), hidden, 0)
+    S = K.states_to_device(golden("states.npz")["states"][:1000])
+    pi, v = net.predict_states(S)
+    lp, lv = net.leaf_prior(S)
+    pr, vr = _torch_fp32(K, model, S)
+    np.testing.assert_allclose(pi.cpu().numpy(), pr, rtol=RTOL_PI, atol=ATOL_PI)
+    np.testing.assert_allclose(v.cpu().numpy(), vr, rtol=0, atol=ATOL_V)
+    assert torch.equal(v, lv)
+    assert net.errors() == 0
+
+
+def test_split_range_guard(mods, golden):
+    """yk_net_create refuses a finite weight the fp16 hi plane cannot hold (|w| >= 65520) with
+    YK_ERR_RANGE, in every packed matrix; weights at +-6e4 (inside the range) still predict within
+    1e-5 of torch fp32.  The mixed-precision trainer (fp16 weight casts) refuses the same."""
+    K, N = mods
+    from yacht_amd._lib import YK_ERR_RANGE, YkError
+    from yacht_amd.train import Trainer
+    model = _torch_model(N, 256, 6, 11)
+    base = {k: t.detach().clone() for k, t in model.state_dict().items()}
+    for name in ("inp.0.weight", "blocks.0.fc1.weight", "blocks.5.fc2.weight", "pi_head.2.weight",
+                 "v_head.2.weight"):
+        sd = {k: t.clone() for k, t in base.items()}
+        sd[name][3, 7] = 1e5 if name != "blocks.5.fc2.weight" else -65520.0
+        with pytest.raises(YkError) as e:
+            N.YkNet(sd, 256, 6)
+        assert e.value.code == YK_ERR_RANGE, name
+        with pytest.raises(YkError) as e:
+            Trainer(sd, 256, 6, max_batch=64, dropout=0.0, seed=0, amp=True)
+        assert e.value.code == YK_ERR_RANGE, name
+    sd = {k: t.clone() for k, t in base.items()}
+    sd["blocks.0.fc1.weight"][3, 7] = 6e4
+    sd["blocks.2.fc2.weight"][5, 9] = -6e4
+    model.load_state_dict(sd)
+    net = N.YkNet(sd, 256, 6)
+    S = K.states_to_device(golden("states.npz")["states"][:1000])
+    pi, v = net.predict_states(S)
+    pr, vr = _torch_fp32(K, model, S)
+    np.testing.assert_allclose(pi.cpu().numpy(), pr, rtol=RTOL_PI, atol=ATOL_PI)
+    np.testing.assert_allclose(v.cpu().numpy(), vr, rtol=0, atol=ATOL_V)
+    assert net.errors() == 0

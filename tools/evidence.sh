@@ -17,6 +17,8 @@
 #   amp         per-wave stamps of the AMP train step (YK_AMP_TIMING build, tools/diag_amp.py)
 #   xlane       tools/_xlane_check: the DPP / permlane exchanges against __shfl_xor
 #   dist2       2 gloo ranks sharing the GPU (tools/dist_rehearsal.sh) -> gpurun_out/dist2_TAG.json
+#   spawn2      the same through bench.py's own launcher (--gpus 2, no torchrun) -> gpurun_out/spawn2_TAG.json
+#   cores       bench.host_cores(): affinity mask, cgroup quota, OMP_NUM_THREADS of the box
 # Example: tools/evidence.sh r05a tests bench prof ab:3:contract=-DXP_CONTRACT
 cd "$(dirname "$0")/.." || exit 2
 tag=$1
@@ -42,6 +44,8 @@ for r in "$@"; do
     amp) steps+=("amp_ts:120:YK_LIB_PATH=tools/_variants/amp/libyacht_hip.so python -u tools/diag_amp.py") ;;
     xlane) steps+=("xlane:60:tools/_xlane_check") ;;
     dist2) steps+=("dist2:600:bash tools/dist_rehearsal.sh > gpurun_out/dist2_$tag.json") ;;
+    spawn2) steps+=("spawn2:600:python3 -u bench.py --gpus 2 --dist-backend gloo --envs 1024 --sims 25 --steps 1 --warmup 1 --coach-games 1024 --no-steady > gpurun_out/spawn2_$tag.json") ;;
+    cores) steps+=('cores:60:python3 -c "import bench, json; print(json.dumps(bench.host_cores()))"') ;;
     *) echo "unknown recipe $r" >&2; exit 2 ;;
   esac
 done
