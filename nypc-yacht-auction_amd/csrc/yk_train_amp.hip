@@ -1329,6 +1329,12 @@ __device__ __forceinline__ double sq_total(const double* part, int n) {
     __syncthreads();
     return tot;
 }
+// the gradient norm's partials summed once (sq_total's order, so the same bits as every update block
+// summing them itself), ahead of k_amp_update: its blocks then read one double
+__global__ __launch_bounds__(256) void k_amp_norm(const double* __restrict__ part, int n, double* __restrict__ out) {
+    const double t = sq_total(part, n);
+    if (threadIdx.x == 0) *out = t;
+}
 // fp16 fragments of one weight matrix W[N][K] (f32, row-major): `trans` packs W^T
 struct PackJob {
     const float* W;
@@ -1420,7 +1426,8 @@ __global__ __launch_bounds__(256) void k_amp_update(const UpdJob* __restrict__ j
         }
         return;
     }
-    const double total = sq_total(part, npart);  // (k_amp_sq's SQ_BLOCKS partials or the fused norm's slots)
+    // (k_amp_sq's SQ_BLOCKS partials or the fused norm's slots; npart 1: k_amp_norm's total)
+    const double total = npart == 1 ? part[0] : sq_total(part, npart);
     const Scaler s0 = *sc;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         *sq_out = total;
@@ -1544,6 +1551,9 @@ __global__ __launch_bounds__(256) void k_amp_update(const UpdJob* __restrict__ j
 #ifndef YK_DW_KG
 #define YK_DW_KG 2
 #endif
+#ifndef AMP_NORM_PASS
+#define AMP_NORM_PASS 0
+#endif
 namespace yk {
 
 struct AmpTrain {
@@ -1566,6 +1576,7 @@ struct AmpTrain {
     int n_pk_jobs = 0;
     long pk_total = 0;
     double* sqpart = nullptr;
+    double* sq_fin = nullptr;       // k_amp_norm's total (AMP_NORM_PASS)
     double* sq_items = nullptr;     // the fused norm's per-item partials (yk_trainer_step)
     bool norm_ready = false;        // the last backward left the total in sq_tot
     Scaler* sc = nullptr;       // the current GradScaler state
@@ -1673,6 +1684,7 @@ int amp_create(AmpTrain** out, int H, int NB, int Bmax, float* P, float* G, cons
     AA(d.dbpi_part, T * LDL);
     AA(d.colpart, T * d.NVEC * H);
     AA(a->sqpart, (size_t)SQ_BLOCKS);
+    AA(a->sq_fin, 1);
     AA(a->sc, 1);
     AA(a->sc_next, 1);
     if (rc != YK_OK) {
@@ -1918,9 +1930,17 @@ int amp_apply(AmpTrain* a, long nparams, float* M, float* V, double* sq_out, flo
         YK_LAUNCHED();
     }
     const long nm = dropout > 0.f ? (long)(1 + a->NB) * a->Bmax * (a->H / 4) : 0;
+    const double* part = fused ? a->sq_items : a->sqpart;
+    int npart = fused ? a->n_norm_dw + a->n_vs_items : SQ_BLOCKS;
+#if AMP_NORM_PASS
+    hipLaunchKernelGGL(k_amp_norm, dim3(1), dim3(256), 0, s, part, npart, a->sq_fin);
+    YK_LAUNCHED();
+    part = a->sq_fin;
+    npart = 1;
+#endif
     hipLaunchKernelGGL(k_amp_update, dim3((unsigned)(a->n_upd_items + (nm + 255) / 256)), dim3(256), 0, s, a->upd_jobs,
-                       a->upd_items, fused ? a->sq_items : a->sqpart, sq_out, a->sc, a->sc_next, max_norm, lr, wd, b1, b2, eps, a->n_upd_items,
-                       a->d, dropout, seed, next_step, fused ? a->n_norm_dw + a->n_vs_items : SQ_BLOCKS);
+                       a->upd_items, part, sq_out, a->sc, a->sc_next, max_norm, lr, wd, b1, b2, eps, a->n_upd_items,
+                       a->d, dropout, seed, next_step, npart);
     YK_LAUNCHED();
     a->mask_valid = nm > 0;
     a->mask_seed = seed;
