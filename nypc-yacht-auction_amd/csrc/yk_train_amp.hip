@@ -1301,6 +1301,9 @@ __global__ __launch_bounds__(256) void k_amp_grads(const DwJob* __restrict__ job
 }
 
 // ------------------------------------------------------------------ optimiser
+#ifndef AMP_MASKS_PER_THREAD
+#define AMP_MASKS_PER_THREAD 1  // k_amp_update's mask blocks: dropout bytes per thread
+#endif
 // GradScaler.unscale_: the norm of the unscaled gradients (an inf / nan anywhere makes it so)
 __global__ void k_amp_sq(const float* __restrict__ g, long n, const Scaler* sc, double* __restrict__ part) {
     __shared__ double red[4];
@@ -1419,10 +1422,13 @@ __global__ __launch_bounds__(256) void k_amp_update(const UpdJob* __restrict__ j
     __shared__ _Float16 Tl[32][40];
     if ((int)blockIdx.x >= n_upd) {  // the blocks past the update's: the next step's dropout draws
         const int q4 = d.H / 4;       // (k_amp_masks' work for row offset 0 and every row of Bmax)
-        const long i = (long)(blockIdx.x - n_upd) * 256 + threadIdx.x;
-        if (i < (long)(1 + d.NB) * d.Bmax * q4) {
-            const int q = (int)(i % q4), row = (int)((i / q4) % d.Bmax), L = (int)(i / ((long)q4 * d.Bmax));
-            d.masks[((long)L * d.Bmax + row) * q4 + q] = (uint8_t)dropout_bits(mseed, L, mstep, (long)row * q4 + q, mp);
+#pragma unroll
+        for (int j = 0; j < AMP_MASKS_PER_THREAD; j++) {
+            const long i = ((long)(blockIdx.x - n_upd) * AMP_MASKS_PER_THREAD + j) * 256 + threadIdx.x;
+            if (i < (long)(1 + d.NB) * d.Bmax * q4) {
+                const int q = (int)(i % q4), row = (int)((i / q4) % d.Bmax), L = (int)(i / ((long)q4 * d.Bmax));
+                d.masks[((long)L * d.Bmax + row) * q4 + q] = (uint8_t)dropout_bits(mseed, L, mstep, (long)row * q4 + q, mp);
+            }
         }
         return;
     }
@@ -1938,7 +1944,8 @@ int amp_apply(AmpTrain* a, long nparams, float* M, float* V, double* sq_out, flo
     part = a->sq_fin;
     npart = 1;
 #endif
-    hipLaunchKernelGGL(k_amp_update, dim3((unsigned)(a->n_upd_items + (nm + 255) / 256)), dim3(256), 0, s, a->upd_jobs,
+    constexpr long MB = 256L * AMP_MASKS_PER_THREAD;  // dropout bytes per mask block
+    hipLaunchKernelGGL(k_amp_update, dim3((unsigned)(a->n_upd_items + (nm + MB - 1) / MB)), dim3(256), 0, s, a->upd_jobs,
                        a->upd_items, part, sq_out, a->sc, a->sc_next, max_norm, lr, wd, b1, b2, eps, a->n_upd_items,
                        a->d, dropout, seed, next_step, npart);
     YK_LAUNCHED();

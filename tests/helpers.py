@@ -50,11 +50,16 @@ def renorm64(pi, ok):
     return np.divide(p, s, out=np.zeros_like(p), where=s > 0), s
 
 
-def check_recorded_priors(pi, v, cnt, leaves, sd, hidden=256, nblocks=6, every=1):
+def check_recorded_priors(pi, v, cnt, leaves, sd, hidden=256, nblocks=6, every=1, net=None):
     """The recorded priors (the production valid-only forward inside the engine, Ps * valids)
     renormalised as MCTS.py:88-91 does vs a float64 forward put through the same lines: zero
     outside the valid set; within the north-star tolerance in predict space; P and v no further
-    from exact than REF_FACTOR x the reference's own f32 forward (v: or within 1e-5)."""
+    from exact than REF_FACTOR x the reference's own f32 forward (v: or within 1e-5).
+    net (a f32-mode YkNet of the same weights, GPU runs): the priors are also held at the north
+    star's 1e-5 itself (rtol, predict space) against yk_net_predict's pi of the same leaves put
+    through the same renormalisation - the predict test_gpu_net holds to 1e-5 of torch fp32 - so
+    the engine's own ops (valid-only softmax statistics, exp_acc, the renormalising sum) add no
+    more than that; v equal to predict's within 1e-6."""
     rs = np.concatenate([np.full(len(range(0, int(c), every)), r) for r, c in enumerate(cnt)])
     ks = np.concatenate([np.arange(0, int(c), every) for c in cnt])
     S = leaves[rs, ks]
@@ -69,6 +74,20 @@ def check_recorded_priors(pi, v, cnt, leaves, sd, hidden=256, nblocks=6, every=1
     Pt[none, 0] = 1.0  # no valid action: P is one-hot on action 0 (MCTS.py:108-111)
     Pe = O.mcts_prior(P, S).astype(np.float64)  # exactly as the reference renormalises (f32, pairwise)
     np.testing.assert_allclose(Pe * mass, Pt * mass, rtol=RTOL_PI, atol=ATOL_PI)
+    if net is not None and getattr(net, "precision", "f32") == "f32":
+        from yacht_amd import kernels as K
+        gp, gv = [], []
+        for i in range(0, len(S), 4096):
+            p_, v_ = net.predict_states(K.states_to_device(np.ascontiguousarray(S[i:i + 4096])))
+            gp.append(p_.cpu().numpy())
+            gv.append(v_.cpu().numpy())
+        Pg, _ = renorm64(np.concatenate(gp), ok)
+        Pg[none, 0] = 1.0
+        d = np.abs(Pe - Pg) * mass
+        tol = 1e-5 * np.abs(Pg) * mass + ATOL_PI
+        print(f"engine priors vs yk_net_predict, predict space: max |d| / (1e-5 |pi| + 1e-7) = {float((d / tol).max()):.3f}")
+        np.testing.assert_allclose(Pe * mass, Pg * mass, rtol=1e-5, atol=ATOL_PI)
+        np.testing.assert_allclose(v[rs, ks], np.concatenate(gv), rtol=0, atol=1e-6)
     # v within 1e-5 of exact, or no worse than the reference's own f32 CPU forward (x REF_FACTOR);
     # P no worse than that forward, relative to exact arithmetic
     rpi, rv = torch_predict(sd, hidden, nblocks, S, torch.float32)

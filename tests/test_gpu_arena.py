@@ -138,7 +138,8 @@ def test_arena_1000_games_net_prior_replayed_by_oracle(Y):
     n, sims, seed, base = 1000, 25, 4711, 100000
     sd = spec.closed_form_weights(256, 6)
     seats = np.where(np.arange(n) < n // 2, 1, -1).astype(np.int32)
-    eng = E.SelfPlayEngine(n, sims, 1.5, 0, net=N.YkNet(sd, 256, 6), max_moves=48, record_predictions=True,
+    ynet = N.YkNet(sd, 256, 6)
+    eng = E.SelfPlayEngine(n, sims, 1.5, 0, net=ynet, max_moves=48, record_predictions=True,
                            max_expansions=24 * sims + 16)
     eng.arena(seats, seed, base)
     r = eng.arena_results()
@@ -148,7 +149,7 @@ def test_arena_1000_games_net_prior_replayed_by_oracle(Y):
                 threads=16)
     assert np.array_equal(o["stats"][:, 1], cnt)
     _compare_arena(r, o, n)
-    assert check_recorded_priors(pi, v, cnt, leaves, sd, every=40) > 10000
+    assert check_recorded_priors(pi, v, cnt, leaves, sd, every=40, net=ynet) > 10000
 
 
 def test_arena_after_selfplay_and_back(Y):

@@ -95,7 +95,7 @@ def test_config5_two_coach_iterations(tmp_path, monkeypatch):
     from yacht_amd import kernels as K
     from yacht_amd.coach import Coach
     from yacht_amd.game import YachtGame
-    from yacht_amd.nnet import NNetWrapper
+    from yacht_amd.nnet import NNetWrapper, YkNet
     from yacht_amd.train import Trainer
     from yacht_amd.utils import dotdict
     d = str(tmp_path)
@@ -187,7 +187,7 @@ def test_config5_two_coach_iterations(tmp_path, monkeypatch):
         assert play["rec"]["n_moves"].min() == 48
         _replay_sampled_games(play)
     assert check_recorded_priors(plays[0]["pi"], plays[0]["v"], plays[0]["cnt"], plays[0]["leaves"],
-                                 plays[0]["sd"], every=16) > 3000
+                                 plays[0]["sd"], every=16, net=YkNet(plays[0]["sd"], 256, 6)) > 3000
 
     # ---- the pooled examples, per iteration, against the host restatement of its image
     for k in range(2):

@@ -113,7 +113,7 @@ def test_selfplay_net_prior_replayed_by_oracle(Y):
     _compare_to_oracle(rec, orc, n)
     # every recorded prediction (root and non-root expansions) is the f32 MLP within tolerance
     assert np.array_equal(leaves[:, 0], rec["states"][:, 0])  # the first expansion is the root
-    assert check_recorded_priors(pi, v, cnt, leaves, sd) == int(cnt.sum())
+    assert check_recorded_priors(pi, v, cnt, leaves, sd, net=net) == int(cnt.sum())
 
 
 def _first_divergence(a_moves, a_counts, b_moves, b_counts, n):
@@ -156,7 +156,8 @@ def _net_prior_sampled_games_vs_oracle(E, N, n, sims, seed, base, stride, diverg
     (visit counts of every move, actions, counters, values, final boards), and the recorded
     priors match the oracle net.  Returns the engine stats."""
     sd = spec.closed_form_weights(256, 6)
-    eng = E.SelfPlayEngine(n, sims, 1.5, 15, net=N.YkNet(sd, 256, 6), max_moves=48, record_predictions=True,
+    ynet = N.YkNet(sd, 256, 6)
+    eng = E.SelfPlayEngine(n, sims, 1.5, 15, net=ynet, max_moves=48, record_predictions=True,
                            max_expansions=48 * sims + 8, record_stride=stride)
     eng.run(seed, base)
     st = eng.stats()
@@ -179,7 +180,7 @@ def _net_prior_sampled_games_vs_oracle(E, N, n, sims, seed, base, stride, diverg
             assert np.array_equal(_dense_counts(rec, e, m), orc["counts"][r, m]), (e, m)
         assert np.array_equal(rec["values"][e, :M], orc["values"][r, :M])
         assert np.array_equal(rec["final"][e], orc["final"][r])
-    assert check_recorded_priors(pi, v, cnt, leaves, sd, every=16) > 10000
+    assert check_recorded_priors(pi, v, cnt, leaves, sd, every=16, net=ynet) > 10000
     if divergence:
         frac, first, frac_ff, first_ff = _divergence_vs_independent_f32(rec, pick, sd, sims, seed, base)
 
