@@ -1,6 +1,6 @@
 """Fixtures of the engine's production path (YachtNNet prior, no prediction recording).  usage:
-python tools/engine_records_dump.py records OUT.npz   the records of a small self-play batch
-python tools/engine_records_dump.py images OUT.npz    packed record images (yk_engine_pack_records)
+python tests/golden/engine_records_dump.py records OUT.npz   the records of a small self-play batch
+python tests/golden/engine_records_dump.py images OUT.npz    packed record images (yk_engine_pack_records)
     of games [0, 3) and [3, 6) ("rank 0" / "rank 1", env ids 0-5) and of all six in one batch:
     tests/golden/engine_images.npz, which the CPU all-gather test (tests/test_dist_cpu.py) pools
 (YK_LIB_PATH selects the library)"""
@@ -9,8 +9,8 @@ import sys
 
 import numpy as np
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "nypc-yacht-auction_amd"))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "nypc-yacht-auction_amd"))
 from oracle import spec  # noqa: E402
 from yacht_amd.engine import SelfPlayEngine  # noqa: E402
 from yacht_amd.nnet import YkNet  # noqa: E402

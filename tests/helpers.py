@@ -133,3 +133,67 @@ def dropout_keep_np(seed, layer, step, rows, H, p, row_base=0):
     u = (d[:, :, None] >> (np.uint64(16) * np.arange(4, dtype=np.uint64))) & np.uint64(0xFFFF)
     keep = u.astype(np.float32) * np.float32(1.0 / 65536.0) >= np.float32(p)
     return keep.reshape(rows, H)
+
+
+# ---- the replay examples from host copies of record images (numpy; yk_examples_from_records restated)
+def host_examples(images: np.ndarray, n_envs: int, max_moves: int, sims: int, n_games: int = -1) -> dict:
+    """The same examples from host copies of the record images, with the full policies
+    (Coach.py:57-61: MCTS.getActionProb's pi per move - one-hot at the played action at temp 0,
+    N / sum(N) at temp 1, MCTS.py:44-54) as a sparse CSR.  An
+    independent restatement of yk_examples_from_records / yk_examples_policies (tests, the 2-rank
+    CPU rehearsal).  Test infrastructure (moved here from yacht_amd/replay.py in round 6)."""
+    from yacht_amd.engine import unpack_record_image
+    from yacht_amd.replay import _vcap
+    imgs = np.ascontiguousarray(images).reshape(images.shape[0] if images.ndim > 1 else 1, -1)
+    total_games = imgs.shape[0] * n_envs
+    n_games = total_games if n_games is None or n_games < 0 else min(n_games, total_games)
+    parts = {k: [] for k in ("states", "values", "targets", "cols", "vals", "lens")}
+    for r in range(imgs.shape[0]):
+        g = min(max(n_games - r * n_envs, 0), n_envs)
+        if g == 0:
+            continue
+        img = unpack_record_image(imgs[r], n_envs, max_moves, sims)
+        nm = np.clip(img["n_moves"][:g], 0, max_moves)
+        mask = np.arange(max_moves)[None, :] < nm[:, None]
+        e_idx, m_idx = np.nonzero(mask)
+        info = img["info"][:g][mask]
+        temp, action = info[:, 0], info[:, 2]
+        voff = img["voff"]
+        a0, a1 = voff[e_idx, m_idx].astype(np.int64), voff[e_idx, m_idx + 1].astype(np.int64)
+        hot = temp != 0
+        lens = np.where(hot, a1 - a0, 1)
+        n = len(temp)
+        starts = np.concatenate([[0], np.cumsum(lens)])
+        within = np.arange(starts[-1]) - np.repeat(starts[:-1], lens)
+        row = np.repeat(np.arange(n), lens)
+        vcap = _vcap(max_moves, sims)
+        raw = img["visits_raw"].reshape(-1)[(e_idx[row].astype(np.int64) * vcap + a0[row] + within)
+                                           .clip(0, n_envs * vcap - 1)]
+        cols = np.where(hot[row], (raw >> 16).astype(np.int64), action[row].astype(np.int64))
+        cnt = np.where(hot[row], (raw & 0xFFFF).astype(np.float64), 1.0)
+        sums = np.bincount(row, weights=cnt, minlength=n)
+        vals = cnt / np.where(sums[row] > 0, sums[row], 1.0)
+        # argmax(pi): the most visited action, the lowest on ties (ascending action order)
+        mx = np.zeros(n)
+        np.maximum.at(mx, row, cnt)
+        big = np.iinfo(np.int64).max
+        first = np.full(n, big, dtype=np.int64)
+        np.minimum.at(first, row, np.where(cnt == mx[row], cols, big))
+        targets = np.where((first == big) | (mx == 0), action, first).astype(np.int32)
+        keep = cnt > 0  # the examples file stores the nonzero entries of pi
+        kl = np.bincount(row[keep], minlength=n)
+        parts["states"].append(img["states"][:g][mask])
+        parts["values"].append(img["values"][:g][mask])
+        parts["targets"].append(targets)
+        parts["cols"].append(cols[keep].astype(np.int32))
+        parts["vals"].append(vals[keep])
+        parts["lens"].append(kl)
+    cat = {k: (np.concatenate(v) if v else None) for k, v in parts.items()}
+    n = 0 if cat["targets"] is None else len(cat["targets"])
+    lens = cat["lens"] if cat["lens"] is not None else np.zeros(0, np.int64)
+    return dict(states=cat["states"] if n else np.zeros((0, 8), np.uint64),
+                values=cat["values"] if n else np.zeros(0),
+                targets=cat["targets"] if n else np.zeros(0, np.int32),
+                pi_indptr=np.concatenate([[0], np.cumsum(lens)]).astype(np.int64),
+                pi_cols=cat["cols"] if n else np.zeros(0, np.int32),
+                pi_vals=cat["vals"] if n else np.zeros(0))

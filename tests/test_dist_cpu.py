@@ -1,8 +1,8 @@
 """Multi-rank trajectory pooling on CPU: world_size 2 over gloo (no GPU).
 
 The images are real engine output (tests/golden/engine_images.npz, written on an MI355X by
-tools/engine_records_dump.py images): games 0-2 as "rank 0", games 3-5 as "rank 1", and all six
-in one batch.  Each rank all-gathers its image; the pooled examples (replay.host_examples) must
+tests/golden/engine_records_dump.py images): games 0-2 as "rank 0", games 3-5 as "rank 1", and all six
+in one batch.  Each rank all-gathers its image; the pooled examples (helpers.host_examples) must
 equal those of the single six-game batch, and every field of every gathered image must come
 back intact and in rank order."""
 import os
@@ -32,7 +32,7 @@ def _worker(rank, world, port, q):
                       LOCAL_RANK=str(rank))
     from yacht_amd import dist as D
     from yacht_amd.engine import unpack_record_image
-    from yacht_amd.replay import host_examples
+    from helpers import host_examples
     r, w, _ = D.setup(backend="gloo")
     g = np.load(os.path.join(GOLDEN, "engine_images.npz"))
     E, M, sims = int(g["per_rank"]), int(g["max_moves"]), int(g["sims"])
@@ -75,7 +75,7 @@ def test_host_examples_of_the_fixture():
     """The pooled examples' content: 48 per game, temp 1 for the first 14 moves (tempThreshold
     15, Coach.py:58), pi summing to 1, the target the argmax of pi."""
     from conftest import GOLDEN
-    from yacht_amd.replay import host_examples
+    from helpers import host_examples
     g = np.load(os.path.join(GOLDEN, "engine_images.npz"))
     h = host_examples(g["img_all"], 2 * int(g["per_rank"]), int(g["max_moves"]), int(g["sims"]))
     n = len(h["targets"])

@@ -2,7 +2,7 @@
 (Coach.py:74-139).
 
 * yk_examples_from_records (the device replay buffer) against two independent host
-  restatements: replay.host_examples (numpy over the packed image) and coach.examples_from_records
+  restatements: helpers.host_examples (numpy over the packed image) and coach.examples_from_records
   (the reference's per-move (board, pi, v) tuples, argmax'd as NNet.py:145-146 does);
 * sharding: the images of games split over "ranks" pool into exactly the single-batch examples;
 * two ranks (gloo) sharing GPU 0 run the Coach's pieces and Coach.learn: the pooled buffer is
@@ -16,6 +16,7 @@ import socket
 import numpy as np
 import pytest
 
+from helpers import host_examples
 from oracle import spec
 
 pytestmark = pytest.mark.gpu
@@ -58,7 +59,7 @@ def test_examples_kernel_matches_host_restatements(Y):
     net = N.YkNet(spec.closed_form_weights(256, 6), 256, 6)
     rec, img = _selfplay(E, net, n, sims, seed, base)
     shard = R.examples_from_images(img, n, 48, sims)
-    h = R.host_examples(img.cpu().numpy(), n, 48, sims)
+    h = host_examples(img.cpu().numpy(), n, 48, sims)
     _assert_same_examples(shard, h)
     # the reference's tuples (Coach.py:72) -> argmax(pi) (NNet.py:145-146), values, boards
     ref = [ex for ep in C.examples_from_records(rec, n) for ex in ep]

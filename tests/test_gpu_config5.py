@@ -9,7 +9,7 @@ dropout 0.3, numItersForTrainExamplesHistory 5, arenaCompare 10.  Checked:
   final boards), and the first iteration's recorded priors are held against a float64 forward
   (helpers.check_recorded_priors);
 * the pooled history: each iteration's ExampleShard equals the host restatement
-  (replay.host_examples) of that iteration's record image, trimmed to the maxlenOfQueue deque's
+  (helpers.host_examples) of that iteration's record image, trimmed to the maxlenOfQueue deque's
   newest 200,000 examples (Coach.py:86-90), and the second iteration trains on both entries
   (Coach.py:99-111);
 * the trainer Coach.learn itself ran: its first 3 amp steps (dropout 0.3) are recorded as they
@@ -27,7 +27,7 @@ import numpy as np
 import pytest
 
 from oracle import oracle as O
-from helpers import check_recorded_priors, dropout_keep_np
+from helpers import check_recorded_priors, dropout_keep_np, host_examples
 
 pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
@@ -66,9 +66,9 @@ def _replay_sampled_games(play):
 
 
 def _same_as_host(shard, img):
-    """The pooled device examples == replay.host_examples of the record image, deque-trimmed."""
+    """The pooled device examples == helpers.host_examples of the record image, deque-trimmed."""
     from yacht_amd import replay as R
-    h = R.host_examples(img[None], GAMES, 48, SIMS)
+    h = host_examples(img[None], GAMES, 48, SIMS)
     total = len(h["targets"])
     assert total == GAMES * 48
     skip = total - MAXLEN

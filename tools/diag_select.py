@@ -1,4 +1,4 @@
-"""Diagnostic: where k_select's time goes (needs the -DYK_SEL_TIMING library, tools/diag_select.sh)."""
+"""Diagnostic: where k_select's time goes (needs the -DYK_SEL_TIMING library, `tools/variant_lib.sh sel -DYK_SEL_TIMING`; tools/evidence.sh select)."""
 import ctypes as C
 import os
 import sys
