@@ -799,7 +799,13 @@ def main():
                                       f"16 x {st.get('scan_edges', 0)} edges gathered + 32 x {st['path_edges']} path "
                                       f"edges + 10 x {st['vnew']} new valid entries + 364 x {st['expansions']} "
                                       f"expansions) / {launches} launches",
-                   "survey_formula_bytes_per_launch": survey_b}
+                   "survey_formula_bytes_per_launch": survey_b,
+                   # SURVEY 8d's byte basis (4 / 16 / 4 / 364 B; rounds 1-4 priced the kernel on it): the
+                   # like-for-like fraction across rounds
+                   "frac_survey_formula": survey_b / (per["expand_backup_select"][0] * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                   "frac_basis": "frac: the kernel's own bytes (6 B per scanned entry, 16 B per gathered edge, 32 B "
+                                 "per path edge, 10 B per new valid entry, 364 B per expansion; since round 5); "
+                                 "frac_survey_formula: SURVEY 8d's formula"}
         if dom == "forward":
             out["roofline"], out["roofline_env"] = fwd, env
         else:
