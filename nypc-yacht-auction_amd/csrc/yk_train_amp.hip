@@ -69,9 +69,6 @@ constexpr int BQ = YK_BQ;       // head-backward action parts per row tile (12: 
                                 // profiles/r05ze_head_parts_trainab.log)
 constexpr int VH = 128;         // v_head hidden width
 constexpr int SQ_BLOCKS = 1024;
-#ifndef AMP_NORM_TICKET
-#define AMP_NORM_TICKET 0  // k_amp_grads' last block sums the norm's partials (no per-block sum in k_amp_update)
-#endif
 
 struct Scaler {  // GradScaler('cuda') state + the AdamW step count (device)
     float scale;
@@ -922,15 +919,6 @@ __device__ __forceinline__ double dw_item(const DwJob* __restrict__ jobs, const 
     }
     return norm ? wave_dsum(ss) : 0.0;
 }
-// a norm partial into its slot: with the last-block ticket (AMP_NORM_TICKET) an agent-scope store (sc1:
-// written through to the device's coherence point, which the last block's agent-scope loads read)
-__device__ __forceinline__ void put_partial(double* slot, double v) {
-#if AMP_NORM_TICKET
-    __hip_atomic_store(slot, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#else
-    *slot = v;
-#endif
-}
 // a block's waves' norm partials -> sqp[slot] (wave order: fixed bits); every thread calls it
 template <int NW>
 __device__ __forceinline__ void block_norm(double ss, double* __restrict__ sqp, int slot) {
@@ -941,7 +929,7 @@ __device__ __forceinline__ void block_norm(double ss, double* __restrict__ sqp, 
         double t = 0.0;
 #pragma unroll
         for (int k = 0; k < NW; k++) t += red[k];
-        put_partial(sqp + slot, t);
+        sqp[slot] = t;
     }
 }
 
@@ -1283,7 +1271,7 @@ __device__ __forceinline__ void vecsum_item(const VsJob* __restrict__ jobs, cons
     }
     if (sqp && threadIdx.x < 64) {  // (the 16 column threads are wave 0's lanes 0-15)
         ss = wave_dsum(ss);
-        if (threadIdx.x == 0) put_partial(sqp + slot, ss);
+        if (threadIdx.x == 0) sqp[slot] = ss;
     }
 }
 // after k_amp_bwd: the trunk's weight gradients (dw_item, a wave each; the heads' ran inside
@@ -1297,8 +1285,7 @@ __global__ __launch_bounds__(256) void k_amp_grads(const DwJob* __restrict__ job
                                                    int nitems, int RS, int rsn, const VsJob* __restrict__ vjobs,
                                                    const int2* __restrict__ vitems, int nvitems, int ntiles,
                                                    int nhtiles, int B, double* __restrict__ sqp, int nall,
-                                                   const Scaler* __restrict__ sc, int* __restrict__ ticket,
-                                                   double* __restrict__ sq_total_out) {
+                                                   const Scaler* __restrict__ sc) {
     __shared__ float part[16][17];
     const float inv = sqp ? 1.0f / sc->scale : 1.f;
     const int ndb = (nitems + 3) / 4;
@@ -1311,39 +1298,9 @@ __global__ __launch_bounds__(256) void k_amp_grads(const DwJob* __restrict__ job
         if (w < nitems) ss = dw_item(jobs, items[w], RS, rsn, threadIdx.x & 63, sqp != nullptr, inv);
         if (sqp) block_norm<4>(ss, sqp, blockIdx.x);
     }
-#if AMP_NORM_TICKET
-    // the last block to finish sums every partial (this launch's and k_amp_bwd's) in sq_total's order:
-    // each block's partial store completes (vmcnt 0) before its ticket, the last reads the slots with
-    // agent-scope loads - no release fence (an L2 writeback per block cost 12 -> 96 us)
-    if (sqp) {
-        __shared__ int last;
-        if (threadIdx.x == 0) {
-            __builtin_amdgcn_s_waitcnt(0);
-            last = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1;
-        }
-        __syncthreads();
-        if (last) {
-            const int n = nall + nvitems;
-            __shared__ double red[4];
-            double t = 0.0;
-#pragma unroll 8
-            for (int i = threadIdx.x; i < n; i += 256) t += __hip_atomic_load(sqp + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            t = xlane_sum(t);
-            if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = t;
-            __syncthreads();
-            if (threadIdx.x == 0) {
-                *sq_total_out = (red[0] + red[1]) + (red[2] + red[3]);
-                __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // the next step's
-            }
-        }
-    }
-#endif
 }
 
 // ------------------------------------------------------------------ optimiser
-#ifndef AMP_MASKS_PER_THREAD
-#define AMP_MASKS_PER_THREAD 1  // k_amp_update's mask blocks: dropout bytes per thread
-#endif
 // GradScaler.unscale_: the norm of the unscaled gradients (an inf / nan anywhere makes it so)
 __global__ void k_amp_sq(const float* __restrict__ g, long n, const Scaler* sc, double* __restrict__ part) {
     __shared__ double red[4];
@@ -1371,12 +1328,6 @@ __device__ __forceinline__ double sq_total(const double* part, int n) {
     const double tot = (red[0] + red[1]) + (red[2] + red[3]);
     __syncthreads();
     return tot;
-}
-// the gradient norm's partials summed once (sq_total's order, so the same bits as every update block
-// summing them itself), ahead of k_amp_update: its blocks then read one double
-__global__ __launch_bounds__(256) void k_amp_norm(const double* __restrict__ part, int n, double* __restrict__ out) {
-    const double t = sq_total(part, n);
-    if (threadIdx.x == 0) *out = t;
 }
 // fp16 fragments of one weight matrix W[N][K] (f32, row-major): `trans` packs W^T
 struct PackJob {
@@ -1462,18 +1413,14 @@ __global__ __launch_bounds__(256) void k_amp_update(const UpdJob* __restrict__ j
     __shared__ _Float16 Tl[32][40];
     if ((int)blockIdx.x >= n_upd) {  // the blocks past the update's: the next step's dropout draws
         const int q4 = d.H / 4;       // (k_amp_masks' work for row offset 0 and every row of Bmax)
-#pragma unroll
-        for (int j = 0; j < AMP_MASKS_PER_THREAD; j++) {
-            const long i = ((long)(blockIdx.x - n_upd) * AMP_MASKS_PER_THREAD + j) * 256 + threadIdx.x;
-            if (i < (long)(1 + d.NB) * d.Bmax * q4) {
-                const int q = (int)(i % q4), row = (int)((i / q4) % d.Bmax), L = (int)(i / ((long)q4 * d.Bmax));
-                d.masks[((long)L * d.Bmax + row) * q4 + q] = (uint8_t)dropout_bits(mseed, L, mstep, (long)row * q4 + q, mp);
-            }
+        const long i = (long)(blockIdx.x - n_upd) * 256 + threadIdx.x;
+        if (i < (long)(1 + d.NB) * d.Bmax * q4) {
+            const int q = (int)(i % q4), row = (int)((i / q4) % d.Bmax), L = (int)(i / ((long)q4 * d.Bmax));
+            d.masks[((long)L * d.Bmax + row) * q4 + q] = (uint8_t)dropout_bits(mseed, L, mstep, (long)row * q4 + q, mp);
         }
         return;
     }
-    // (k_amp_sq's SQ_BLOCKS partials or the fused norm's slots; npart 1: k_amp_norm's total)
-    const double total = npart == 1 ? part[0] : sq_total(part, npart);
+    const double total = sq_total(part, npart);  // (k_amp_sq's SQ_BLOCKS partials or the fused norm's slots)
     const Scaler s0 = *sc;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         *sq_out = total;
@@ -1597,9 +1544,6 @@ __global__ __launch_bounds__(256) void k_amp_update(const UpdJob* __restrict__ j
 #ifndef YK_DW_KG
 #define YK_DW_KG 2
 #endif
-#ifndef AMP_NORM_PASS
-#define AMP_NORM_PASS 0
-#endif
 namespace yk {
 
 struct AmpTrain {
@@ -1622,8 +1566,6 @@ struct AmpTrain {
     int n_pk_jobs = 0;
     long pk_total = 0;
     double* sqpart = nullptr;
-    double* sq_fin = nullptr;       // k_amp_norm's total (AMP_NORM_PASS) / the last grads block's (AMP_NORM_TICKET)
-    int* ticket = nullptr;          // k_amp_grads' finished-block count (AMP_NORM_TICKET; reset by the last)
     double* sq_items = nullptr;     // the fused norm's per-item partials (yk_trainer_step)
     bool norm_ready = false;        // the last backward left the total in sq_tot
     Scaler* sc = nullptr;       // the current GradScaler state
@@ -1731,8 +1673,6 @@ int amp_create(AmpTrain** out, int H, int NB, int Bmax, float* P, float* G, cons
     AA(d.dbpi_part, T * LDL);
     AA(d.colpart, T * d.NVEC * H);
     AA(a->sqpart, (size_t)SQ_BLOCKS);
-    AA(a->sq_fin, 1);
-    AA(a->ticket, 1);
     AA(a->sc, 1);
     AA(a->sc_next, 1);
     if (rc != YK_OK) {
@@ -1751,7 +1691,6 @@ int amp_create(AmpTrain** out, int H, int NB, int Bmax, float* P, float* G, cons
     YK_HIP(hipMemcpy(a->off_dev, offv.data(), sizeof(long) * ntens, hipMemcpyHostToDevice));
     Scaler s0{init_scale > 0.f ? init_scale : 65536.0f, 0, 0, 0, growth_interval > 0 ? growth_interval : 2000};
     YK_HIP(hipMemcpy(a->sc, &s0, sizeof(Scaler), hipMemcpyHostToDevice));
-    YK_HIP(hipMemset(a->ticket, 0, sizeof(int)));
     // weight-gradient jobs: (dU T layout, X T layout, gradient, N, K)
     std::vector<DwJob> jobs;
     auto tl4 = [](const _Float16* p) { return reinterpret_cast<const float4*>(p); };
@@ -1916,7 +1855,7 @@ int amp_backward(AmpTrain* a, const yk_state_t* states, const int32_t* targets, 
     }
     hipLaunchKernelGGL(k_amp_grads, dim3((unsigned)((a->n_dw_trunk + 3) / 4 + a->n_vs_items)), dim3(256), 0, s,
                        a->dw_jobs, a->dw_items, a->n_dw_trunk, a->RS, rsn, a->vs_jobs, a->vs_items, a->n_vs_items, TT, T,
-                       B, sqp, a->n_norm_dw, a->sc, a->ticket, a->sq_fin);
+                       B, sqp, a->n_norm_dw, a->sc);
     YK_LAUNCHED();
     a->norm_ready = fuse_norm;
     return YK_OK;
@@ -1979,23 +1918,9 @@ int amp_apply(AmpTrain* a, long nparams, float* M, float* V, double* sq_out, flo
         YK_LAUNCHED();
     }
     const long nm = dropout > 0.f ? (long)(1 + a->NB) * a->Bmax * (a->H / 4) : 0;
-    const double* part = fused ? a->sq_items : a->sqpart;
-    int npart = fused ? a->n_norm_dw + a->n_vs_items : SQ_BLOCKS;
-#if AMP_NORM_PASS
-    hipLaunchKernelGGL(k_amp_norm, dim3(1), dim3(256), 0, s, part, npart, a->sq_fin);
-    YK_LAUNCHED();
-    part = a->sq_fin;
-    npart = 1;
-#elif AMP_NORM_TICKET
-    if (fused) {
-        part = a->sq_fin;
-        npart = 1;
-    }
-#endif
-    constexpr long MB = 256L * AMP_MASKS_PER_THREAD;  // dropout bytes per mask block
-    hipLaunchKernelGGL(k_amp_update, dim3((unsigned)(a->n_upd_items + (nm + MB - 1) / MB)), dim3(256), 0, s, a->upd_jobs,
-                       a->upd_items, part, sq_out, a->sc, a->sc_next, max_norm, lr, wd, b1, b2, eps, a->n_upd_items,
-                       a->d, dropout, seed, next_step, npart);
+    hipLaunchKernelGGL(k_amp_update, dim3((unsigned)(a->n_upd_items + (nm + 255) / 256)), dim3(256), 0, s, a->upd_jobs,
+                       a->upd_items, fused ? a->sq_items : a->sqpart, sq_out, a->sc, a->sc_next, max_norm, lr, wd, b1, b2, eps, a->n_upd_items,
+                       a->d, dropout, seed, next_step, fused ? a->n_norm_dw + a->n_vs_items : SQ_BLOCKS);
     YK_LAUNCHED();
     a->mask_valid = nm > 0;
     a->mask_seed = seed;
