@@ -514,7 +514,9 @@ __device__ __forceinline__ uint32_t xlane_u(uint32_t v) {
     else {
         // v_permlane{16,32}_swap(v, v): the first result holds the lower row / half in both
         // positions, the second the upper
-        const bool upper = (__lane_id() & O) != 0;  // the lane's position in the wave, any launch shape
+        // (threadIdx.x & O is the lane's bit O for the 1-D workgroups of multiples of 64 threads every
+        // launch of this library uses; __lane_id()'s mbcnt pair cost the expand 0.8 us, r06d A/B)
+        const bool upper = (threadIdx.x & O) != 0;
         if constexpr (O == 16) {
             const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
             return upper ? r[0] : r[1];

@@ -237,9 +237,6 @@ __device__ __forceinline__ void layernorm(float (&x)[VPL], const float* g, const
 // operation, as numpy does); the forward's LayerNorm row passes - VALU-bound and on every layer's
 // critical path - contract their multiply-adds into v_pk_fma_f32 (one rounding instead of two: no
 // less accurate than torch's own LayerNorm kernels, which fuse them too).  Scoped per function.
-#ifndef FWD_SS_OWN
-#define FWD_SS_OWN 0  // the end phase's per-wave softmax statistics in their own LDS (one barrier, not two)
-#endif
 #define YK_ROW_CONTRACT _Pragma("clang fp contract(fast)")
 typedef float f2v __attribute__((ext_vector_type(2)));
 typedef _Float16 h2v __attribute__((ext_vector_type(2)));
@@ -1161,18 +1158,6 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
             ss[j] = t[j];
         }
     }
-#if FWD_SS_OWN
-    // the per-wave statistics in their own 1-2 KB (not T's storage, which slower waves may still be
-    // reading for v_head.2): stored as soon as a wave's merges end, one barrier before the row merge
-    __shared__ float2 SSo[NW * ROWS];
-    if (mlse && (lane & 15) == 0) {
-#pragma unroll
-        for (int j = 0; j < 4; j++) SSo[wave * ROWS + 4 * (lane >> 4) + j] = make_float2(sm[j], ss[j]);
-    }
-    SS = SSo;
-    if (mlse) {
-        lds_barrier();
-#else
     lds_barrier();  // every wave is done with v_head.2 (reads of T) and stored its av columns
     if (mlse && (lane & 15) == 0) {
 #pragma unroll
@@ -1180,7 +1165,6 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
     }
     if (mlse) {
         lds_barrier();
-#endif
         if (tid < ROWS && row0 + tid < n && ((amask >> tid) & 1u)) {  // (max, log sum exp(x - max)) of the row
             float2 q[NW];
             float m = -INFINITY, sm = 0.f;
