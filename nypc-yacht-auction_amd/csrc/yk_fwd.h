@@ -518,7 +518,7 @@ __device__ __forceinline__ void pi_chunk(const _Float16* A, int sa, W2 (&ring)[R
 // PL = 2: f32-equivalent hi/lo planes (the parity mode); PL = 1: one fp16 plane of weights and
 // GEMM inputs with f32 accumulation (the fp16 predict mode, as the reference's autocast('cuda')
 // predict, NNet.py:186-189; LayerNorm, SiLU, softmax and the value head stay f32)
-template <int H, int PL, int NW>
+template <int H, int PL, int NW, bool NB0 = false>
 __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __restrict__ states,
                                              const float* __restrict__ xin, const int32_t* __restrict__ rows,
                                              const int32_t* __restrict__ count, int n,
@@ -553,6 +553,7 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
     __shared__ uint32_t RM[ROWS][TMW];                       // each row's tile mask
     __shared__ uint16_t TRB[PI_TILES];                       // per tile: the rows that keep a column in it
     __shared__ uint32_t VHC;                                 // waves whose v_head.2 columns are in X
+    __shared__ uint32_t SYNC_LOST;                           // a value-head wait timed out (FWD_ERR_SYNC)
 
     if (count) n = min(n, *count);
     if (row0 >= n) return;
@@ -682,7 +683,10 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
     if (gw) ring_fill_part<PL, KS, NT, RW, RQ, RQ2>(ring, w_first, nt0);  // part 2 of the first fill
     __builtin_amdgcn_sched_barrier(0);
     if (tid < TMW) UM[tid] = 0u;
-    if (tid == 0) VHC = 0u;
+    if (tid == 0) {
+        VHC = 0u;
+        SYNC_LOST = 0u;
+    }
     lds_barrier();
     if (lane < TMW) {  // this wave's rows' tile masks, and into the union (read after the input barrier)
         uint32_t w = 0;
@@ -892,8 +896,9 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
         }
         lds_barrier();
     };
-    for (int b = 0; b + 1 < net.NB; b++) block(b, std::false_type{});
-    if (net.NB > 0) {
+    // NB0 (nblocks = 0, a separate instantiation: no runtime branch joins the ring's streams here)
+    if constexpr (!NB0) {
+        for (int b = 0; b + 1 < net.NB; b++) block(b, std::false_type{});
         block(net.NB - 1, std::true_type{});
     } else {
         if (wave < 4) build_tiles(wave);  // (no block: read after the heads' LayerNorm barrier)
@@ -1120,7 +1125,7 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
             }
             __builtin_amdgcn_s_sleep(1);
         }
-        if (!seen && lane == 0 && net.err) atomicOr(net.err, FWD_ERR_SYNC);
+        if (!seen && lane == 0) SYNC_LOST = 1u;  // (reported at the very end: no global write on this path)
 #pragma unroll
         for (int rr = 0; rr < ROWS / 4; rr++) {
             const int r = wave * (ROWS / 4) + rr;
@@ -1178,6 +1183,9 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
             mlse[(long)part * mstride + row0 + tid] = make_float2(m, parts > 1 ? sm : logf(sm));
         }
     }
+    // the last statement: a branch around a global atomic earlier would merge the wait counters of
+    // its paths at the join and drain the policy ring's loads in flight (section 8-)
+    if (wave < 4 && lane == 0 && SYNC_LOST && net.err) atomicOr(net.err, FWD_ERR_SYNC);
 }
 
 }  // namespace

@@ -38,7 +38,7 @@ using namespace ykf;
 
 namespace {
 
-template <int H, int PL>
+template <int H, int PL, bool NB0 = false>
 __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* __restrict__ states,
                                                  const float* __restrict__ xin, const int32_t* __restrict__ rows,
                                                  const int32_t* __restrict__ count, int n,
@@ -51,7 +51,7 @@ __global__ __launch_bounds__(NTHR) void k_forward(NetDev net, const yk_state_t* 
     if (count) n = min(n, *count);
     const int part = (int)(blockIdx.x % (unsigned)parts);
     const int row0 = (int)(blockIdx.x / (unsigned)parts) * ROWS;
-    forward_tile<H, PL, WAVES>(net, states, xin, rows, nullptr, n, logits, vout, active, mlse, valid_only, want,
+    forward_tile<H, PL, WAVES, NB0>(net, states, xin, rows, nullptr, n, logits, vout, active, mlse, valid_only, want,
                                parts, mstride, row0, part);
 }
 
@@ -131,17 +131,20 @@ int launch_forward(const NetDev& net, const yk_state_t* states, const float* x, 
     if (parts < 1 || parts > 4 || (parts > 1 && (!mlse || mstride < n))) return YK_ERR_ARG;
     const dim3 grid((unsigned)((n + ROWS - 1) / ROWS * parts)), block(NTHR);
     const int vo = valid_only ? 1 : 0;
-#define YK_FWD(HH, PP) hipLaunchKernelGGL((k_forward<HH, PP>), grid, block, 0, stream, net, states, x, rows, count, n, \
-                                           logits, v, active, mlse, vo, (uint32_t)want, parts, mstride)
+#define YK_FWD1(HH, PP, Z) hipLaunchKernelGGL((k_forward<HH, PP, Z>), grid, block, 0, stream, net, states, x, rows, count, \
+                                               n, logits, v, active, mlse, vo, (uint32_t)want, parts, mstride)
+#define YK_FWD(HH, PP) \
+    if (net.NB == 0) YK_FWD1(HH, PP, true); else YK_FWD1(HH, PP, false)
     const bool f16 = net.planes == 1;
     switch (net.H) {
-        case 64: if (f16) YK_FWD(64, 1); else YK_FWD(64, 2); break;
-        case 128: if (f16) YK_FWD(128, 1); else YK_FWD(128, 2); break;
-        case 256: if (f16) YK_FWD(256, 1); else YK_FWD(256, 2); break;
-        case 512: if (f16) YK_FWD(512, 1); else YK_FWD(512, 2); break;
+        case 64: if (f16) { YK_FWD(64, 1); } else { YK_FWD(64, 2); } break;
+        case 128: if (f16) { YK_FWD(128, 1); } else { YK_FWD(128, 2); } break;
+        case 256: if (f16) { YK_FWD(256, 1); } else { YK_FWD(256, 2); } break;
+        case 512: if (f16) { YK_FWD(512, 1); } else { YK_FWD(512, 2); } break;
         default: return YK_ERR_ARG;
     }
 #undef YK_FWD
+#undef YK_FWD1
     YK_LAUNCHED();
     return YK_OK;
 }
