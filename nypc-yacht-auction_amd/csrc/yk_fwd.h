@@ -237,9 +237,6 @@ __device__ __forceinline__ void layernorm(float (&x)[VPL], const float* g, const
 // operation, as numpy does); the forward's LayerNorm row passes - VALU-bound and on every layer's
 // critical path - contract their multiply-adds into v_pk_fma_f32 (one rounding instead of two: no
 // less accurate than torch's own LayerNorm kernels, which fuse them too).  Scoped per function.
-#ifndef FWD_SYNC
-#define FWD_SYNC 1  // the value head's v_head.2 count: 1 release / acquire, 0 relaxed + volatile, 2 (A/B) without the timeout flag
-#endif
 #define YK_ROW_CONTRACT _Pragma("clang fp contract(fast)")
 typedef float f2v __attribute__((ext_vector_type(2)));
 typedef _Float16 h2v __attribute__((ext_vector_type(2)));
@@ -1070,11 +1067,12 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
     constexpr uint32_t NVW = NW < 8 ? NW : 8;
     if (NW == 8 || wave < 8) {
         store_acc<1>(X, LD, vwave, av, VS + VS_BV1 * H);
-#if FWD_SYNC == 1
-        if (lane == 0) __hip_atomic_fetch_add(&VHC, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-#else
+        // the count's increment follows the column stores in this wave's LDS order (a wave's DS
+        // operations execute in issue order), and the compiler fence keeps the stores ahead of it in
+        // the code; a release atomic instead costs an lgkmcnt(0) drain here and ~0.5 us per forward
+        // (profiles/r06g_forward_sync_ab.log)
+        __atomic_signal_fence(__ATOMIC_RELEASE);
         if (lane == 0) atomicAdd(&VHC, 1u);
-#endif
     }
     float sm[4], ss[4];  // running max and sum exp of the lane's rows 4 q + j
     bool allc[4];
@@ -1124,23 +1122,11 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
     if (wave < 4) {  // SiLU -> Linear(128, 1) -> tanh  YachtNNet.py:49-52,69, rows 4 wave .. 4 wave + 3
         // (bounded: a wave that never sees every count flags the net's error word instead of hanging
         // the grid; yk_net_errors / the engine's ERR_FWD_SYNC report it)
-#if FWD_SYNC == 2
         for (int it = 0; it < (1 << 20) && *(volatile uint32_t*)&VHC < NVW; it++) __builtin_amdgcn_s_sleep(1);
-#else
-        bool seen = false;
-        for (int it = 0; it < (1 << 20); it++) {
-#if FWD_SYNC == 1
-            if (__hip_atomic_load(&VHC, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= NVW) {
-#else
-            if (*(volatile uint32_t*)&VHC >= NVW) {
-#endif
-                seen = true;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-        if (!seen && lane == 0) SYNC_LOST = 1u;  // (reported at the very end: no global write on this path)
-#endif
+        // (reads of X stay after the count's: compiler fence; a timeout is flagged, reported at the
+        // kernel's very end, where a global write adds no wait to any load in flight)
+        __atomic_signal_fence(__ATOMIC_ACQUIRE);
+        if (lane == 0 && *(volatile uint32_t*)&VHC < NVW) SYNC_LOST = 1u;
 #pragma unroll
         for (int rr = 0; rr < ROWS / 4; rr++) {
             const int r = wave * (ROWS / 4) + rr;
