@@ -885,26 +885,54 @@ struct DwJob {
 // norm: returns the item's sum of (g / scale)^2 over what it writes, in every lane (yk_trainer_step's
 // fused gradient norm: the grads k_amp_sq would read, summed where they are made); else 0
 __device__ __forceinline__ double wave_dsum(double x) { return xlane_sum(x); }
-__device__ __forceinline__ double dw_item(const DwJob* __restrict__ jobs, const int4 it, int RS, int rsn, int lane,
-                                          bool norm = false, float inv = 1.f) {
-    const DwJob jb = jobs[it.x];
-    const int nt = it.y, kt0 = it.z, nk = it.w;
-    floatx4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
-    for (int rs = 0; rs < rsn; rs++) {
-        const float4 a = jb.A[((long)nt * RS + rs) * 64 + lane];
-        float4 x[4];
+#ifndef AMP_DW_DEPTH
+#define AMP_DW_DEPTH 4  // batch slices of a dW item in flight per wave
+#endif
+typedef float f4v_t __attribute__((ext_vector_type(4)));
+// a float4 through a global-address-space pointer: a global_load, not a flat one (which also counts in
+// lgkmcnt, so every wait on it drains the LDS / scalar queue too)
+__device__ __forceinline__ float4 gld4(const float4* p) {
+    return __builtin_bit_cast(float4, *(const __attribute__((address_space(1))) f4v_t*)p);
+}
+template <int NK>
+__device__ __forceinline__ double dw_item_t(const DwJob& jb, int nt, int kt0, int RS, int rsn, int lane, bool norm,
+                                            float inv) {
+    // the slices' fragments stream AMP_DW_DEPTH deep: slice rs + D is loaded while slice rs's MFMAs run
+    // (loads unconditional - past the last slice they re-read it - so no branch joins the load
+    // stream and each MFMA waits only for its own slice); the MFMAs run in slice order, as before
+    constexpr int D = AMP_DW_DEPTH;
+    const float4* A = jb.A + (long)nt * RS * 64 + lane;
+    const float4* X[NK];
 #pragma unroll
-        for (int t = 0; t < 4; t++)
-            x[t] = t < nk ? jb.X[((long)(kt0 + t) * RS + rs) * 64 + lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int t = 0; t < NK; t++) X[t] = jb.X + (long)(kt0 + t) * RS * 64 + lane;
+    floatx4 acc[NK];
 #pragma unroll
-        for (int t = 0; t < 4; t++)
-            if (t < nk) acc[t] = mfma(a, x[t], acc[t]);
+    for (int t = 0; t < NK; t++) acc[t] = zero4();
+    float4 a[D], x[D][NK];
+#pragma unroll
+    for (int p = 0; p < D; p++) {
+        const int s0 = min(p, rsn - 1);
+        a[p] = gld4(A + (long)s0 * 64);
+#pragma unroll
+        for (int t = 0; t < NK; t++) x[p][t] = gld4(X[t] + (long)s0 * 64);
+    }
+    for (int rs = 0; rs < rsn; rs += D) {
+#pragma unroll
+        for (int p = 0; p < D; p++) {
+            if (rs + p < rsn) {
+#pragma unroll
+                for (int t = 0; t < NK; t++) acc[t] = mfma(a[p], x[p][t], acc[t]);
+            }
+            const int nx = min(rs + p + D, rsn - 1);
+            a[p] = gld4(A + (long)nx * 64);
+#pragma unroll
+            for (int t = 0; t < NK; t++) x[p][t] = gld4(X[t] + (long)nx * 64);
+        }
     }
     const int q = lane >> 4, c = lane & 15;
     double ss = 0.0;
 #pragma unroll
-    for (int t = 0; t < 4; t++) {
-        if (t >= nk) break;
+    for (int t = 0; t < NK; t++) {
         const int k = 16 * (kt0 + t) + c;
 #pragma unroll
         for (int j = 0; j < 4; j++) {
@@ -912,12 +940,22 @@ __device__ __forceinline__ double dw_item(const DwJob* __restrict__ jobs, const 
             if (n < jb.N && k < jb.K) {
                 const float g = r16(acc[t][j]);  // fp16 grad_weight
                 jb.dst[(long)n * jb.K + k] = g;
-                const double x = (double)(g * inv);
-                ss += x * x;
+                const double x2 = (double)(g * inv);
+                ss += x2 * x2;
             }
         }
     }
     return norm ? wave_dsum(ss) : 0.0;
+}
+__device__ __forceinline__ double dw_item(const DwJob* __restrict__ jobs, const int4 it, int RS, int rsn, int lane,
+                                          bool norm = false, float inv = 1.f) {
+    const DwJob jb = jobs[it.x];
+    switch (it.w) {  // (uniform: the item's column tiles; amp_create's kg 2 or 4 divides every job's)
+        case 1: return dw_item_t<1>(jb, it.y, it.z, RS, rsn, lane, norm, inv);
+        case 2: return dw_item_t<2>(jb, it.y, it.z, RS, rsn, lane, norm, inv);
+        case 3: return dw_item_t<3>(jb, it.y, it.z, RS, rsn, lane, norm, inv);
+        default: return dw_item_t<4>(jb, it.y, it.z, RS, rsn, lane, norm, inv);
+    }
 }
 // a block's waves' norm partials -> sqp[slot] (wave order: fixed bits); every thread calls it
 template <int NW>
@@ -1249,13 +1287,15 @@ __device__ __forceinline__ void vecsum_item(const VsJob* __restrict__ jobs, cons
     const int c = it.y + (threadIdx.x & 15), g = threadIdx.x >> 4;
     const int rows = jb.per_example == 1 ? B : jb.per_example == 2 ? nhtiles : ntiles;
     float a0 = 0.f, a1 = 0.f;
+    typedef const __attribute__((address_space(1))) float gfloat;  // (global loads, not flat)
+    gfloat* src = (gfloat*)jb.src;
     if (c < jb.N) {
         int r = g;
         for (; r + 16 < rows; r += 32) {
-            a0 += jb.src[(long)r * jb.ld + c];
-            a1 += jb.src[(long)(r + 16) * jb.ld + c];
+            a0 += src[(long)r * jb.ld + c];
+            a1 += src[(long)(r + 16) * jb.ld + c];
         }
-        for (; r < rows; r += 16) a0 += jb.src[(long)r * jb.ld + c];
+        for (; r < rows; r += 16) a0 += src[(long)r * jb.ld + c];
     }
     part[g][threadIdx.x & 15] = a0 + a1;
     __syncthreads();
