@@ -1291,6 +1291,21 @@ __device__ __forceinline__ void vecsum_item(const VsJob* __restrict__ jobs, cons
     gfloat* src = (gfloat*)jb.src;
     if (c < jb.N) {
         int r = g;
+        // per-example jobs (B rows): eight loads in flight per batch, added in the same order (a0: rows
+        // g, g + 32, ..; a1: g + 16, g + 48, ..) as the one-pair loop below
+        for (; r + 16 + 96 < rows; r += 128) {
+            float v[8];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                v[2 * k] = src[(long)(r + 32 * k) * jb.ld + c];
+                v[2 * k + 1] = src[(long)(r + 32 * k + 16) * jb.ld + c];
+            }
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                a0 += v[2 * k];
+                a1 += v[2 * k + 1];
+            }
+        }
         for (; r + 16 < rows; r += 32) {
             a0 += src[(long)r * jb.ld + c];
             a1 += src[(long)(r + 16) * jb.ld + c];
@@ -1331,11 +1346,15 @@ __global__ __launch_bounds__(256) void k_amp_grads(const DwJob* __restrict__ job
     const int ndb = (nitems + 3) / 4;
     if ((int)blockIdx.x >= ndb) {
         const int v = (int)blockIdx.x - ndb;
+#ifndef AMP_DIAG_NO_VS
         if (v < nvitems) vecsum_item(vjobs, vitems[v], ntiles, nhtiles, B, part, sqp, nall + v, inv);
+#endif
     } else {
         const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
         double ss = 0.0;
+#ifndef AMP_DIAG_NO_DW
         if (w < nitems) ss = dw_item(jobs, items[w], RS, rsn, threadIdx.x & 63, sqp != nullptr, inv);
+#endif
         if (sqp) block_norm<4>(ss, sqp, blockIdx.x);
     }
 }
