@@ -885,11 +885,11 @@ struct DwJob {
 // norm: returns the item's sum of (g / scale)^2 over what it writes, in every lane (yk_trainer_step's
 // fused gradient norm: the grads k_amp_sq would read, summed where they are made); else 0
 __device__ __forceinline__ double wave_dsum(double x) { return xlane_sum(x); }
-#ifndef AMP_VS_PER_BLOCK
-#define AMP_VS_PER_BLOCK 1  // column-sum items per k_amp_grads block
-#endif
 #ifndef AMP_DW_DEPTH
-#define AMP_DW_DEPTH 4  // batch slices of a dW item in flight per wave
+// batch slices of a dW item in flight per wave: 2 (AMP step 112.9 -> 111.8 us at batch 512, = at 64;
+// 4 and 8 slower at 64 and 8 at 512 too: more registers, fewer resident blocks - and 4 column-sum
+// items per block slower, profiles/r06m_dw_depth_trainab.log)
+#define AMP_DW_DEPTH 2
 #endif
 typedef float f4v_t __attribute__((ext_vector_type(4)));
 // a float4 through a global-address-space pointer: a global_load, not a flat one (which also counts in
@@ -1350,13 +1350,7 @@ __global__ __launch_bounds__(256) void k_amp_grads(const DwJob* __restrict__ job
     if ((int)blockIdx.x >= ndb) {
         const int v = (int)blockIdx.x - ndb;
 #ifndef AMP_DIAG_NO_VS
-        // AMP_VS_PER_BLOCK items per block, in turn (fewer, longer blocks: the launch's blocks stay
-        // resident in one round beside the dW waves)
-        for (int q = 0; q < AMP_VS_PER_BLOCK; q++) {
-            const int vi = v * AMP_VS_PER_BLOCK + q;
-            if (vi < nvitems) vecsum_item(vjobs, vitems[vi], ntiles, nhtiles, B, part, sqp, nall + vi, inv);
-            if (AMP_VS_PER_BLOCK > 1) __syncthreads();  // (part is rewritten by the next item)
-        }
+        if (v < nvitems) vecsum_item(vjobs, vitems[v], ntiles, nhtiles, B, part, sqp, nall + v, inv);
 #endif
     } else {
         const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -1921,9 +1915,7 @@ int amp_backward(AmpTrain* a, const yk_state_t* states, const int32_t* targets, 
 #undef YK_AMP_FWD
         default: return YK_ERR_ARG;
     }
-    hipLaunchKernelGGL(k_amp_grads,
-                       dim3((unsigned)((a->n_dw_trunk + 3) / 4 + (a->n_vs_items + AMP_VS_PER_BLOCK - 1) / AMP_VS_PER_BLOCK)),
-                       dim3(256), 0, s,
+    hipLaunchKernelGGL(k_amp_grads, dim3((unsigned)((a->n_dw_trunk + 3) / 4 + a->n_vs_items)), dim3(256), 0, s,
                        a->dw_jobs, a->dw_items, a->n_dw_trunk, a->RS, rsn, a->vs_jobs, a->vs_items, a->n_vs_items, TT, T,
                        B, sqp, a->n_norm_dw, a->sc);
     YK_LAUNCHED();
