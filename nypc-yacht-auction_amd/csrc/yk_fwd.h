@@ -1122,11 +1122,15 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
     if (wave < 4) {  // SiLU -> Linear(128, 1) -> tanh  YachtNNet.py:49-52,69, rows 4 wave .. 4 wave + 3
         // (bounded: a wave that never sees every count flags the net's error word instead of hanging
         // the grid; yk_net_errors / the engine's ERR_FWD_SYNC report it)
-        for (int it = 0; it < (1 << 20) && *(volatile uint32_t*)&VHC < NVW; it++) __builtin_amdgcn_s_sleep(1);
+        // (a relaxed atomic load is a ds_read; a volatile access through the generic pointer was a
+        // flat load, whose wait also drained the wave's logit stores)
+        for (int it = 0; it < (1 << 20) && __hip_atomic_load(&VHC, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < NVW;
+             it++)
+            __builtin_amdgcn_s_sleep(1);
         // (reads of X stay after the count's: compiler fence; a timeout is flagged, reported at the
         // kernel's very end, where a global write adds no wait to any load in flight)
         __atomic_signal_fence(__ATOMIC_ACQUIRE);
-        if (lane == 0 && *(volatile uint32_t*)&VHC < NVW) SYNC_LOST = 1u;
+        if (lane == 0 && __hip_atomic_load(&VHC, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < NVW) SYNC_LOST = 1u;
 #pragma unroll
         for (int rr = 0; rr < ROWS / 4; rr++) {
             const int r = wave * (ROWS / 4) + rr;

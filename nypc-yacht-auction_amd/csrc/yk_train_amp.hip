@@ -897,6 +897,12 @@ typedef float f4v_t __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ float4 gld4(const float4* p) {
     return __builtin_bit_cast(float4, *(const __attribute__((address_space(1))) f4v_t*)p);
 }
+typedef __attribute__((address_space(1))) float gfloat_t;  // global float: global_load / global_store
+__device__ __forceinline__ gfloat_t* gptr(float* p) { return (gfloat_t*)p; }
+__device__ __forceinline__ void gst4(float* p, float4 v) {
+    *(__attribute__((address_space(1))) f4v_t*)p = __builtin_bit_cast(f4v_t, v);
+}
+__device__ __forceinline__ void gsth8(float4* p, half8 v) { *(__attribute__((address_space(1))) half8*)p = v; }
 template <int NK>
 __device__ __forceinline__ double dw_item_t(const DwJob& jb, int nt, int kt0, int RS, int rsn, int lane, bool norm,
                                             float inv) {
@@ -942,7 +948,7 @@ __device__ __forceinline__ double dw_item_t(const DwJob& jb, int nt, int kt0, in
             const int n = 16 * nt + 4 * q + j;
             if (n < jb.N && k < jb.K) {
                 const float g = r16(acc[t][j]);  // fp16 grad_weight
-                jb.dst[(long)n * jb.K + k] = g;
+                gptr(jb.dst)[(long)n * jb.K + k] = g;
                 const double x2 = (double)(g * inv);
                 ss += x2 * x2;
             }
@@ -1323,7 +1329,7 @@ __device__ __forceinline__ void vecsum_item(const VsJob* __restrict__ jobs, cons
 #pragma unroll
         for (int k = 0; k < 16; k++) s += part[k][threadIdx.x];
         const float v = jb.round16 ? r16(s) : s;
-        jb.dst[c] = v;
+        gptr(jb.dst)[c] = v;
         const double x = jb.in_grad ? (double)(v * inv) : 0.0;
         ss = x * x;
     }
@@ -1513,12 +1519,12 @@ __global__ __launch_bounds__(256) void k_amp_update(const UpdJob* __restrict__ j
         const int t = threadIdx.x;
         if (!jb.dstN) {
             for (int i = 0; i < 4; i++)
-                if (4 * t + i < it.k0) jb.Gm[(long)it.n0 + 4 * t + i] = (jb.Gm[(long)it.n0 + 4 * t + i] * inv) * cf;
+                if (4 * t + i < it.k0) gptr(jb.Gm)[(long)it.n0 + 4 * t + i] = (gptr(jb.Gm)[(long)it.n0 + 4 * t + i] * inv) * cf;
         } else {
             const int n = it.n0 + (t >> 3);
             for (int i = 0; i < 4; i++) {
                 const int k = it.k0 + (t & 7) * 4 + i;
-                if (n < jb.N && k < jb.K) jb.Gm[(long)n * jb.K + k] = (jb.Gm[(long)n * jb.K + k] * inv) * cf;
+                if (n < jb.N && k < jb.K) gptr(jb.Gm)[(long)n * jb.K + k] = (gptr(jb.Gm)[(long)n * jb.K + k] * inv) * cf;
             }
         }
         return;
@@ -1539,7 +1545,12 @@ __global__ __launch_bounds__(256) void k_amp_update(const UpdJob* __restrict__ j
             const int e = 4 * t + i;
             if (e < it.k0) {
                 const long o = (long)it.n0 + e;
-                adamw_elem(jb.W[o], jb.Gm[o], jb.Mm[o], jb.Vm[o], inv, coef, decay, b1, b2, eps, step_size, bc2_sqrt);
+                float p = gptr(jb.W)[o], g = gptr(jb.Gm)[o], m = gptr(jb.Mm)[o], v = gptr(jb.Vm)[o];
+                adamw_elem(p, g, m, v, inv, coef, decay, b1, b2, eps, step_size, bc2_sqrt);
+                gptr(jb.W)[o] = p;
+                gptr(jb.Gm)[o] = g;
+                gptr(jb.Mm)[o] = m;
+                gptr(jb.Vm)[o] = v;
             }
         }
         return;
@@ -1552,16 +1563,16 @@ __global__ __launch_bounds__(256) void k_amp_update(const UpdJob* __restrict__ j
                        reinterpret_cast<uintptr_t>(jb.Mm) | reinterpret_cast<uintptr_t>(jb.Vm)) & 15) == 0;
     if (vec) {  // 16-byte aligned rows: four elements per load
         const long o = o4;
-        float4 p = *reinterpret_cast<const float4*>(jb.W + o), g = *reinterpret_cast<const float4*>(jb.Gm + o);
-        float4 m = *reinterpret_cast<const float4*>(jb.Mm + o), v = *reinterpret_cast<const float4*>(jb.Vm + o);
+        float4 p = gld4(reinterpret_cast<const float4*>(jb.W + o)), g = gld4(reinterpret_cast<const float4*>(jb.Gm + o));
+        float4 m = gld4(reinterpret_cast<const float4*>(jb.Mm + o)), v = gld4(reinterpret_cast<const float4*>(jb.Vm + o));
         adamw_elem(p.x, g.x, m.x, v.x, inv, coef, decay, b1, b2, eps, step_size, bc2_sqrt);
         adamw_elem(p.y, g.y, m.y, v.y, inv, coef, decay, b1, b2, eps, step_size, bc2_sqrt);
         adamw_elem(p.z, g.z, m.z, v.z, inv, coef, decay, b1, b2, eps, step_size, bc2_sqrt);
         adamw_elem(p.w, g.w, m.w, v.w, inv, coef, decay, b1, b2, eps, step_size, bc2_sqrt);
-        *reinterpret_cast<float4*>(jb.W + o) = p;
-        *reinterpret_cast<float4*>(jb.Gm + o) = g;
-        *reinterpret_cast<float4*>(jb.Mm + o) = m;
-        *reinterpret_cast<float4*>(jb.Vm + o) = v;
+        gst4(jb.W + o, p);
+        gst4(jb.Gm + o, g);
+        gst4(jb.Mm + o, m);
+        gst4(jb.Vm + o, v);
         Tl[r][c] = f16_of_stored(p.x);
         Tl[r][c + 1] = f16_of_stored(p.y);
         Tl[r][c + 2] = f16_of_stored(p.z);
@@ -1573,12 +1584,12 @@ __global__ __launch_bounds__(256) void k_amp_update(const UpdJob* __restrict__ j
             float pv = 0.f;
             if (n < jb.N && k < jb.K) {
                 const long o = (long)n * jb.K + k;
-                float p = jb.W[o], g = jb.Gm[o], m = jb.Mm[o], v = jb.Vm[o];
+                float p = gptr(jb.W)[o], g = gptr(jb.Gm)[o], m = gptr(jb.Mm)[o], v = gptr(jb.Vm)[o];
                 adamw_elem(p, g, m, v, inv, coef, decay, b1, b2, eps, step_size, bc2_sqrt);
-                jb.W[o] = p;
-                jb.Gm[o] = g;
-                jb.Mm[o] = m;
-                jb.Vm[o] = v;
+                gptr(jb.W)[o] = p;
+                gptr(jb.Gm)[o] = g;
+                gptr(jb.Mm)[o] = m;
+                gptr(jb.Vm)[o] = v;
                 pv = p;
             }
             Tl[r][c + i] = f16_of_stored(pv);
@@ -1591,12 +1602,12 @@ __global__ __launch_bounds__(256) void k_amp_update(const UpdJob* __restrict__ j
         const int rr = 16 * f + (l & 15), kk = 8 * (l >> 4);
 #pragma unroll
         for (int j = 0; j < 8; j++) h[j] = Tl[rr][kk + j];
-        *reinterpret_cast<half8*>(jb.dstN + ((long)(it.n0 / 16 + f) * (jb.KpN / 32) + it.k0 / 32) * 64 + l) = h;
+        gsth8(jb.dstN + ((long)(it.n0 / 16 + f) * (jb.KpN / 32) + it.k0 / 32) * 64 + l, h);
     } else if (jb.dstT) {  // W^T: fragment (k0 / 16 + f, n0 / 32), lane l = W[32 ks + 8 (l >> 4) + j][16 nt + (l & 15)]
         const int kk = 16 * f + (l & 15), rr = 8 * (l >> 4);
 #pragma unroll
         for (int j = 0; j < 8; j++) h[j] = Tl[rr + j][kk];
-        *reinterpret_cast<half8*>(jb.dstT + ((long)(it.k0 / 16 + f) * (jb.KpT / 32) + it.n0 / 32) * 64 + l) = h;
+        gsth8(jb.dstT + ((long)(it.k0 / 16 + f) * (jb.KpT / 32) + it.n0 / 32) * 64 + l, h);
     }
 }
 
