@@ -69,6 +69,9 @@ constexpr int BQ = YK_BQ;       // head-backward action parts per row tile (12: 
                                 // profiles/r05ze_head_parts_trainab.log)
 constexpr int VH = 128;         // v_head hidden width
 constexpr int SQ_BLOCKS = 1024;
+#ifndef YK_DW_KG
+#define YK_DW_KG 2  // column tiles per trunk dW item
+#endif
 
 struct Scaler {  // GradScaler('cuda') state + the AdamW step count (device)
     float scale;
@@ -966,6 +969,84 @@ __device__ __forceinline__ double dw_item(const DwJob* __restrict__ jobs, const 
         default: return dw_item_t<4>(jb, it.y, it.z, RS, rsn, lane, norm, inv);
     }
 }
+#ifndef AMP_DW_SPLIT
+#define AMP_DW_SPLIT 2  // waves per trunk dW item in k_amp_grads (the batch's slices split between them)
+#endif
+#ifndef AMP_DW_CH
+#define AMP_DW_CH 4  // slices a part loads at once
+#endif
+constexpr int DW_IPB = 4 / AMP_DW_SPLIT;  // trunk dW items per 4-wave k_amp_grads block
+// one trunk dW item over S waves of the block (S = AMP_DW_SPLIT): wave part p sums slices
+// [p rsn / S, (p + 1) rsn / S) with every slice's fragments loaded at once (up to 8), and part 0 adds
+// the others' accumulators in part order (through LDS) and stores.  Every wave of the block calls it
+// (has: whether its item exists), for the barrier.
+template <int NK>
+__device__ __forceinline__ double dw_item_split(const DwJob& jb, bool has, int nt, int kt0, int RS, int rsn, int lane,
+                                                int part, bool norm, float inv, float* red, int wave) {
+    constexpr int S = AMP_DW_SPLIT, CH = AMP_DW_CH;
+    floatx4 acc[NK];
+#pragma unroll
+    for (int t = 0; t < NK; t++) acc[t] = zero4();
+    const int lo = part * rsn / S, hi = (part + 1) * rsn / S;
+    if (has && hi > lo) {
+        const float4* A = jb.A + (long)nt * RS * 64 + lane;
+        const float4* X[NK];
+#pragma unroll
+        for (int t = 0; t < NK; t++) X[t] = jb.X + (long)(kt0 + t) * RS * 64 + lane;
+        for (int r0 = lo; r0 < hi; r0 += CH) {
+            float4 a[CH], x[CH][NK];
+#pragma unroll
+            for (int p = 0; p < CH; p++) {
+                const int s0 = min(r0 + p, hi - 1);
+                a[p] = gld4(A + (long)s0 * 64);
+#pragma unroll
+                for (int t = 0; t < NK; t++) x[p][t] = gld4(X[t] + (long)s0 * 64);
+            }
+#pragma unroll
+            for (int p = 0; p < CH; p++)
+                if (r0 + p < hi) {
+#pragma unroll
+                    for (int t = 0; t < NK; t++) acc[t] = mfma(a[p], x[p][t], acc[t]);
+                }
+        }
+    }
+    if (S > 1) {
+        if (part > 0) {
+#pragma unroll
+            for (int t = 0; t < NK; t++)
+#pragma unroll
+                for (int j = 0; j < 4; j++) red[((wave * 4 + t) * 4 + j) * 64 + lane] = acc[t][j];
+        }
+        __syncthreads();
+        if (part == 0) {
+#pragma unroll
+            for (int q = 1; q < S; q++)
+#pragma unroll
+                for (int t = 0; t < NK; t++)
+#pragma unroll
+                    for (int j = 0; j < 4; j++) acc[t][j] += red[(((wave + q) * 4 + t) * 4 + j) * 64 + lane];
+        }
+    }
+    double ss = 0.0;
+    if (has && part == 0) {
+        const int q = lane >> 4, c = lane & 15;
+#pragma unroll
+        for (int t = 0; t < NK; t++) {
+            const int k = 16 * (kt0 + t) + c;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int n = 16 * nt + 4 * q + j;
+                if (n < jb.N && k < jb.K) {
+                    const float g = r16(acc[t][j]);  // fp16 grad_weight
+                    gptr(jb.dst)[(long)n * jb.K + k] = g;
+                    const double x2 = (double)(g * inv);
+                    ss += x2 * x2;
+                }
+            }
+        }
+    }
+    return norm ? wave_dsum(ss) : 0.0;
+}
 // a block's waves' norm partials -> sqp[slot] (wave order: fixed bits); every thread calls it
 template <int NW>
 __device__ __forceinline__ void block_norm(double ss, double* __restrict__ sqp, int slot) {
@@ -1351,18 +1432,26 @@ __global__ __launch_bounds__(256) void k_amp_grads(const DwJob* __restrict__ job
                                                    int nhtiles, int B, double* __restrict__ sqp, int nall,
                                                    const Scaler* __restrict__ sc) {
     __shared__ float part[16][17];
+    __shared__ float red[AMP_DW_SPLIT > 1 ? 4 * 4 * 4 * 64 : 1];  // the split dW items' partial accumulators
     const float inv = sqp ? 1.0f / sc->scale : 1.f;
-    const int ndb = (nitems + 3) / 4;
+    const int ndb = (nitems + DW_IPB - 1) / DW_IPB;
     if ((int)blockIdx.x >= ndb) {
         const int v = (int)blockIdx.x - ndb;
 #ifndef AMP_DIAG_NO_VS
         if (v < nvitems) vecsum_item(vjobs, vitems[v], ntiles, nhtiles, B, part, sqp, nall + v, inv);
 #endif
     } else {
-        const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
+        const int wave = threadIdx.x >> 6;
+        const int w = blockIdx.x * DW_IPB + wave / AMP_DW_SPLIT;
         double ss = 0.0;
 #ifndef AMP_DIAG_NO_DW
-        if (w < nitems) ss = dw_item(jobs, items[w], RS, rsn, threadIdx.x & 63, sqp != nullptr, inv);
+        const bool has = w < nitems;
+        const int4 it = items[has ? w : 0];
+        const DwJob jb = jobs[it.x];
+        // (every trunk item has YK_DW_KG column tiles: amp_create builds them so, and every trunk
+        // matrix's column-tile count, H / 16 or 4 for the input layer, is a multiple of it)
+        ss = dw_item_split<YK_DW_KG>(jb, has, it.y, it.z, RS, rsn, threadIdx.x & 63, wave % AMP_DW_SPLIT, sqp != nullptr,
+                                     inv, red, wave);
 #endif
         if (sqp) block_norm<4>(ss, sqp, blockIdx.x);
     }
@@ -1614,9 +1703,6 @@ __global__ __launch_bounds__(256) void k_amp_update(const UpdJob* __restrict__ j
 }  // namespace
 
 // ------------------------------------------------------------------ host
-#ifndef YK_DW_KG
-#define YK_DW_KG 2
-#endif
 namespace yk {
 
 struct AmpTrain {
@@ -1785,9 +1871,14 @@ int amp_create(AmpTrain** out, int H, int NB, int Bmax, float* P, float* G, cons
             for (int nt = 0; nt < ntn; nt++) items.push_back(make_int4((int)j, nt, k0, std::min(kg, ntk - k0)));
     }
     a->n_dw_items = (int)items.size();
+    for (const int4& it : items)  // (k_amp_grads runs the trunk's items as YK_DW_KG-tile items)
+        if (it.x < 1 + 2 * NB && it.w != YK_DW_KG) {
+            amp_destroy(a);
+            return YK_ERR_ARG;
+        }
     a->n_dw_trunk = 0;  // the items of the input layer's and the blocks' matrices come first
     while (a->n_dw_trunk < a->n_dw_items && items[a->n_dw_trunk].x < 1 + 2 * NB) a->n_dw_trunk++;
-    a->n_norm_dw = (a->n_dw_trunk + 3) / 4 + (a->n_dw_items - a->n_dw_trunk + TW - 1) / TW;
+    a->n_norm_dw = (a->n_dw_trunk + DW_IPB - 1) / DW_IPB + (a->n_dw_items - a->n_dw_trunk + TW - 1) / TW;
     // column-sum jobs: bias / LayerNorm gradients and the two loss sums
     std::vector<VsJob> vj;
     const int ldc = d.NVEC * H;
@@ -1916,7 +2007,7 @@ int amp_backward(AmpTrain* a, const yk_state_t* states, const int32_t* targets, 
         YK_LAUNCHED();                                                                                              \
         hipLaunchKernelGGL(k_amp_bwd<HH>, dim3(TT + (a->n_dw_items - a->n_dw_trunk + TW - 1) / TW), dim3(TTHR), 0, s, \
                            d, B, dropout, seed, step, row_base, a->dw_jobs, a->dw_items + a->n_dw_trunk,          \
-                           a->n_dw_items - a->n_dw_trunk, rsn, sqp, (a->n_dw_trunk + 3) / 4);                      \
+                           a->n_dw_items - a->n_dw_trunk, rsn, sqp, (a->n_dw_trunk + DW_IPB - 1) / DW_IPB);        \
         YK_LAUNCHED();                                                                                              \
         break;
         YK_AMP_FWD(64)
@@ -1926,7 +2017,7 @@ int amp_backward(AmpTrain* a, const yk_state_t* states, const int32_t* targets, 
 #undef YK_AMP_FWD
         default: return YK_ERR_ARG;
     }
-    hipLaunchKernelGGL(k_amp_grads, dim3((unsigned)((a->n_dw_trunk + 3) / 4 + a->n_vs_items)), dim3(256), 0, s,
+    hipLaunchKernelGGL(k_amp_grads, dim3((unsigned)((a->n_dw_trunk + DW_IPB - 1) / DW_IPB + a->n_vs_items)), dim3(256), 0, s,
                        a->dw_jobs, a->dw_items, a->n_dw_trunk, a->RS, rsn, a->vs_jobs, a->vs_items, a->n_vs_items, TT, T,
                        B, sqp, a->n_norm_dw, a->sc);
     YK_LAUNCHED();
