@@ -130,6 +130,18 @@ __device__ __forceinline__ floatx4 mfma(float4 a, float4 b, floatx4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, a), __builtin_bit_cast(half8, b), c, 0, 0, 0);
 }
 __device__ __forceinline__ floatx4 zero4() { return floatx4{0.f, 0.f, 0.f, 0.f}; }
+// Accesses through pointers read from job tables compile to flat_load / flat_store, which count in
+// lgkmcnt too (so every LDS / scalar wait also drains them); these go through the global address space
+typedef float f4v_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 gld4(const float4* p) {
+    return __builtin_bit_cast(float4, *(const __attribute__((address_space(1))) f4v_t*)p);
+}
+typedef __attribute__((address_space(1))) float gfloat_t;
+__device__ __forceinline__ gfloat_t* gptr(float* p) { return (gfloat_t*)p; }
+__device__ __forceinline__ void gst4(float* p, float4 v) {
+    *(__attribute__((address_space(1))) f4v_t*)p = __builtin_bit_cast(f4v_t, v);
+}
+__device__ __forceinline__ void gsth8(float4* p, half8 v) { *(__attribute__((address_space(1))) half8*)p = v; }
 __device__ __forceinline__ float wsum(float v) { return xlane_sum(v); }
 // two full-wave sums at once on the DPP path (quad / row shuffles, row broadcasts, lane 63 read):
 // the row passes' reductions, whose latency is on every layer's critical path
@@ -888,102 +900,22 @@ struct DwJob {
 // norm: returns the item's sum of (g / scale)^2 over what it writes, in every lane (yk_trainer_step's
 // fused gradient norm: the grads k_amp_sq would read, summed where they are made); else 0
 __device__ __forceinline__ double wave_dsum(double x) { return xlane_sum(x); }
-#ifndef AMP_DW_DEPTH
-// batch slices of a dW item in flight per wave: 2 (AMP step 112.9 -> 111.8 us at batch 512, = at 64;
-// 4 and 8 slower at 64 and 8 at 512 too: more registers, fewer resident blocks - and 4 column-sum
-// items per block slower, profiles/r06m_dw_depth_trainab.log)
-#define AMP_DW_DEPTH 2
-#endif
-typedef float f4v_t __attribute__((ext_vector_type(4)));
-// a float4 through a global-address-space pointer: a global_load, not a flat one (which also counts in
-// lgkmcnt, so every wait on it drains the LDS / scalar queue too)
-__device__ __forceinline__ float4 gld4(const float4* p) {
-    return __builtin_bit_cast(float4, *(const __attribute__((address_space(1))) f4v_t*)p);
-}
-typedef __attribute__((address_space(1))) float gfloat_t;  // global float: global_load / global_store
-__device__ __forceinline__ gfloat_t* gptr(float* p) { return (gfloat_t*)p; }
-__device__ __forceinline__ void gst4(float* p, float4 v) {
-    *(__attribute__((address_space(1))) f4v_t*)p = __builtin_bit_cast(f4v_t, v);
-}
-__device__ __forceinline__ void gsth8(float4* p, half8 v) { *(__attribute__((address_space(1))) half8*)p = v; }
-template <int NK>
-__device__ __forceinline__ double dw_item_t(const DwJob& jb, int nt, int kt0, int RS, int rsn, int lane, bool norm,
-                                            float inv) {
-    // the slices' fragments stream AMP_DW_DEPTH deep: slice rs + D is loaded while slice rs's MFMAs run
-    // (loads unconditional - past the last slice they re-read it - so no branch joins the load
-    // stream and each MFMA waits only for its own slice); the MFMAs run in slice order, as before
-    constexpr int D = AMP_DW_DEPTH;
-    const float4* A = jb.A + (long)nt * RS * 64 + lane;
-    const float4* X[NK];
-#pragma unroll
-    for (int t = 0; t < NK; t++) X[t] = jb.X + (long)(kt0 + t) * RS * 64 + lane;
-    floatx4 acc[NK];
-#pragma unroll
-    for (int t = 0; t < NK; t++) acc[t] = zero4();
-    float4 a[D], x[D][NK];
-#pragma unroll
-    for (int p = 0; p < D; p++) {
-        const int s0 = min(p, rsn - 1);
-        a[p] = gld4(A + (long)s0 * 64);
-#pragma unroll
-        for (int t = 0; t < NK; t++) x[p][t] = gld4(X[t] + (long)s0 * 64);
-    }
-    for (int rs = 0; rs < rsn; rs += D) {
-#pragma unroll
-        for (int p = 0; p < D; p++) {
-            if (rs + p < rsn) {
-#pragma unroll
-                for (int t = 0; t < NK; t++) acc[t] = mfma(a[p], x[p][t], acc[t]);
-            }
-            const int nx = min(rs + p + D, rsn - 1);
-            a[p] = gld4(A + (long)nx * 64);
-#pragma unroll
-            for (int t = 0; t < NK; t++) x[p][t] = gld4(X[t] + (long)nx * 64);
-        }
-    }
-    const int q = lane >> 4, c = lane & 15;
-    double ss = 0.0;
-#pragma unroll
-    for (int t = 0; t < NK; t++) {
-        const int k = 16 * (kt0 + t) + c;
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const int n = 16 * nt + 4 * q + j;
-            if (n < jb.N && k < jb.K) {
-                const float g = r16(acc[t][j]);  // fp16 grad_weight
-                gptr(jb.dst)[(long)n * jb.K + k] = g;
-                const double x2 = (double)(g * inv);
-                ss += x2 * x2;
-            }
-        }
-    }
-    return norm ? wave_dsum(ss) : 0.0;
-}
-__device__ __forceinline__ double dw_item(const DwJob* __restrict__ jobs, const int4 it, int RS, int rsn, int lane,
-                                          bool norm = false, float inv = 1.f) {
-    const DwJob jb = jobs[it.x];
-    switch (it.w) {  // (uniform: the item's column tiles; amp_create's kg 2 or 4 divides every job's)
-        case 1: return dw_item_t<1>(jb, it.y, it.z, RS, rsn, lane, norm, inv);
-        case 2: return dw_item_t<2>(jb, it.y, it.z, RS, rsn, lane, norm, inv);
-        case 3: return dw_item_t<3>(jb, it.y, it.z, RS, rsn, lane, norm, inv);
-        default: return dw_item_t<4>(jb, it.y, it.z, RS, rsn, lane, norm, inv);
-    }
-}
 #ifndef AMP_DW_SPLIT
-#define AMP_DW_SPLIT 2  // waves per trunk dW item in k_amp_grads (the batch's slices split between them)
+#define AMP_DW_SPLIT 1  // waves per trunk dW item in k_amp_grads (2, 4: the batch's slices split; slower, r06p)
 #endif
 #ifndef AMP_DW_CH
 #define AMP_DW_CH 4  // slices a part loads at once
 #endif
 constexpr int DW_IPB = 4 / AMP_DW_SPLIT;  // trunk dW items per 4-wave k_amp_grads block
-// one trunk dW item over S waves of the block (S = AMP_DW_SPLIT): wave part p sums slices
-// [p rsn / S, (p + 1) rsn / S) with every slice's fragments loaded at once (up to 8), and part 0 adds
+// one dW item over S waves of the block (S = AMP_DW_SPLIT in k_amp_grads): wave part p sums slices
+// [p rsn / S, (p + 1) rsn / S), AMP_DW_CH slices' fragments loaded at once (global loads, unconditional:
+// past the part's last slice they re-read it), the MFMAs in slice order; part 0 adds
 // the others' accumulators in part order (through LDS) and stores.  Every wave of the block calls it
 // (has: whether its item exists), for the barrier.
-template <int NK>
+template <int NK, int S = AMP_DW_SPLIT>
 __device__ __forceinline__ double dw_item_split(const DwJob& jb, bool has, int nt, int kt0, int RS, int rsn, int lane,
                                                 int part, bool norm, float inv, float* red, int wave) {
-    constexpr int S = AMP_DW_SPLIT, CH = AMP_DW_CH;
+    constexpr int CH = AMP_DW_CH;
     floatx4 acc[NK];
 #pragma unroll
     for (int t = 0; t < NK; t++) acc[t] = zero4();
@@ -1046,6 +978,17 @@ __device__ __forceinline__ double dw_item_split(const DwJob& jb, bool has, int n
         }
     }
     return norm ? wave_dsum(ss) : 0.0;
+}
+// one weight-gradient item for one wave (the heads' items inside k_amp_bwd): the chunked form, unsplit
+__device__ __forceinline__ double dw_item(const DwJob* __restrict__ jobs, const int4 it, int RS, int rsn, int lane,
+                                          bool norm = false, float inv = 1.f) {
+    const DwJob jb = jobs[it.x];
+    switch (it.w) {  // (uniform: the item's column tiles; amp_create's kg 2 or 4 divides every job's)
+        case 1: return dw_item_split<1, 1>(jb, true, it.y, it.z, RS, rsn, lane, 0, norm, inv, nullptr, 0);
+        case 2: return dw_item_split<2, 1>(jb, true, it.y, it.z, RS, rsn, lane, 0, norm, inv, nullptr, 0);
+        case 3: return dw_item_split<3, 1>(jb, true, it.y, it.z, RS, rsn, lane, 0, norm, inv, nullptr, 0);
+        default: return dw_item_split<4, 1>(jb, true, it.y, it.z, RS, rsn, lane, 0, norm, inv, nullptr, 0);
+    }
 }
 // a block's waves' norm partials -> sqp[slot] (wave order: fixed bits); every thread calls it
 template <int NW>
