@@ -904,7 +904,9 @@ __device__ __forceinline__ double wave_dsum(double x) { return xlane_sum(x); }
 #define AMP_DW_SPLIT 1  // waves per trunk dW item in k_amp_grads (2, 4: the batch's slices split; slower, r06p)
 #endif
 #ifndef AMP_DW_CH
-#define AMP_DW_CH 4  // slices a part loads at once
+// slices whose fragments a dW item loads at once: 8 (AMP step at batch 512 111.9 -> 109.5 us; 4: 110.2,
+// 2: 112.2; at batch 64 8 costs 1 us over 4 - the reference trains at 512; profiles/r06q_dw_chunk_trainab.log)
+#define AMP_DW_CH 8
 #endif
 constexpr int DW_IPB = 4 / AMP_DW_SPLIT;  // trunk dW items per 4-wave k_amp_grads block
 // one dW item over S waves of the block (S = AMP_DW_SPLIT in k_amp_grads): wave part p sums slices
