@@ -903,6 +903,9 @@ __device__ __forceinline__ double wave_dsum(double x) { return xlane_sum(x); }
 #ifndef AMP_DW_SPLIT
 #define AMP_DW_SPLIT 1  // waves per trunk dW item in k_amp_grads (2, 4: the batch's slices split; slower, r06p)
 #endif
+#ifndef AMP_VS_PAIRS
+#define AMP_VS_PAIRS 4  // row pairs per batch of a column sum's loads
+#endif
 #ifndef AMP_DW_CH
 // slices whose fragments a dW item loads at once: 8 (AMP step at batch 512 111.9 -> 109.5 us; 4: 110.2,
 // 2: 112.2; at batch 64 8 costs 1 us over 4 - the reference trains at 512; profiles/r06q_dw_chunk_trainab.log)
@@ -1326,17 +1329,18 @@ __device__ __forceinline__ void vecsum_item(const VsJob* __restrict__ jobs, cons
     gfloat* src = (gfloat*)jb.src;
     if (c < jb.N) {
         int r = g;
-        // per-example jobs (B rows): eight loads in flight per batch, added in the same order (a0: rows
+        // per-example jobs (B rows): 2 VSP loads in flight per batch, added in the same order (a0: rows
         // g, g + 32, ..; a1: g + 16, g + 48, ..) as the one-pair loop below
-        for (; r + 16 + 96 < rows; r += 128) {
-            float v[8];
+        constexpr int VSP = AMP_VS_PAIRS;
+        for (; r + 16 + 32 * (VSP - 1) < rows; r += 32 * VSP) {
+            float v[2 * VSP];
 #pragma unroll
-            for (int k = 0; k < 4; k++) {
+            for (int k = 0; k < VSP; k++) {
                 v[2 * k] = src[(long)(r + 32 * k) * jb.ld + c];
                 v[2 * k + 1] = src[(long)(r + 32 * k + 16) * jb.ld + c];
             }
 #pragma unroll
-            for (int k = 0; k < 4; k++) {
+            for (int k = 0; k < VSP; k++) {
                 a0 += v[2 * k];
                 a1 += v[2 * k + 1];
             }
