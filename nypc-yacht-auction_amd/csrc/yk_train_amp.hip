@@ -904,7 +904,7 @@ __device__ __forceinline__ double wave_dsum(double x) { return xlane_sum(x); }
 #define AMP_DW_SPLIT 1  // waves per trunk dW item in k_amp_grads (2, 4: the batch's slices split; slower, r06p)
 #endif
 #ifndef AMP_VS_PAIRS
-#define AMP_VS_PAIRS 4  // row pairs per batch of a column sum's loads
+#define AMP_VS_PAIRS 4  // row pairs per batch of a column sum's loads (8, 16: within 0.3 us, r06r)
 #endif
 #ifndef AMP_DW_CH
 // slices whose fragments a dW item loads at once: 8 (AMP step at batch 512 111.9 -> 109.5 us; 4: 110.2,
@@ -1407,9 +1407,6 @@ __global__ __launch_bounds__(256) void k_amp_grads(const DwJob* __restrict__ job
 }
 
 // ------------------------------------------------------------------ optimiser
-#ifndef AMP_UPD_HOIST
-#define AMP_UPD_HOIST 0  // k_amp_update: the work item / job / GradScaler loads ahead of the norm's sum
-#endif
 // GradScaler.unscale_: the norm of the unscaled gradients (an inf / nan anywhere makes it so)
 __global__ void k_amp_sq(const float* __restrict__ g, long n, const Scaler* sc, double* __restrict__ part) {
     __shared__ double red[4];
@@ -1529,17 +1526,8 @@ __global__ __launch_bounds__(256) void k_amp_update(const UpdJob* __restrict__ j
         }
         return;
     }
-#if AMP_UPD_HOIST
-    // the block's work item, its job and the GradScaler state first: their dependent loads then
-    // overlap the norm's sum instead of following it
-    const UpdItem it = items[blockIdx.x];
-    const UpdJob jb = jobs[it.job];
-    const Scaler s0 = *sc;
-    const double total = sq_total(part, npart);
-#else
     const double total = sq_total(part, npart);  // (k_amp_sq's SQ_BLOCKS partials or the fused norm's slots)
     const Scaler s0 = *sc;
-#endif
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         *sq_out = total;
         Scaler n = s0;  // GradScaler('cuda').update: growth 2, backoff 0.5
@@ -1564,10 +1552,8 @@ __global__ __launch_bounds__(256) void k_amp_update(const UpdJob* __restrict__ j
         // -> +-0, infinite ones -> nan), nan for a nan norm
         float cf = max_norm / ((float)sqrt(total) + 1e-6f);
         cf = cf > 1.0f ? 1.0f : cf;
-#if !AMP_UPD_HOIST
         const UpdItem it = items[blockIdx.x];
         const UpdJob jb = jobs[it.job];
-#endif
         const int t = threadIdx.x;
         if (!jb.dstN) {
             for (int i = 0; i < 4; i++)
@@ -1588,10 +1574,8 @@ __global__ __launch_bounds__(256) void k_amp_update(const UpdJob* __restrict__ j
     float coef = max_norm / (norm + 1e-6f);
     coef = coef > 1.0f ? 1.0f : coef;
     const float decay = 1.0f - lr * wd;
-#if !AMP_UPD_HOIST
     const UpdItem it = items[blockIdx.x];
     const UpdJob jb = jobs[it.job];
-#endif
     const int t = threadIdx.x;
     if (!jb.dstN) {  // a vector slice: 4 consecutive elements per thread
 #pragma unroll
