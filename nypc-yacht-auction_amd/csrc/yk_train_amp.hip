@@ -1407,9 +1407,7 @@ __global__ __launch_bounds__(256) void k_amp_grads(const DwJob* __restrict__ job
 }
 
 // ------------------------------------------------------------------ optimiser
-#ifndef AMP_UPD_IPB
-#define AMP_UPD_IPB 1  // > 1: k_amp_update_p, that many work items per block, pipelined
-#endif
+
 // GradScaler.unscale_: the norm of the unscaled gradients (an inf / nan anywhere makes it so)
 __global__ void k_amp_sq(const float* __restrict__ g, long n, const Scaler* sc, double* __restrict__ part) {
     __shared__ double red[4];
@@ -1653,174 +1651,6 @@ __global__ __launch_bounds__(256) void k_amp_update(const UpdJob* __restrict__ j
 }
 
 
-#if AMP_UPD_IPB > 1
-// k_amp_update with AMP_UPD_IPB work items per block, software-pipelined: the norm is summed once per
-// block, and item q + 1's parameter / gradient / moment loads are issued before item q's fp16 repack
-// (they do not depend on it), so a block's items share one dependent chain.  Same AdamW arithmetic
-// per element as k_amp_update (bit-identical results).
-struct UpdLane {
-    long o;        // the thread's first element (flat buffer offset)
-    uint32_t msk;  // which of its 4 consecutive elements exist
-    bool vec;      // one 16-byte access per array
-};
-__device__ __forceinline__ UpdLane upd_lane(const UpdItem& it, const UpdJob& jb, int t) {
-    UpdLane L;
-    if (!jb.dstN) {  // a vector slice: 4 consecutive elements per thread
-        L.o = (long)it.n0 + 4 * t;
-        L.msk = 0;
-#pragma unroll
-        for (int i = 0; i < 4; i++) L.msk |= (4 * t + i < it.k0 ? 1u : 0u) << i;
-        L.vec = false;
-    } else {
-        const int n = it.n0 + (t >> 3), k = it.k0 + (t & 7) * 4;
-        L.o = (long)n * jb.K + k;
-        L.msk = 0;
-#pragma unroll
-        for (int i = 0; i < 4; i++) L.msk |= (n < jb.N && k + i < jb.K ? 1u : 0u) << i;
-        L.vec = L.msk == 15u && (jb.K & 3) == 0 &&
-                ((reinterpret_cast<uintptr_t>(jb.W) | reinterpret_cast<uintptr_t>(jb.Gm) |
-                  reinterpret_cast<uintptr_t>(jb.Mm) | reinterpret_cast<uintptr_t>(jb.Vm)) & 15) == 0;
-    }
-    return L;
-}
-__device__ __forceinline__ void upd_load(const UpdJob& jb, const UpdLane& L, float4& p, float4& g, float4& m, float4& v) {
-    if (L.vec) {
-        p = gld4(reinterpret_cast<const float4*>(jb.W + L.o));
-        g = gld4(reinterpret_cast<const float4*>(jb.Gm + L.o));
-        m = gld4(reinterpret_cast<const float4*>(jb.Mm + L.o));
-        v = gld4(reinterpret_cast<const float4*>(jb.Vm + L.o));
-    } else {
-        float* pp = &p.x; float* gg = &g.x; float* mm = &m.x; float* vv = &v.x;
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const bool on = (L.msk >> i) & 1u;
-            const long o = on ? L.o + i : 0;  // (a valid address either way)
-            pp[i] = gptr(jb.W)[o];
-            gg[i] = gptr(jb.Gm)[o];
-            mm[i] = gptr(jb.Mm)[o];
-            vv[i] = gptr(jb.Vm)[o];
-        }
-    }
-}
-template <int IPB>
-__global__ __launch_bounds__(256) void k_amp_update_p(const UpdJob* __restrict__ jobs, const UpdItem* __restrict__ items,
-                                                      const double* __restrict__ part, double* sq_out,
-                                                      const Scaler* __restrict__ sc, Scaler* __restrict__ sc_next,
-                                                      float max_norm, float lr, float wd, float b1, float b2, float eps,
-                                                      int n_upd, AmpDev d, float mp, uint64_t mseed, uint64_t mstep,
-                                                      int npart) {
-    __shared__ _Float16 Tl[32][40];
-    const int nub = (n_upd + IPB - 1) / IPB;
-    if ((int)blockIdx.x >= nub) {  // the next step's dropout draws (as k_amp_update's)
-        const int q4 = d.H / 4;
-        const long i = (long)(blockIdx.x - nub) * 256 + threadIdx.x;
-        if (i < (long)(1 + d.NB) * d.Bmax * q4) {
-            const int q = (int)(i % q4), row = (int)((i / q4) % d.Bmax), L = (int)(i / ((long)q4 * d.Bmax));
-            d.masks[((long)L * d.Bmax + row) * q4 + q] = (uint8_t)dropout_bits(mseed, L, mstep, (long)row * q4 + q, mp);
-        }
-        return;
-    }
-    const int t = threadIdx.x;
-    const int i0 = (int)blockIdx.x * IPB;
-    const int ni = min(IPB, n_upd - i0);
-    const double total = sq_total(part, npart);
-    const Scaler s0 = *sc;
-    if (blockIdx.x == 0 && t == 0) {
-        *sq_out = total;
-        Scaler n = s0;
-        if (!isfinite(total)) {
-            n.scale *= 0.5f;
-            n.tracker = 0;
-            n.found_inf = 1;
-        } else {
-            n.steps += 1;
-            n.found_inf = 0;
-            if (++n.tracker == n.growth_interval) {
-                n.scale *= 2.0f;
-                n.tracker = 0;
-            }
-        }
-        *sc_next = n;
-    }
-    const float inv = 1.0f / s0.scale;
-    if (!isfinite(total)) {  // skipped: G as torch leaves p.grad (k_amp_update)
-        float cf = max_norm / ((float)sqrt(total) + 1e-6f);
-        cf = cf > 1.0f ? 1.0f : cf;
-        for (int q = 0; q < ni; q++) {
-            const UpdItem it = items[i0 + q];
-            const UpdJob jb = jobs[it.job];
-            const UpdLane L = upd_lane(it, jb, t);
-            for (int i = 0; i < 4; i++)
-                if ((L.msk >> i) & 1u) gptr(jb.Gm)[L.o + i] = (gptr(jb.Gm)[L.o + i] * inv) * cf;
-        }
-        return;
-    }
-    const double st = (double)(s0.steps + 1);
-    const float step_size = (float)((double)lr / (1.0 - pow((double)b1, st)));
-    const float bc2_sqrt = (float)sqrt(1.0 - pow((double)b2, st));
-    const float norm = (float)sqrt(total);
-    float coef = max_norm / (norm + 1e-6f);
-    coef = coef > 1.0f ? 1.0f : coef;
-    const float decay = 1.0f - lr * wd;
-    UpdItem it = items[i0];
-    UpdJob jb = jobs[it.job];
-    UpdLane L = upd_lane(it, jb, t);
-    float4 p, g, m, v;
-    upd_load(jb, L, p, g, m, v);
-#pragma unroll 1
-    for (int q = 0; q < ni; q++) {
-        float* pp = &p.x; float* gg = &g.x; float* mm = &m.x; float* vv = &v.x;
-#pragma unroll
-        for (int i = 0; i < 4; i++) adamw_elem(pp[i], gg[i], mm[i], vv[i], inv, coef, decay, b1, b2, eps, step_size, bc2_sqrt);
-        if (L.vec) {
-            gst4(jb.W + L.o, p);
-            gst4(jb.Gm + L.o, g);
-            gst4(jb.Mm + L.o, m);
-            gst4(jb.Vm + L.o, v);
-        } else {
-#pragma unroll
-            for (int i = 0; i < 4; i++)
-                if ((L.msk >> i) & 1u) {
-                    gptr(jb.W)[L.o + i] = pp[i];
-                    gptr(jb.Gm)[L.o + i] = gg[i];
-                    gptr(jb.Mm)[L.o + i] = mm[i];
-                    gptr(jb.Vm)[L.o + i] = vv[i];
-                }
-        }
-        const bool mat = jb.dstN != nullptr;
-        if (mat) {
-            const int r = t >> 3, c = (t & 7) * 4;
-#pragma unroll
-            for (int i = 0; i < 4; i++) Tl[r][c + i] = f16_of_stored((L.msk >> i) & 1u ? pp[i] : 0.f);
-        }
-        const UpdItem itc = it;
-        const UpdJob jbc = jb;
-        if (q + 1 < ni) {  // the next item's loads, ahead of this one's repack
-            it = items[i0 + q + 1];
-            jb = jobs[it.job];
-            L = upd_lane(it, jb, t);
-            upd_load(jb, L, p, g, m, v);
-        }
-        if (mat) {  // (uniform: one job per item)
-            __syncthreads();
-            const int f = (t >> 6) & 1, l = t & 63;
-            half8 h;
-            if (t < 128) {
-                const int rr = 16 * f + (l & 15), kk = 8 * (l >> 4);
-#pragma unroll
-                for (int j = 0; j < 8; j++) h[j] = Tl[rr][kk + j];
-                gsth8(jbc.dstN + ((long)(itc.n0 / 16 + f) * (jbc.KpN / 32) + itc.k0 / 32) * 64 + l, h);
-            } else if (jbc.dstT) {
-                const int kk = 16 * f + (l & 15), rr = 8 * (l >> 4);
-#pragma unroll
-                for (int j = 0; j < 8; j++) h[j] = Tl[rr + j][kk];
-                gsth8(jbc.dstT + ((long)(itc.k0 / 16 + f) * (jbc.KpT / 32) + itc.n0 / 32) * 64 + l, h);
-            }
-            __syncthreads();  // (Tl is rewritten by the next item)
-        }
-    }
-}
-#endif
 }  // namespace
 
 // ------------------------------------------------------------------ host
@@ -2203,13 +2033,7 @@ int amp_apply(AmpTrain* a, long nparams, float* M, float* V, double* sq_out, flo
         YK_LAUNCHED();
     }
     const long nm = dropout > 0.f ? (long)(1 + a->NB) * a->Bmax * (a->H / 4) : 0;
-#if AMP_UPD_IPB > 1
-    hipLaunchKernelGGL(k_amp_update_p<AMP_UPD_IPB>,
-                       dim3((unsigned)((a->n_upd_items + AMP_UPD_IPB - 1) / AMP_UPD_IPB + (nm + 255) / 256)), dim3(256),
-                       0, s, a->upd_jobs,
-#else
     hipLaunchKernelGGL(k_amp_update, dim3((unsigned)(a->n_upd_items + (nm + 255) / 256)), dim3(256), 0, s, a->upd_jobs,
-#endif
                        a->upd_items, fused ? a->sq_items : a->sqpart, sq_out, a->sc, a->sc_next, max_norm, lr, wd, b1, b2, eps, a->n_upd_items,
                        a->d, dropout, seed, next_step, fused ? a->n_norm_dw + a->n_vs_items : SQ_BLOCKS);
     YK_LAUNCHED();
