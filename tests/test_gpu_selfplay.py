@@ -95,11 +95,14 @@ def test_selfplay_hash_prior_batch_vs_oracle(Y):
     assert eng.stats()["expansions"] == int(orc["stats"][:, 1].sum())
 
 
-def test_selfplay_net_prior_replayed_by_oracle(Y):
+@pytest.mark.parametrize("hidden,nblocks", [(256, 6), (256, 0), (64, 1)])
+def test_selfplay_net_prior_replayed_by_oracle(Y, hidden, nblocks):
+    """The engine's self-play with the net prior, replayed by the oracle from its recorded
+    predictions; nblocks 0 (no residual block: the forward's own instantiation) and hidden 64 too."""
     _, E, N = Y
     n, sims, seed, base = 6, 12, 77, 10
-    sd = spec.closed_form_weights(256, 6)
-    net = N.YkNet(sd, 256, 6)
+    sd = spec.closed_form_weights(hidden, nblocks)
+    net = N.YkNet(sd, hidden, nblocks)
     eng = E.SelfPlayEngine(n, sims, 1.5, 15, net=net, max_moves=64, record_predictions=True,
                            max_expansions=64 * sims)
     eng.run(seed, base)
@@ -113,7 +116,8 @@ def test_selfplay_net_prior_replayed_by_oracle(Y):
     _compare_to_oracle(rec, orc, n)
     # every recorded prediction (root and non-root expansions) is the f32 MLP within tolerance
     assert np.array_equal(leaves[:, 0], rec["states"][:, 0])  # the first expansion is the root
-    assert check_recorded_priors(pi, v, cnt, leaves, sd, net=net) == int(cnt.sum())
+    assert check_recorded_priors(pi, v, cnt, leaves, sd, hidden, nblocks, net=net) == int(cnt.sum())
+    assert net.errors() == 0
 
 
 def _first_divergence(a_moves, a_counts, b_moves, b_counts, n):
