@@ -95,10 +95,10 @@ def test_selfplay_hash_prior_batch_vs_oracle(Y):
     assert eng.stats()["expansions"] == int(orc["stats"][:, 1].sum())
 
 
-@pytest.mark.parametrize("hidden,nblocks", [(256, 6), (256, 0), (64, 1)])
+@pytest.mark.parametrize("hidden,nblocks", [(256, 6), (256, 0)])
 def test_selfplay_net_prior_replayed_by_oracle(Y, hidden, nblocks):
     """The engine's self-play with the net prior, replayed by the oracle from its recorded
-    predictions; nblocks 0 (no residual block: the forward's own instantiation) and hidden 64 too."""
+    predictions; also at nblocks 0 (no residual block: the forward's own instantiation)."""
     _, E, N = Y
     n, sims, seed, base = 6, 12, 77, 10
     sd = spec.closed_form_weights(hidden, nblocks)
