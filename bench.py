@@ -473,7 +473,8 @@ def spawn_ranks(nprocs, argv, timeout_s, script=None, out=None, err=None, poll_s
     `err` (stderr is inherited when `err` is sys.stderr).  The first child to fail (or the
     timeout) ends the job: the other ranks' process groups are terminated (then killed) and the
     return code is non-zero (the failing rank's code, 124 on timeout, 1 when rank 0 printed no
-    JSON line or more than one).  -> exit code."""
+    JSON line or more than one, 128 + the signal when this process is told to stop: the ranks then
+    stop too; a child also gets SIGTERM if this process dies, PR_SET_PDEATHSIG).  -> exit code."""
     import signal
     import subprocess
     import threading
@@ -499,14 +500,22 @@ def spawn_ranks(nprocs, argv, timeout_s, script=None, out=None, err=None, poll_s
                 err.flush()
         stream.close()
 
-    pumps = []
-    for r in range(nprocs):
+    def die_with_parent():  # (in the child, before exec: no GPU state exists yet)
+        try:
+            import ctypes
+            ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, signal.SIGTERM)  # PR_SET_PDEATHSIG
+        except OSError:
+            pass
+
+    for r in range(nprocs):  # every child first: preexec_fn runs while this process has no threads
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nprocs),
                    LOCAL_WORLD_SIZE=str(nprocs), GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
                    YK_SELF_SPAWNED="1")
-        p = subprocess.Popen([sys.executable, "-u", script] + list(argv), env=env, stdout=subprocess.PIPE,
-                             stderr=None if err is sys.stderr else subprocess.PIPE, start_new_session=True)
-        procs.append(p)
+        procs.append(subprocess.Popen([sys.executable, "-u", script] + list(argv), env=env, stdout=subprocess.PIPE,
+                                      stderr=None if err is sys.stderr else subprocess.PIPE, start_new_session=True,
+                                      preexec_fn=die_with_parent))
+    pumps = []
+    for r, p in enumerate(procs):
         for stream, kind in ((p.stdout, "out"), (p.stderr, "err")):
             if stream is not None:  # (stderr: inherited unless `err` is not this process's stderr)
                 t = threading.Thread(target=pump, args=(stream, r if kind == "out" else -1 - r), daemon=True)
@@ -525,9 +534,21 @@ def spawn_ranks(nprocs, argv, timeout_s, script=None, out=None, err=None, poll_s
             while any(p.poll() is None for p in live) and time.time() < t_end:
                 time.sleep(0.1)
 
+    # a launcher that is itself terminated (a driver's time limit) takes its ranks down with it
+    stopped = []
+
+    def on_signal(signum, frame):
+        stopped.append(signum)
+
+    old_handlers = {sg: signal.signal(sg, on_signal) for sg in (signal.SIGTERM, signal.SIGINT, signal.SIGHUP)}
     t0 = time.time()
     rc = 0
     while True:
+        if stopped:
+            err.write(f"spawn_ranks: signal {stopped[0]}; stopping every rank\n")
+            stop_all()
+            rc = 128 + stopped[0]
+            break
         codes = [p.poll() for p in procs]
         bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
         if bad:
@@ -544,6 +565,8 @@ def spawn_ranks(nprocs, argv, timeout_s, script=None, out=None, err=None, poll_s
             rc = 124
             break
         time.sleep(poll_s)
+    for sg, h in old_handlers.items():
+        signal.signal(sg, h)
     for t in pumps:
         t.join(timeout=5.0)
     if rc == 0 and len(lines) != 1:

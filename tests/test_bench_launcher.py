@@ -100,3 +100,43 @@ def test_bench_gpus2_without_launcher_fails_loudly_without_gpu():
     assert r.returncode != 0
     assert r.stdout.strip() == ""
     assert "spawn_ranks: rank" in r.stderr
+
+
+def test_terminated_launcher_stops_its_ranks(tmp_path):
+    """SIGTERM to the launcher (a driver's time limit) stops every rank, and the launcher exits
+    128 + 15; the ranks record their pids so the test can check none survives."""
+    body = f"""
+        import os, time
+        with open(os.path.join({str(tmp_path)!r}, "pid%s" % os.environ["RANK"]), "w") as fh:
+            fh.write(str(os.getpid()))
+        time.sleep(120)
+    """
+    script = _script(tmp_path, body)
+    runner = tmp_path / "launch.py"
+    runner.write_text(textwrap.dedent(f"""
+        import sys
+        sys.path.insert(0, {REPO!r})
+        import bench
+        sys.exit(bench.spawn_ranks(3, [], 100.0, script={script!r}))
+    """))
+    p = subprocess.Popen([sys.executable, str(runner)], stdout=subprocess.PIPE, stderr=subprocess.PIPE)
+    t0 = time.time()
+    while len(list(tmp_path.glob("pid*"))) < 3 and time.time() - t0 < 60:
+        time.sleep(0.1)
+    pids = [int((tmp_path / f"pid{r}").read_text()) for r in range(3)]
+    p.terminate()
+    rc = p.wait(timeout=60)
+    assert rc == 128 + 15
+    time.sleep(0.5)
+    def alive(pid):
+        try:
+            with open(f"/proc/{pid}/status") as fh:
+                state = [ln for ln in fh if ln.startswith("State:")][0]
+        except (FileNotFoundError, IndexError):
+            return False
+        return " Z " not in state and "zombie" not in state
+    for _ in range(50):
+        if not any(alive(pid) for pid in pids):
+            break
+        time.sleep(0.1)
+    assert not any(alive(pid) for pid in pids), "a rank survived its launcher"
