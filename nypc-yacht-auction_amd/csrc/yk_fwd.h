@@ -1004,6 +1004,11 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
     // order: workgroups reading the same weight lines together is faster than spreading them
     // (a per-workgroup rotation of the chunk order cost 0.5 us)
     const int m = cnt > wave ? (cnt - wave + NW - 1) / NW : 0;
+#ifdef FWD_HEAD_PRIO
+    // (A/B) the younger waves, which end their policy chunks ~7K cycles after the older ones, raised
+    // in the SIMDs' issue arbitration for the head
+    if (wave >= NW / 2) __builtin_amdgcn_s_setprio(FWD_HEAD_PRIO);
+#endif
     const int nf = m / PC, l = m % PC, nch = nf + (l ? 1 : 0);
 
     auto chunk_tiles = [&](int c, int (&tl)[PC]) {  // (the PC list reads unconditional: one LDS round trip)
