@@ -1004,11 +1004,6 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
     // order: workgroups reading the same weight lines together is faster than spreading them
     // (a per-workgroup rotation of the chunk order cost 0.5 us)
     const int m = cnt > wave ? (cnt - wave + NW - 1) / NW : 0;
-#ifdef FWD_HEAD_PRIO
-    // (A/B) the younger waves, which end their policy chunks ~7K cycles after the older ones, raised
-    // in the SIMDs' issue arbitration for the head
-    if (wave >= NW / 2) __builtin_amdgcn_s_setprio(FWD_HEAD_PRIO);
-#endif
     const int nf = m / PC, l = m % PC, nch = nf + (l ? 1 : 0);
 
     auto chunk_tiles = [&](int c, int (&tl)[PC]) {  // (the PC list reads unconditional: one LDS round trip)
@@ -1135,7 +1130,9 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
         // (reads of X stay after the count's: compiler fence; a timeout is flagged, reported at the
         // kernel's very end, where a global write adds no wait to any load in flight)
         __atomic_signal_fence(__ATOMIC_ACQUIRE);
+#ifndef FWD_NO_SYNC_FLAG
         if (lane == 0 && __hip_atomic_load(&VHC, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < NVW) SYNC_LOST = 1u;
+#endif
 #pragma unroll
         for (int rr = 0; rr < ROWS / 4; rr++) {
             const int r = wave * (ROWS / 4) + rr;
@@ -1195,7 +1192,9 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
     }
     // the last statement: a branch around a global atomic earlier would merge the wait counters of
     // its paths at the join and drain the policy ring's loads in flight (section 8-)
+#ifndef FWD_NO_SYNC_FLAG
     if (wave < 4 && lane == 0 && SYNC_LOST && net.err) atomicOr(net.err, FWD_ERR_SYNC);
+#endif
 }
 
 }  // namespace
