@@ -237,6 +237,11 @@ __device__ __forceinline__ void layernorm(float (&x)[VPL], const float* g, const
 // operation, as numpy does); the forward's LayerNorm row passes - VALU-bound and on every layer's
 // critical path - contract their multiply-adds into v_pk_fma_f32 (one rounding instead of two: no
 // less accurate than torch's own LayerNorm kernels, which fuse them too).  Scoped per function.
+#ifndef FWD_SYNC_MODE
+// (A/B) how a timed-out value-head wait is reported: 0 not at all, 1 LDS flag from a re-read of the
+// count + the net's error word at the end, 2 NaN v for the tile, 3 LDS flag from the loop count + error word
+#define FWD_SYNC_MODE 1
+#endif
 #define YK_ROW_CONTRACT _Pragma("clang fp contract(fast)")
 typedef float f2v __attribute__((ext_vector_type(2)));
 typedef _Float16 h2v __attribute__((ext_vector_type(2)));
@@ -1124,14 +1129,18 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
         // the grid; yk_net_errors / the engine's ERR_FWD_SYNC report it)
         // (a relaxed atomic load is a ds_read; a volatile access through the generic pointer was a
         // flat load, whose wait also drained the wave's logit stores)
-        for (int it = 0; it < (1 << 20) && __hip_atomic_load(&VHC, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < NVW;
-             it++)
+        int it = 0;
+        for (; it < (1 << 20) && __hip_atomic_load(&VHC, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < NVW; it++)
             __builtin_amdgcn_s_sleep(1);
         // (reads of X stay after the count's: compiler fence; a timeout is flagged, reported at the
         // kernel's very end, where a global write adds no wait to any load in flight)
         __atomic_signal_fence(__ATOMIC_ACQUIRE);
-#ifndef FWD_NO_SYNC_FLAG
+        const bool lost = it >= (1 << 20);  // (wave-uniform)
+        (void)lost;
+#if FWD_SYNC_MODE == 1
         if (lane == 0 && __hip_atomic_load(&VHC, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < NVW) SYNC_LOST = 1u;
+#elif FWD_SYNC_MODE == 3
+        if (lost && lane == 0) SYNC_LOST = 1u;
 #endif
 #pragma unroll
         for (int rr = 0; rr < ROWS / 4; rr++) {
@@ -1140,7 +1149,12 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
             const float* wv2 = VS + VS_BV1 * H + 128;
             float s = silu(X[r * LD + 2 * lane]) * wv2[2 * lane] + silu(X[r * LD + 2 * lane + 1]) * wv2[2 * lane + 1];
             s = wave_sum(s);
-            if (lane == 0 && part == 0 && row < n && ((amask >> r) & 1u)) vout[row] = tanhf(s + bv2);  // active rows only
+#if FWD_SYNC_MODE == 2
+            const float vv = lost ? __builtin_nanf("") : tanhf(s + bv2);  // (a timed-out hand-off: NaN, never stale)
+#else
+            const float vv = tanhf(s + bv2);
+#endif
+            if (lane == 0 && part == 0 && row < n && ((amask >> r) & 1u)) vout[row] = vv;  // active rows only
         }
     }
     // softmax statistics of the policy logits per row: over the 16 column lanes, then the waves
@@ -1192,7 +1206,7 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
     }
     // the last statement: a branch around a global atomic earlier would merge the wait counters of
     // its paths at the join and drain the policy ring's loads in flight (section 8-)
-#ifndef FWD_NO_SYNC_FLAG
+#if FWD_SYNC_MODE == 1 || FWD_SYNC_MODE == 3
     if (wave < 4 && lane == 0 && SYNC_LOST && net.err) atomicOr(net.err, FWD_ERR_SYNC);
 #endif
 }
