@@ -239,7 +239,8 @@ __device__ __forceinline__ void layernorm(float (&x)[VPL], const float* g, const
 // less accurate than torch's own LayerNorm kernels, which fuse them too).  Scoped per function.
 #ifndef FWD_SYNC_MODE
 // (A/B) how a timed-out value-head wait is reported: 0 not at all, 1 LDS flag from a re-read of the
-// count + the net's error word at the end, 2 NaN v for the tile, 3 LDS flag from the loop count + error word
+// count + the net's error word at the end, 2 NaN v for the tile, 3 LDS flag from the loop count + error word,
+// 4 the error word written right after the wait (loop count)
 #define FWD_SYNC_MODE 1
 #endif
 #define YK_ROW_CONTRACT _Pragma("clang fp contract(fast)")
@@ -1141,6 +1142,9 @@ __device__ __forceinline__ void forward_tile(NetDev net, const yk_state_t* __res
         if (lane == 0 && __hip_atomic_load(&VHC, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < NVW) SYNC_LOST = 1u;
 #elif FWD_SYNC_MODE == 3
         if (lost && lane == 0) SYNC_LOST = 1u;
+#elif FWD_SYNC_MODE == 4
+        // (here, in the older waves' slack before the end: only their own logit stores are in flight)
+        if (lost && lane == 0 && net.err) atomicOr(net.err, FWD_ERR_SYNC);
 #endif
 #pragma unroll
         for (int rr = 0; rr < ROWS / 4; rr++) {
